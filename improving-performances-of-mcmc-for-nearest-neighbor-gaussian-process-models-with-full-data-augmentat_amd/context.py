@@ -1,0 +1,162 @@
+"""One device context per MCMC chain (replaces the per-chain ``mclapply``
+worker of Scripts/mcmc_nngp_update_Gaussian.R:25 -- HIP is not fork-safe, so
+chains are contexts, possibly on different devices, not forked processes).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import COVFUNS, Info, check, colmajor, f64, i32, lib
+
+
+class ChainContext:
+    """Device-resident state of one chain: locations, NNarray, colouring,
+    observations, the current/proposal Vecchia factors, the latent field."""
+
+    def __init__(self, locs, NNarray, coloring, locs_match, observed_field, device: int = -1):
+        locs = np.asarray(locs, np.float64)
+        if locs.ndim == 1:
+            locs = locs[:, None]
+        NNarray = np.asarray(NNarray, np.int32)
+        n, d = locs.shape
+        b = NNarray.shape[1]
+        self.n, self.d, self.b = n, d, b
+        self.n_obs = len(observed_field)
+        h = C.c_void_p()
+        check(lib.nngp_ctx_create(colmajor(locs, np.float64), n, d, colmajor(NNarray, np.int32), b,
+                                  i32(coloring), i32(locs_match), f64(observed_field), self.n_obs,
+                                  int(device), C.byref(h)))
+        self._h = h
+
+    # ------------------------------------------------------------ lifetime
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib.nngp_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _chk(self, status):
+        check(status, self._h)
+
+    @property
+    def info(self) -> dict:
+        inf = Info()
+        self._chk(lib.nngp_ctx_info(self._h, C.byref(inf)))
+        return {k: getattr(inf, k) for k, _ in Info._fields_}
+
+    # ------------------------------------------------------------ factor (A4/A5)
+    def factor(self, which: int, covfun: str, covparms) -> None:
+        cp = f64(covparms)
+        self._chk(lib.nngp_factor(self._h, which, COVFUNS[covfun], cp, len(cp)))
+
+    def get_linv(self, which: int = 0) -> np.ndarray:
+        out = np.zeros(self.n * self.b)
+        self._chk(lib.nngp_get_linv(self._h, which, out))
+        return out.reshape(self.b, self.n).T.copy()
+
+    def set_linv(self, which: int, Linv) -> None:
+        self._chk(lib.nngp_set_linv(self._h, which, colmajor(Linv, np.float64)))
+
+    def accept_factor(self) -> None:
+        self._chk(lib.nngp_accept_factor(self._h))
+
+    def precision_diag(self) -> np.ndarray:
+        out = np.zeros(self.n)
+        self._chk(lib.nngp_get_precision_diag(self._h, out))
+        return out
+
+    # ------------------------------------------------------------ state
+    def set_field(self, field) -> None:
+        self._chk(lib.nngp_set_field(self._h, f64(field)))
+
+    def get_field(self) -> np.ndarray:
+        out = np.zeros(self.n)
+        self._chk(lib.nngp_get_field(self._h, out))
+        return out
+
+    def set_mu(self, mu, beta0: float) -> None:
+        """mu = None means mu == beta_0 for every observation (no X)."""
+        self._mu_keep = None if mu is None else f64(mu)
+        ptr = None if mu is None else self._mu_keep.ctypes.data
+        self._chk(lib.nngp_set_mu(self._h, ptr, float(beta0)))
+
+    # ------------------------------------------------------------ kernels
+    def loglik(self, which: int, beta0: float, log_scale: float) -> float:
+        out = C.c_double()
+        self._chk(lib.nngp_loglik(self._h, which, float(beta0), float(log_scale), C.byref(out)))
+        return out.value
+
+    def sweep(self, n_sweeps: int, beta0: float, log_scale: float, log_noise_variance: float,
+              seed: int, counter_base: int, z=None) -> None:
+        zp = None
+        if z is not None:
+            z = np.ascontiguousarray(np.atleast_2d(z), np.float64)
+            assert z.shape == (n_sweeps, self.n)
+            zp = z.ctypes.data
+        self._chk(lib.nngp_sweep(self._h, int(n_sweeps), float(beta0), float(log_scale),
+                                 float(log_noise_variance), int(seed) & (2 ** 64 - 1),
+                                 int(counter_base) & (2 ** 64 - 1), zp))
+
+    def sweep_timed(self, n_sweeps, beta0, log_scale, log_noise_variance, seed, counter_base,
+                    per_kernel: bool = False):
+        ms = C.c_double()
+        kms = C.c_double()
+        self._chk(lib.nngp_sweep_timed(self._h, int(n_sweeps), float(beta0), float(log_scale),
+                                       float(log_noise_variance), int(seed), int(counter_base),
+                                       C.byref(ms), C.byref(kms) if per_kernel else None))
+        return ms.value, (kms.value if per_kernel else None)
+
+    def ancillary_propose(self, beta0: float, dlog_scale: float) -> None:
+        self._chk(lib.nngp_ancillary_propose(self._h, float(beta0), float(dlog_scale)))
+
+    def field_response_ratio(self, beta0: float, log_noise_variance: float) -> float:
+        out = C.c_double()
+        self._chk(lib.nngp_field_response_ratio(self._h, float(beta0), float(log_noise_variance),
+                                                C.byref(out)))
+        return out.value
+
+    def accept_field(self) -> None:
+        self._chk(lib.nngp_accept_field(self._h))
+
+    def beta0_stats(self):
+        a, b = C.c_double(), C.c_double()
+        self._chk(lib.nngp_beta0_stats(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def sum_squared_residuals(self, beta0: float) -> float:
+        out = C.c_double()
+        self._chk(lib.nngp_sum_squared_residuals(self._h, float(beta0), C.byref(out)))
+        return out.value
+
+    def spmv(self, which: int, X) -> np.ndarray:
+        X = np.asarray(X, np.float64)
+        vec = X.ndim == 1
+        X2 = X[:, None] if vec else X
+        out = np.zeros(X2.shape[0] * X2.shape[1])
+        self._chk(lib.nngp_spmv(self._h, which, colmajor(X2, np.float64), X2.shape[1], out))
+        Y = out.reshape(X2.shape[1], X2.shape[0]).T
+        return Y[:, 0].copy() if vec else Y.copy()
+
+    def tri_solve(self, which: int, u) -> np.ndarray:
+        out = np.zeros(self.n)
+        self._chk(lib.nngp_tri_solve(self._h, which, f64(u), out))
+        return out
+
+
+def device_normals(seed: int, sweep: int, n: int, device: int = 0) -> np.ndarray:
+    out = np.zeros(n)
+    check(lib.nngp_device_normals(device, seed, sweep, n, out))
+    return out

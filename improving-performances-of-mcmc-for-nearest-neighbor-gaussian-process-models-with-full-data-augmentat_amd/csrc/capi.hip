@@ -1,0 +1,803 @@
+// C ABI (include/nngp.h) of the MI355X-native NNGP chromatic-Gibbs hot path.
+// One nngp_ctx per MCMC chain: device buffers, the sweep layout planned on the
+// host (graph_prep.cpp), one HIP stream, and cached hipGraphs of the sweep.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/nngp.h"
+#include "graph_prep.h"
+#include "kernels.h"
+
+using namespace nngp;
+
+struct nngp_ctx {
+  int device = 0;
+  hipStream_t st = nullptr;
+  int n = 0, d = 0, b = 0, n_obs = 0, ds = 2;
+  std::string err;
+  SweepLayout lay;
+  std::vector<int> level_ptr, level_rows;
+  // device buffers
+  double* locs_d = nullptr;  // n x d row-major
+  double* sc_d = nullptr;    // n x ds scaled coordinates
+  int* nn_d = nullptr;       // n x b row-major, 0-based, -1 = NA
+  double* linv_d[2] = {nullptr, nullptr};
+  int* fail_d = nullptr;
+  int* chunk_slot0_d = nullptr;
+  int* chunk_len_d = nullptr;
+  long long* chunk_off_d = nullptr;
+  int* collen_d = nullptr;
+  int* slot_loc_d = nullptr;
+  int* rpos_d = nullptr;
+  int* ent_rowpos_d = nullptr;
+  int* ent_src_d = nullptr;
+  double* ent_val_d = nullptr;
+  double* D_slot_d = nullptr;
+  double* R_slot_d = nullptr;
+  int* nobs_slot_d = nullptr;
+  double* w_slot_d = nullptr;
+  double* r_d = nullptr;
+  int* level_rows_d = nullptr;
+  int* obs_ptr_d = nullptr;
+  int* obs_idx_d = nullptr;
+  int* lm_d = nullptr;  // locs_match, 0-based
+  double* y_d = nullptr;
+  double* mu_d = nullptr;
+  double* field_d = nullptr;
+  double* field_prop_d = nullptr;
+  double* tmp_d = nullptr;
+  double* tmp2_d = nullptr;
+  double* partials_d = nullptr;
+  double* res_d = nullptr;
+  double* z_d = nullptr;
+  size_t z_cap = 0;
+  SweepScalars* scal_d = nullptr;
+  SweepScalars* scal_h = nullptr;  // pinned
+  double* res_h = nullptr;         // pinned, 8 doubles
+  bool have_factor[2] = {false, false};
+  bool have_field = false, have_mu = false, mu_is_const = true;
+  double mu_beta0 = 0.0;
+  std::map<int, hipGraphExec_t> graphs;
+  std::vector<hipGraph_t> graph_objs;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail_hip(nngp_ctx* c, hipError_t e, const char* what) {
+  std::string m = std::string(what) + ": " + hipGetErrorString(e);
+  if (c) c->err = m;
+  g_err = m;
+  return NNGP_ERR_HIP;
+}
+int fail_msg(nngp_ctx* c, int code, const std::string& m) {
+  if (c) c->err = m;
+  g_err = m;
+  return code;
+}
+
+#define HIPCHK(c, x)                                       \
+  do {                                                     \
+    hipError_t e_ = (x);                                   \
+    if (e_ != hipSuccess) return fail_hip((c), e_, #x);    \
+  } while (0)
+
+template <typename T>
+hipError_t dalloc(T** p, size_t count) {
+  if (count == 0) count = 1;
+  return hipMalloc((void**)p, sizeof(T) * count);
+}
+template <typename T>
+hipError_t upload(T* dst, const T* src, size_t count, hipStream_t st) {
+  if (count == 0) return hipSuccess;
+  return hipMemcpyAsync(dst, src, sizeof(T) * count, hipMemcpyHostToDevice, st);
+}
+
+int set_device(nngp_ctx* c) {
+  hipError_t e = hipSetDevice(c->device);
+  if (e != hipSuccess) return fail_hip(c, e, "hipSetDevice");
+  return NNGP_OK;
+}
+
+// sweep-layout pointers
+SweepDev sweep_dev(nngp_ctx* c) {
+  SweepDev L;
+  L.chunk_slot0 = c->chunk_slot0_d;
+  L.chunk_len = c->chunk_len_d;
+  L.chunk_off = c->chunk_off_d;
+  L.collen = c->collen_d;
+  L.slot_loc = c->slot_loc_d;
+  L.ent_val = c->ent_val_d;
+  L.ent_rowpos = c->ent_rowpos_d;
+  L.D_slot = c->D_slot_d;
+  L.R_slot = c->R_slot_d;
+  L.nobs_slot = c->nobs_slot_d;
+  L.w_slot = c->w_slot_d;
+  L.r = c->r_d;
+  return L;
+}
+
+int refresh_sweep_values(nngp_ctx* c) {
+  HIPCHK(c, launch_sell_refresh(c->st, c->chunk_slot0_d, c->chunk_off_d, c->lay.nchunks, nullptr,
+                                c->collen_d, c->n, c->ent_src_d, c->linv_d[0], c->ent_val_d,
+                                c->D_slot_d));
+  return NNGP_OK;
+}
+
+// reduce partials to res_d and copy 4 doubles to the host (synchronises)
+int fetch4(nngp_ctx* c, int nblocks, double out[4]) {
+  HIPCHK(c, launch_reduce4(c->st, c->partials_d, nblocks, c->res_d));
+  HIPCHK(c, hipMemcpyAsync(c->res_h, c->res_d, 4 * sizeof(double), hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  for (int k = 0; k < 4; ++k) out[k] = c->res_h[k];
+  return NNGP_OK;
+}
+
+}  // namespace
+
+// ====================================================================== ABI
+extern "C" {
+
+int nngp_abi_version(void) { return NNGP_ABI_VERSION; }
+
+const char* nngp_status_string(int s) {
+  switch (s) {
+    case NNGP_OK: return "ok";
+    case NNGP_ERR_ARG: return "invalid argument";
+    case NNGP_ERR_HIP: return "HIP runtime error";
+    case NNGP_ERR_CHOL: return "local covariance not positive definite";
+    case NNGP_ERR_STATE: return "call out of order";
+    case NNGP_ERR_NOMEM: return "allocation failed";
+    case NNGP_ERR_NODEV: return "no HIP device";
+    case NNGP_ERR_COMM: return "RCCL error";
+  }
+  return "unknown status";
+}
+
+// ---------------------------------------------------------------- host prep
+int nngp_order_maxmin(const double* locs, int n, int d, int* order) {
+  if (!locs || !order || n < 1 || d < 1) return fail_msg(nullptr, NNGP_ERR_ARG, "order_maxmin: bad args");
+  std::vector<int> o;
+  try { order_maxmin(locs, n, d, o); } catch (std::bad_alloc&) { return NNGP_ERR_NOMEM; }
+  for (int i = 0; i < n; ++i) order[i] = o[i] + 1;
+  return NNGP_OK;
+}
+
+int nngp_find_ordered_nn(const double* locs, int n, int d, int m, int* NNarray) {
+  if (!locs || !NNarray || n < 1 || d < 1 || m < 0) return fail_msg(nullptr, NNGP_ERR_ARG, "find_ordered_nn: bad args");
+  std::vector<int> nn;
+  try { find_ordered_nn(locs, n, d, m, nn); } catch (std::bad_alloc&) { return NNGP_ERR_NOMEM; }
+  const int b = m + 1;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < b; ++j) {
+      int v = nn[(size_t)i * b + j];
+      NNarray[i + (size_t)j * n] = v < 0 ? INT_MIN : v + 1;
+    }
+  return NNGP_OK;
+}
+
+static bool nn_to_rowmajor(const int* NNarray, int n, int b, std::vector<int>& nn, std::string& err) {
+  nn.resize((size_t)n * b);
+  for (int i = 0; i < n; ++i) {
+    for (int j = 0; j < b; ++j) {
+      int v = NNarray[i + (size_t)j * n];
+      if (v == INT_MIN) { nn[(size_t)i * b + j] = -1; continue; }
+      if (v < 1 || v > n) { err = "NNarray entry out of range"; return false; }
+      if (j == 0 && v != i + 1) { err = "NNarray[, 1] must be 1..n"; return false; }
+      if (j > 0 && v - 1 >= i) { err = "NNarray neighbours must precede the row (ordered NN)"; return false; }
+      nn[(size_t)i * b + j] = v - 1;
+    }
+  }
+  return true;
+}
+
+int nngp_greedy_coloring(const int* NNarray, int n, int b, int* coloring, int* n_colors) {
+  if (!NNarray || !coloring || n < 1 || b < 1) return fail_msg(nullptr, NNGP_ERR_ARG, "greedy_coloring: bad args");
+  std::vector<int> nn, col;
+  std::string err;
+  if (!nn_to_rowmajor(NNarray, n, b, nn, err)) return fail_msg(nullptr, NNGP_ERR_ARG, err);
+  int K = greedy_coloring(nn.data(), n, b, col);
+  std::memcpy(coloring, col.data(), sizeof(int) * n);
+  if (n_colors) *n_colors = K;
+  return NNGP_OK;
+}
+
+// ---------------------------------------------------------------- context
+void nngp_ctx_destroy(nngp_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->st) hipStreamSynchronize(c->st);
+  for (auto& kv : c->graphs) hipGraphExecDestroy(kv.second);
+  for (auto g : c->graph_objs) hipGraphDestroy(g);
+  void* ptrs[] = {c->locs_d, c->sc_d, c->nn_d, c->linv_d[0], c->linv_d[1], c->fail_d,
+                  c->chunk_slot0_d, c->chunk_len_d, c->chunk_off_d, c->collen_d, c->slot_loc_d,
+                  c->rpos_d, c->ent_rowpos_d, c->ent_src_d, c->ent_val_d, c->D_slot_d, c->R_slot_d,
+                  c->nobs_slot_d, c->w_slot_d, c->r_d, c->level_rows_d, c->obs_ptr_d, c->obs_idx_d,
+                  c->lm_d, c->y_d, c->mu_d, c->field_d, c->field_prop_d, c->tmp_d, c->tmp2_d,
+                  c->partials_d, c->res_d, c->z_d, c->scal_d};
+  for (void* p : ptrs) if (p) hipFree(p);
+  if (c->scal_h) hipHostFree(c->scal_h);
+  if (c->res_h) hipHostFree(c->res_h);
+  if (c->st) hipStreamDestroy(c->st);
+  delete c;
+}
+
+const char* nngp_ctx_last_error(const nngp_ctx* c) { return c ? c->err.c_str() : g_err.c_str(); }
+
+int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b, const int* coloring,
+                    const int* locs_match, const double* observed_field, int n_obs, int device,
+                    nngp_ctx** out) {
+  if (!out) return fail_msg(nullptr, NNGP_ERR_ARG, "ctx_create: out == NULL");
+  *out = nullptr;
+  if (!locs || !NNarray || !coloring || !locs_match || !observed_field || n < 1 || d < 1 || d > 4 ||
+      b < 1 || b > 32 || n_obs < 1)
+    return fail_msg(nullptr, NNGP_ERR_ARG, "ctx_create: bad arguments (need n>=1, 1<=d<=4, 1<=b<=32, n_obs>=1)");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail_msg(nullptr, NNGP_ERR_NODEV, "no HIP device");
+  nngp_ctx* c = new (std::nothrow) nngp_ctx();
+  if (!c) return NNGP_ERR_NOMEM;
+  if (device < 0) { if (hipGetDevice(&device) != hipSuccess) device = 0; }
+  if (device >= ndev) { delete c; return fail_msg(nullptr, NNGP_ERR_ARG, "device ordinal out of range"); }
+  c->device = device;
+  c->n = n; c->d = d; c->b = b; c->n_obs = n_obs;
+  c->ds = d <= 2 ? 2 : (d == 3 ? 3 : 4);
+  int rc;
+  std::vector<int> nn;
+  std::string err;
+  if (!nn_to_rowmajor(NNarray, n, b, nn, err)) { int e = fail_msg(nullptr, NNGP_ERR_ARG, err); delete c; return e; }
+  for (int i = 0; i < n; ++i)
+    if (coloring[i] < 1) { delete c; return fail_msg(nullptr, NNGP_ERR_ARG, "coloring must be >= 1"); }
+  // validate colouring: no two members of a Vecchia row share a colour
+  for (int k = 0; k < n; ++k)
+    for (int j = 0; j < b; ++j) {
+      int a = nn[(size_t)k * b + j];
+      if (a < 0) continue;
+      for (int q = j + 1; q < b; ++q) {
+        int e2 = nn[(size_t)k * b + q];
+        if (e2 >= 0 && coloring[a] == coloring[e2]) {
+          delete c;
+          return fail_msg(nullptr, NNGP_ERR_ARG, "coloring is not a proper colouring of the moral graph");
+        }
+      }
+    }
+  std::vector<int> lm0(n_obs), obs_cnt(n + 1, 0);
+  for (int o = 0; o < n_obs; ++o) {
+    if (locs_match[o] < 1 || locs_match[o] > n) { delete c; return fail_msg(nullptr, NNGP_ERR_ARG, "locs_match out of range"); }
+    lm0[o] = locs_match[o] - 1;
+    obs_cnt[lm0[o] + 1]++;
+  }
+  for (int i = 0; i < n; ++i) obs_cnt[i + 1] += obs_cnt[i];
+  std::vector<int> obs_idx(n_obs);
+  {
+    std::vector<int> f(obs_cnt.begin(), obs_cnt.end() - 1);
+    for (int o = 0; o < n_obs; ++o) obs_idx[f[lm0[o]]++] = o;
+  }
+  if (!build_sweep_layout(nn.data(), n, b, coloring, locs, d, c->lay, err)) {
+    delete c;
+    return fail_msg(nullptr, NNGP_ERR_ARG, err);
+  }
+  dag_levels(nn.data(), n, b, c->level_ptr, c->level_rows);
+  std::vector<int> nobs_slot(n);
+  for (int s = 0; s < n; ++s) { int i = c->lay.slot_loc[s]; nobs_slot[s] = obs_cnt[i + 1] - obs_cnt[i]; }
+  std::vector<double> locs_rm((size_t)n * d);
+  for (int i = 0; i < n; ++i)
+    for (int k = 0; k < d; ++k) locs_rm[(size_t)i * d + k] = locs[i + (size_t)k * n];
+
+  if ((rc = set_device(c))) { delete c; return rc; }
+#define CK(x)                                                     \
+  do {                                                            \
+    hipError_t e_ = (x);                                          \
+    if (e_ != hipSuccess) {                                       \
+      int r_ = fail_hip(nullptr, e_, #x);                         \
+      nngp_ctx_destroy(c);                                        \
+      return r_;                                                  \
+    }                                                             \
+  } while (0)
+  CK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+  const SweepLayout& L = c->lay;
+  CK(dalloc(&c->locs_d, (size_t)n * d));
+  CK(dalloc(&c->sc_d, (size_t)n * c->ds));
+  CK(dalloc(&c->nn_d, (size_t)n * b));
+  CK(dalloc(&c->linv_d[0], (size_t)n * b));
+  CK(dalloc(&c->linv_d[1], (size_t)n * b));
+  CK(dalloc(&c->fail_d, 1));
+  CK(dalloc(&c->chunk_slot0_d, L.nchunks));
+  CK(dalloc(&c->chunk_len_d, L.nchunks));
+  CK(dalloc(&c->chunk_off_d, (size_t)L.nchunks + 1));
+  CK(dalloc(&c->collen_d, n));
+  CK(dalloc(&c->slot_loc_d, n));
+  CK(dalloc(&c->rpos_d, n));
+  CK(dalloc(&c->ent_rowpos_d, (size_t)L.n_entries));
+  CK(dalloc(&c->ent_src_d, (size_t)L.n_entries));
+  CK(dalloc(&c->ent_val_d, (size_t)L.n_entries));
+  CK(dalloc(&c->D_slot_d, n));
+  CK(dalloc(&c->R_slot_d, n));
+  CK(dalloc(&c->nobs_slot_d, n));
+  CK(dalloc(&c->w_slot_d, n));
+  CK(dalloc(&c->r_d, n));
+  CK(dalloc(&c->level_rows_d, n));
+  CK(dalloc(&c->obs_ptr_d, (size_t)n + 1));
+  CK(dalloc(&c->obs_idx_d, n_obs));
+  CK(dalloc(&c->lm_d, n_obs));
+  CK(dalloc(&c->y_d, n_obs));
+  CK(dalloc(&c->mu_d, n_obs));
+  CK(dalloc(&c->field_d, n));
+  CK(dalloc(&c->field_prop_d, n));
+  CK(dalloc(&c->tmp_d, n));
+  CK(dalloc(&c->tmp2_d, n));
+  CK(dalloc(&c->partials_d, 4 * kRedBlocks));
+  CK(dalloc(&c->res_d, 8));
+  CK(dalloc(&c->scal_d, 1));
+  CK(hipHostMalloc((void**)&c->scal_h, sizeof(SweepScalars), hipHostMallocDefault));
+  CK(hipHostMalloc((void**)&c->res_h, 8 * sizeof(double), hipHostMallocDefault));
+  CK(upload(c->locs_d, locs_rm.data(), locs_rm.size(), c->st));
+  CK(upload(c->nn_d, nn.data(), nn.size(), c->st));
+  CK(upload(c->chunk_slot0_d, L.chunk_slot0.data(), L.nchunks, c->st));
+  CK(upload(c->chunk_len_d, L.chunk_len.data(), L.nchunks, c->st));
+  CK(upload(c->chunk_off_d, L.chunk_off.data(), (size_t)L.nchunks + 1, c->st));
+  CK(upload(c->collen_d, L.collen.data(), n, c->st));
+  CK(upload(c->slot_loc_d, L.slot_loc.data(), n, c->st));
+  CK(upload(c->rpos_d, L.rpos.data(), n, c->st));
+  CK(upload(c->ent_rowpos_d, L.ent_rowpos.data(), (size_t)L.n_entries, c->st));
+  CK(upload(c->ent_src_d, L.ent_src.data(), (size_t)L.n_entries, c->st));
+  CK(hipMemsetAsync(c->ent_val_d, 0, sizeof(double) * std::max<long long>(1, L.n_entries), c->st));
+  CK(upload(c->nobs_slot_d, nobs_slot.data(), n, c->st));
+  CK(upload(c->level_rows_d, c->level_rows.data(), n, c->st));
+  CK(upload(c->obs_ptr_d, obs_cnt.data(), (size_t)n + 1, c->st));
+  CK(upload(c->obs_idx_d, obs_idx.data(), n_obs, c->st));
+  CK(upload(c->lm_d, lm0.data(), n_obs, c->st));
+  CK(upload(c->y_d, observed_field, n_obs, c->st));
+  CK(hipStreamSynchronize(c->st));
+#undef CK
+  *out = c;
+  return NNGP_OK;
+}
+
+int nngp_ctx_info(const nngp_ctx* c, nngp_info* info) {
+  if (!c || !info) return NNGP_ERR_ARG;
+  info->n = c->n; info->b = c->b; info->d = c->d; info->n_obs = c->n_obs;
+  info->n_colors = c->lay.K;
+  info->n_levels = (int)c->level_ptr.size() - 1;
+  info->nnz = c->lay.nnz;
+  info->n_entries = c->lay.n_entries;
+  info->max_collen = c->lay.max_collen;
+  info->device = c->device;
+  return NNGP_OK;
+}
+
+// ---------------------------------------------------------------- factor
+static int covfun_family(int covfun, int d, const double* cp, int ncp, double* var, double* nug,
+                         double* nu, std::string& err) {
+  int need = 0, fam = 0;
+  switch (covfun) {
+    case NNGP_EXPONENTIAL_ISOTROPIC: case NNGP_EXPONENTIAL_SPHERE: need = 3; fam = 0; break;
+    case NNGP_MATERN15_ISOTROPIC: need = 3; fam = 1; break;
+    case NNGP_EXPONENTIAL_SCALEDIM: need = d + 2; fam = 0; break;
+    case NNGP_EXPONENTIAL_SPACETIME: need = 4; fam = 0; break;
+    case NNGP_MATERN_ISOTROPIC: case NNGP_MATERN_SPHERE: need = 4; fam = 2; break;
+    case NNGP_MATERN_SCALEDIM: need = d + 3; fam = 2; break;
+    case NNGP_MATERN_SPACETIME: need = 5; fam = 2; break;
+    default: err = "unknown covfun"; return -1;
+  }
+  if (ncp != need) { err = "covparms has the wrong length for this covfun"; return -1; }
+  if ((covfun == NNGP_EXPONENTIAL_SPHERE || covfun == NNGP_MATERN_SPHERE) && d != 2) { err = "sphere covfuns need d == 2 (lon, lat)"; return -1; }
+  if ((covfun == NNGP_EXPONENTIAL_SPACETIME || covfun == NNGP_MATERN_SPACETIME) && d < 2) { err = "spacetime covfuns need d >= 2"; return -1; }
+  for (int k = 0; k < ncp; ++k)
+    if (!std::isfinite(cp[k])) { err = "non-finite covparms"; return -1; }
+  *var = cp[0];
+  *nug = cp[ncp - 1];
+  *nu = 0.0;
+  if (fam == 2) *nu = cp[ncp - 2];
+  if (!(*var > 0)) { err = "variance must be > 0"; return -1; }
+  for (int k = 1; k < ncp - 1 - (fam == 2 ? 1 : 0); ++k)
+    if (!(cp[k] > 0)) { err = "ranges must be > 0"; return -1; }
+  if (fam == 2 && !(*nu > 0)) { err = "smoothness must be > 0"; return -1; }
+  return fam;
+}
+
+int nngp_factor(nngp_ctx* c, int which, int covfun, const double* cp, int ncp) {
+  if (!c || (which != 0 && which != 1) || !cp) return fail_msg(c, NNGP_ERR_ARG, "factor: bad args");
+  double var, nug, nu;
+  std::string err;
+  int fam = covfun_family(covfun, c->d, cp, ncp, &var, &nug, &nu, err);
+  if (fam < 0) return fail_msg(c, NNGP_ERR_ARG, err);
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  const int ds = (covfun == NNGP_EXPONENTIAL_SPHERE || covfun == NNGP_MATERN_SPHERE) ? 3 : c->ds;
+  if (ds > c->ds) {
+    // sphere on d == 2: scaled coordinates are 3-D; grow the buffer once
+    hipFree(c->sc_d);
+    c->sc_d = nullptr;
+    HIPCHK(c, dalloc(&c->sc_d, (size_t)c->n * 4));
+    c->ds = 4;  // capacity marker
+  }
+  const int use_ds = (covfun == NNGP_EXPONENTIAL_SPHERE || covfun == NNGP_MATERN_SPHERE) ? 3 : (c->d <= 2 ? 2 : (c->d == 3 ? 3 : 4));
+  HIPCHK(c, launch_scale_coords(c->st, covfun, cp, ncp, c->locs_d, c->n, c->d, c->sc_d, use_ds));
+  const int big = INT_MAX;
+  HIPCHK(c, hipMemcpyAsync(c->fail_d, &big, sizeof(int), hipMemcpyHostToDevice, c->st));
+  HIPCHK(c, launch_factor(c->st, fam, var, nug, nu, c->sc_d, use_ds, c->nn_d, c->n, c->b, c->linv_d[which], c->fail_d));
+  int fail = 0;
+  HIPCHK(c, hipMemcpyAsync(&fail, c->fail_d, sizeof(int), hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  if (fail != big) {
+    c->have_factor[which] = false;
+    char buf[160];
+    std::snprintf(buf, sizeof buf, "vecchia factor: local covariance of row %d is not positive definite", fail);
+    return fail_msg(c, NNGP_ERR_CHOL, buf);
+  }
+  c->have_factor[which] = true;
+  if (which == 0) return refresh_sweep_values(c);
+  return NNGP_OK;
+}
+
+int nngp_get_linv(nngp_ctx* c, int which, double* Linv) {
+  if (!c || !Linv || (which != 0 && which != 1)) return NNGP_ERR_ARG;
+  if (!c->have_factor[which]) return fail_msg(c, NNGP_ERR_STATE, "get_linv: factor not computed");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  std::vector<double> rm((size_t)c->n * c->b);
+  HIPCHK(c, hipMemcpyAsync(rm.data(), c->linv_d[which], rm.size() * sizeof(double), hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  for (int i = 0; i < c->n; ++i)
+    for (int j = 0; j < c->b; ++j) Linv[i + (size_t)j * c->n] = rm[(size_t)i * c->b + j];
+  return NNGP_OK;
+}
+
+int nngp_set_linv(nngp_ctx* c, int which, const double* Linv) {
+  if (!c || !Linv || (which != 0 && which != 1)) return NNGP_ERR_ARG;
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  std::vector<double> rm((size_t)c->n * c->b);
+  for (int i = 0; i < c->n; ++i)
+    for (int j = 0; j < c->b; ++j) rm[(size_t)i * c->b + j] = Linv[i + (size_t)j * c->n];
+  HIPCHK(c, hipMemcpyAsync(c->linv_d[which], rm.data(), rm.size() * sizeof(double), hipMemcpyHostToDevice, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  c->have_factor[which] = true;
+  if (which == 0) return refresh_sweep_values(c);
+  return NNGP_OK;
+}
+
+int nngp_accept_factor(nngp_ctx* c) {
+  if (!c) return NNGP_ERR_ARG;
+  if (!c->have_factor[1]) return fail_msg(c, NNGP_ERR_STATE, "accept_factor: no proposal factor");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  std::swap(c->linv_d[0], c->linv_d[1]);
+  std::swap(c->have_factor[0], c->have_factor[1]);
+  // cached graphs captured the old buffer pointers
+  for (auto& kv : c->graphs) hipGraphExecDestroy(kv.second);
+  c->graphs.clear();
+  for (auto g : c->graph_objs) hipGraphDestroy(g);
+  c->graph_objs.clear();
+  return refresh_sweep_values(c);
+}
+
+int nngp_get_precision_diag(nngp_ctx* c, double* D) {
+  if (!c || !D) return NNGP_ERR_ARG;
+  if (!c->have_factor[0]) return fail_msg(c, NNGP_ERR_STATE, "precision_diag: no factor");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  std::vector<double> Ds(c->n);
+  HIPCHK(c, hipMemcpyAsync(Ds.data(), c->D_slot_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  for (int s = 0; s < c->n; ++s) D[c->lay.slot_loc[s]] = Ds[s];
+  return NNGP_OK;
+}
+
+// ---------------------------------------------------------------- state
+int nngp_set_field(nngp_ctx* c, const double* field) {
+  if (!c || !field) return NNGP_ERR_ARG;
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->field_d, field, c->n * sizeof(double), hipMemcpyHostToDevice, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  c->have_field = true;
+  return NNGP_OK;
+}
+
+int nngp_get_field(nngp_ctx* c, double* field) {
+  if (!c || !field) return NNGP_ERR_ARG;
+  if (!c->have_field) return fail_msg(c, NNGP_ERR_STATE, "get_field: no field");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  HIPCHK(c, hipMemcpyAsync(field, c->field_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  return NNGP_OK;
+}
+
+int nngp_set_mu(nngp_ctx* c, const double* mu, double beta0) {
+  if (!c) return NNGP_ERR_ARG;
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  if (mu) HIPCHK(c, hipMemcpyAsync(c->mu_d, mu, c->n_obs * sizeof(double), hipMemcpyHostToDevice, c->st));
+  c->mu_is_const = (mu == nullptr);
+  c->mu_beta0 = beta0;
+  HIPCHK(c, launch_residual_sums(c->st, c->n, c->slot_loc_d, c->obs_ptr_d, c->obs_idx_d, c->y_d,
+                                 mu ? c->mu_d : nullptr, beta0, c->R_slot_d));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  c->have_mu = true;
+  return NNGP_OK;
+}
+
+// ---------------------------------------------------------------- loglik
+int nngp_loglik(nngp_ctx* c, int which, double beta0, double log_scale, double* ll) {
+  if (!c || !ll || (which != 0 && which != 1)) return NNGP_ERR_ARG;
+  if (!c->have_factor[which] || !c->have_field) return fail_msg(c, NNGP_ERR_STATE, "loglik: need factor and field");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  int nb = launch_row_stats(c->st, c->linv_d[which], c->nn_d, c->n, c->b, c->field_d, beta0, nullptr,
+                            nullptr, c->partials_d);
+  HIPCHK(c, hipGetLastError());
+  double r[4];
+  if ((rc = fetch4(c, nb, r))) return rc;
+  *ll = r[0] - c->n * 0.5 * log_scale - 0.5 * r[1] / std::exp(log_scale);
+  return NNGP_OK;
+}
+
+// ---------------------------------------------------------------- sweep
+static int sweep_prepare(nngp_ctx* c, double beta0, double log_scale, double lnv, uint64_t seed,
+                         uint64_t counter_base) {
+  if (!c->have_factor[0] || !c->have_field || !c->have_mu)
+    return fail_msg(c, NNGP_ERR_STATE, "sweep: need factor, field and mu");
+  if (c->mu_is_const && c->mu_beta0 != beta0) {
+    // residual sums depend on beta0 when mu = beta0
+    HIPCHK(c, launch_residual_sums(c->st, c->n, c->slot_loc_d, c->obs_ptr_d, c->obs_idx_d, c->y_d,
+                                   nullptr, beta0, c->R_slot_d));
+    c->mu_beta0 = beta0;
+  }
+  c->scal_h->inv_s2 = std::exp(-log_scale);
+  c->scal_h->inv_t2 = std::exp(-lnv);
+  c->scal_h->beta0 = beta0;
+  c->scal_h->pad = 0;
+  c->scal_h->seed = seed;
+  c->scal_h->counter_base = counter_base;
+  HIPCHK(c, hipMemcpyAsync(c->scal_d, c->scal_h, sizeof(SweepScalars), hipMemcpyHostToDevice, c->st));
+  return NNGP_OK;
+}
+
+// r = B (field - beta0), written at Morton positions; w_slot = field - beta0
+static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, const double* z_dev,
+                              std::vector<hipEvent_t>* evs) {
+  const int n = c->n;
+  HIPCHK(c, launch_field_to_slots(c->st, n, c->slot_loc_d, c->field_d, c->scal_d, c->w_slot_d));
+  // shift read from device memory so a replayed graph sees the current beta0
+  launch_row_stats(c->st, c->linv_d[0], c->nn_d, n, c->b, c->field_d, 0.0, c->r_d, c->rpos_d,
+                   c->partials_d, &c->scal_d->beta0);
+  HIPCHK(c, hipGetLastError());
+  SweepDev L = sweep_dev(c);
+  for (int s = 0; s < n_sweeps; ++s) {
+    for (int col = 0; col < c->lay.K; ++col) {
+      int ch0 = c->lay.color_chunk_ptr[col];
+      int nch = c->lay.color_chunk_ptr[col + 1] - ch0;
+      int slot_end = c->lay.color_slot_ptr[col + 1];
+      if (evs) HIPCHK(c, hipEventRecord((*evs)[2 * ((size_t)s * c->lay.K + col)], c->st));
+      HIPCHK(c, launch_sweep_color(c->st, L, ch0, nch, slot_end, c->scal_d, s, z_dev, n));
+      if (evs) HIPCHK(c, hipEventRecord((*evs)[2 * ((size_t)s * c->lay.K + col) + 1], c->st));
+    }
+  }
+  HIPCHK(c, launch_slots_to_field(c->st, n, c->slot_loc_d, c->w_slot_d, c->scal_d, c->field_d));
+  return NNGP_OK;
+}
+
+int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double lnv, uint64_t seed,
+               uint64_t counter_base, const double* z) {
+  if (!c || n_sweeps < 0) return NNGP_ERR_ARG;
+  if (n_sweeps == 0) return NNGP_OK;
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  if ((rc = sweep_prepare(c, beta0, log_scale, lnv, seed, counter_base))) return rc;
+  if (z) {
+    size_t need = (size_t)n_sweeps * c->n;
+    if (need > c->z_cap) {
+      if (c->z_d) hipFree(c->z_d);
+      c->z_d = nullptr;
+      c->z_cap = 0;
+      HIPCHK(c, dalloc(&c->z_d, need));
+      c->z_cap = need;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->z_d, z, need * sizeof(double), hipMemcpyHostToDevice, c->st));
+    if ((rc = enqueue_sweep_body(c, n_sweeps, c->z_d, nullptr))) return rc;
+  } else {
+    // replay a captured graph of the whole call (launch-bound at small n)
+    auto it = c->graphs.find(n_sweeps);
+    if (it == c->graphs.end()) {
+      hipGraph_t g;
+      HIPCHK(c, hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
+      rc = enqueue_sweep_body(c, n_sweeps, nullptr, nullptr);
+      hipError_t e = hipStreamEndCapture(c->st, &g);
+      if (rc) return rc;
+      if (e != hipSuccess) return fail_hip(c, e, "hipStreamEndCapture");
+      hipGraphExec_t ex;
+      HIPCHK(c, hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+      c->graph_objs.push_back(g);
+      it = c->graphs.emplace(n_sweeps, ex).first;
+    }
+    HIPCHK(c, hipGraphLaunch(it->second, c->st));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  return NNGP_OK;
+}
+
+int nngp_sweep_timed(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double lnv,
+                     uint64_t seed, uint64_t counter_base, double* ms, double* kernel_ms) {
+  if (!c || n_sweeps < 1 || !ms) return NNGP_ERR_ARG;
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  if ((rc = sweep_prepare(c, beta0, log_scale, lnv, seed, counter_base))) return rc;
+  hipEvent_t e0, e1;
+  HIPCHK(c, hipEventCreate(&e0));
+  HIPCHK(c, hipEventCreate(&e1));
+  std::vector<hipEvent_t> evs;
+  if (kernel_ms) {
+    evs.resize(2 * (size_t)n_sweeps * c->lay.K);
+    for (auto& e : evs) HIPCHK(c, hipEventCreate(&e));
+    HIPCHK(c, hipEventRecord(e0, c->st));
+    rc = enqueue_sweep_body(c, n_sweeps, nullptr, &evs);
+    HIPCHK(c, hipEventRecord(e1, c->st));
+  } else {
+    auto it = c->graphs.find(n_sweeps);
+    if (it == c->graphs.end()) {
+      hipGraph_t g;
+      HIPCHK(c, hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
+      rc = enqueue_sweep_body(c, n_sweeps, nullptr, nullptr);
+      hipError_t e = hipStreamEndCapture(c->st, &g);
+      if (rc) return rc;
+      if (e != hipSuccess) return fail_hip(c, e, "hipStreamEndCapture");
+      hipGraphExec_t ex;
+      HIPCHK(c, hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+      c->graph_objs.push_back(g);
+      it = c->graphs.emplace(n_sweeps, ex).first;
+    }
+    HIPCHK(c, hipEventRecord(e0, c->st));
+    HIPCHK(c, hipGraphLaunch(it->second, c->st));
+    HIPCHK(c, hipEventRecord(e1, c->st));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  if (rc) return rc;
+  float f = 0;
+  HIPCHK(c, hipEventElapsedTime(&f, e0, e1));
+  *ms = f;
+  if (kernel_ms) {
+    double tot = 0;
+    for (size_t k = 0; k < evs.size(); k += 2) {
+      float g = 0;
+      HIPCHK(c, hipEventElapsedTime(&g, evs[k], evs[k + 1]));
+      tot += g;
+    }
+    *kernel_ms = tot;
+    for (auto& e : evs) hipEventDestroy(e);
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  return NNGP_OK;
+}
+
+// ---------------------------------------------------------------- MH helpers
+static int tri_solve_dev(nngp_ctx* c, const double* linv, const double* u, double* x) {
+  for (size_t l = 0; l + 1 < c->level_ptr.size(); ++l) {
+    int a = c->level_ptr[l], e = c->level_ptr[l + 1];
+    if (e > a) HIPCHK(c, launch_tri_level(c->st, c->level_rows_d + a, e - a, linv, c->nn_d, c->b, u, x));
+  }
+  return NNGP_OK;
+}
+
+int nngp_ancillary_propose(nngp_ctx* c, double beta0, double dlog_scale) {
+  if (!c) return NNGP_ERR_ARG;
+  if (!c->have_factor[0] || !c->have_factor[1] || !c->have_field)
+    return fail_msg(c, NNGP_ERR_STATE, "ancillary_propose: need both factors and the field");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  // tmp = B_cur (field - beta0)
+  launch_row_stats(c->st, c->linv_d[0], c->nn_d, c->n, c->b, c->field_d, beta0, c->tmp_d, nullptr,
+                   c->partials_d);
+  HIPCHK(c, hipGetLastError());
+  if ((rc = tri_solve_dev(c, c->linv_d[1], c->tmp_d, c->tmp2_d))) return rc;
+  HIPCHK(c, launch_axpby_shift(c->st, c->n, c->tmp2_d, std::exp(0.5 * dlog_scale), beta0, c->field_prop_d));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  return NNGP_OK;
+}
+
+int nngp_field_response_ratio(nngp_ctx* c, double beta0, double lnv, double* ratio) {
+  if (!c || !ratio) return NNGP_ERR_ARG;
+  if (!c->have_field || !c->have_mu) return fail_msg(c, NNGP_ERR_STATE, "response_ratio: need field and mu");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  int nb = launch_obs_reduce(c->st, 1, c->n_obs, c->y_d, c->mu_is_const ? nullptr : c->mu_d, beta0,
+                             c->lm_d, c->field_d, c->field_prop_d, 0.5 * std::exp(-lnv), c->partials_d);
+  HIPCHK(c, hipGetLastError());
+  double r[4];
+  if ((rc = fetch4(c, nb, r))) return rc;
+  *ratio = r[0];
+  return NNGP_OK;
+}
+
+int nngp_accept_field(nngp_ctx* c) {
+  if (!c) return NNGP_ERR_ARG;
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->field_d, c->field_prop_d, c->n * sizeof(double), hipMemcpyDeviceToDevice, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  return NNGP_OK;
+}
+
+int nngp_beta0_stats(nngp_ctx* c, double* oqo, double* oqf) {
+  if (!c || !oqo || !oqf) return NNGP_ERR_ARG;
+  if (!c->have_factor[0] || !c->have_field) return fail_msg(c, NNGP_ERR_STATE, "beta0_stats: need factor and field");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  int nb = launch_row_stats(c->st, c->linv_d[0], c->nn_d, c->n, c->b, c->field_d, 0.0, nullptr, nullptr,
+                            c->partials_d);
+  HIPCHK(c, hipGetLastError());
+  double r[4];
+  if ((rc = fetch4(c, nb, r))) return rc;
+  *oqo = r[2];
+  *oqf = r[3];
+  return NNGP_OK;
+}
+
+int nngp_sum_squared_residuals(nngp_ctx* c, double beta0, double* ssr) {
+  if (!c || !ssr) return NNGP_ERR_ARG;
+  if (!c->have_field || !c->have_mu) return fail_msg(c, NNGP_ERR_STATE, "ssr: need field and mu");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  int nb = launch_obs_reduce(c->st, 0, c->n_obs, c->y_d, c->mu_is_const ? nullptr : c->mu_d, beta0,
+                             c->lm_d, c->field_d, nullptr, 0.0, c->partials_d);
+  HIPCHK(c, hipGetLastError());
+  double r[4];
+  if ((rc = fetch4(c, nb, r))) return rc;
+  *ssr = r[0];
+  return NNGP_OK;
+}
+
+int nngp_spmv(nngp_ctx* c, int which, const double* X, int ncols, double* Y) {
+  if (!c || !X || !Y || ncols < 0 || (which != 0 && which != 1)) return NNGP_ERR_ARG;
+  if (!c->have_factor[which]) return fail_msg(c, NNGP_ERR_STATE, "spmv: no factor");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  for (int col = 0; col < ncols; ++col) {
+    HIPCHK(c, hipMemcpyAsync(c->tmp2_d, X + (size_t)col * c->n, c->n * sizeof(double), hipMemcpyHostToDevice, c->st));
+    launch_row_stats(c->st, c->linv_d[which], c->nn_d, c->n, c->b, c->tmp2_d, 0.0, c->tmp_d, nullptr, c->partials_d);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(Y + (size_t)col * c->n, c->tmp_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+  }
+  return NNGP_OK;
+}
+
+int nngp_tri_solve(nngp_ctx* c, int which, const double* u, double* x) {
+  if (!c || !u || !x || (which != 0 && which != 1)) return NNGP_ERR_ARG;
+  if (!c->have_factor[which]) return fail_msg(c, NNGP_ERR_STATE, "tri_solve: no factor");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->tmp_d, u, c->n * sizeof(double), hipMemcpyHostToDevice, c->st));
+  if ((rc = tri_solve_dev(c, c->linv_d[which], c->tmp_d, c->tmp2_d))) return rc;
+  HIPCHK(c, hipMemcpyAsync(x, c->tmp2_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  return NNGP_OK;
+}
+
+int nngp_device_normals(int device, uint64_t seed, uint64_t sweep, int n, double* z) {
+  if (!z || n < 1) return NNGP_ERR_ARG;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail_msg(nullptr, NNGP_ERR_NODEV, "no HIP device");
+  if (device < 0) device = 0;
+  if (hipSetDevice(device) != hipSuccess) return NNGP_ERR_HIP;
+  double* d = nullptr;
+  if (hipMalloc((void**)&d, sizeof(double) * n) != hipSuccess) return NNGP_ERR_NOMEM;
+  hipError_t e = launch_normals(nullptr, seed, sweep, n, d);
+  if (e == hipSuccess) e = hipMemcpy(z, d, sizeof(double) * n, hipMemcpyDeviceToHost);
+  hipFree(d);
+  return e == hipSuccess ? NNGP_OK : fail_hip(nullptr, e, "device_normals");
+}
+
+}  // extern "C"

@@ -1,0 +1,459 @@
+// Host-side init-time graph preparation (C++).
+//
+// Replaces, with the same semantics and bit-exact outputs given the ordering:
+//   GpGp::find_ordered_nn ........ Scripts/mcmc_nngp_initialize.R:93
+//   moral graph + colouring ...... Scripts/mcmc_nngp_initialize.R:97-110,
+//                                  Scripts/Coloring.R:2-20
+//   GpGp::order_maxmin ........... Scripts/mcmc_nngp_initialize.R:29 (exact
+//                                  max-min; GpGp's is approximate+jittered)
+// and plans the HBM layout of the chromatic sweep (DESIGN.md "Layout").
+//
+// Squared distances are accumulated in coordinate order as
+// t = x_query - x_other; s += t*t (compiled with -ffp-contract=off) so ties
+// and orderings are reproducible bit-for-bit.
+#include "graph_prep.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <numeric>
+
+namespace nngp {
+namespace {
+
+inline double sqdist(const double* locs, int n, int d, int a, int b) {
+  double s = 0.0;
+  for (int k = 0; k < d; ++k) {
+    double t = locs[a + (size_t)k * n] - locs[b + (size_t)k * n];
+    s += t * t;
+  }
+  return s;
+}
+
+// Uniform grid over the first dg = min(d,3) coordinates of points [0, P).
+struct Grid {
+  int dg = 1;
+  double lo[3] = {0, 0, 0};
+  double cs = 1.0;
+  long long nc[3] = {1, 1, 1};
+  std::vector<int> start;  // ncells + 1
+  std::vector<int> pts;    // point ids grouped by cell, ascending inside a cell
+
+  long long ncells() const { return nc[0] * nc[1] * nc[2]; }
+
+  long long coord(double x, int k) const {
+    long long c = (long long)std::floor((x - lo[k]) / cs);
+    if (c < 0) c = 0;
+    if (c >= nc[k]) c = nc[k] - 1;
+    return c;
+  }
+  long long cell_of(const double* locs, int n, int i, long long* cc) const {
+    long long id = 0;
+    for (int k = 2; k >= 0; --k) {
+      cc[k] = (k < dg) ? coord(locs[i + (size_t)k * n], k) : 0;
+      id = id * nc[k] + cc[k];
+    }
+    return id;
+  }
+  long long id_of(const long long* cc) const { return (cc[2] * nc[1] + cc[1]) * nc[0] + cc[0]; }
+
+  void build(const double* locs, int n, int d, int P, double pts_per_cell) {
+    dg = std::min(d, 3);
+    double hi[3];
+    for (int k = 0; k < 3; ++k) { lo[k] = 0; hi[k] = 0; nc[k] = 1; }
+    for (int k = 0; k < dg; ++k) {
+      double a = std::numeric_limits<double>::infinity(), b = -a;
+      for (int i = 0; i < n; ++i) {  // bounding box of ALL points: stable across prefixes
+        double x = locs[i + (size_t)k * n];
+        a = std::min(a, x); b = std::max(b, x);
+      }
+      lo[k] = a; hi[k] = b;
+    }
+    double target = std::max(1.0, P / pts_per_cell);
+    double ext[3];
+    double maxext = 0;
+    for (int k = 0; k < dg; ++k) { ext[k] = hi[k] - lo[k]; maxext = std::max(maxext, ext[k]); }
+    if (!(maxext > 0)) maxext = 1.0;
+    // choose cs so that prod ceil(ext/cs) ~ target (bisection on cs)
+    double a = maxext / target, b = maxext * 1.0000001;
+    if (a <= 0) a = maxext * 1e-9;
+    for (int it = 0; it < 60; ++it) {
+      double mid = std::sqrt(a * b);
+      double cells = 1;
+      for (int k = 0; k < dg; ++k) cells *= std::max(1.0, std::ceil(ext[k] / mid));
+      if (cells > target) a = mid; else b = mid;
+    }
+    cs = b;
+    for (int k = 0; k < dg; ++k) nc[k] = std::max(1LL, (long long)std::ceil(ext[k] / cs));
+    long long C = ncells();
+    start.assign(C + 1, 0);
+    pts.resize(P);
+    std::vector<long long> cid(P);
+    long long cc[3];
+    for (int i = 0; i < P; ++i) { cid[i] = cell_of(locs, n, i, cc); start[cid[i] + 1]++; }
+    for (long long c = 0; c < C; ++c) start[c + 1] += start[c];
+    std::vector<int> fill(start.begin(), start.end() - 1);
+    for (int i = 0; i < P; ++i) pts[fill[cid[i]]++] = i;
+  }
+};
+
+struct Cand {
+  double s;
+  int j;
+};
+inline bool lex_less(double s1, int j1, double s2, int j2) { return s1 < s2 || (s1 == s2 && j1 < j2); }
+
+struct TopM {
+  int m, cnt = 0;
+  Cand* c;
+  void reset() { cnt = 0; }
+  void offer(double s, int j) {
+    if (cnt == m && !lex_less(s, j, c[cnt - 1].s, c[cnt - 1].j)) return;
+    int p = cnt < m ? cnt++ : cnt - 1;
+    while (p > 0 && lex_less(s, j, c[p - 1].s, c[p - 1].j)) { c[p] = c[p - 1]; --p; }
+    c[p].s = s; c[p].j = j;
+  }
+  double worst() const { return c[cnt - 1].s; }
+};
+
+}  // namespace
+
+void morton_keys(const double* locs, int n, int d, std::vector<uint64_t>& keys) {
+  int dg = std::min(d, 3);
+  double lo[3] = {0, 0, 0}, hi[3] = {1, 1, 1};
+  for (int k = 0; k < dg; ++k) {
+    double a = std::numeric_limits<double>::infinity(), b = -a;
+    for (int i = 0; i < n; ++i) { double x = locs[i + (size_t)k * n]; a = std::min(a, x); b = std::max(b, x); }
+    lo[k] = a; hi[k] = (b > a) ? b : a + 1.0;
+  }
+  const int bits = dg == 1 ? 63 : (dg == 2 ? 31 : 21);
+  const double scale = (double)((1ULL << bits) - 1);
+  keys.resize(n);
+  for (int i = 0; i < n; ++i) {
+    uint64_t q[3] = {0, 0, 0};
+    for (int k = 0; k < dg; ++k) {
+      double u = (locs[i + (size_t)k * n] - lo[k]) / (hi[k] - lo[k]);
+      u = std::min(1.0, std::max(0.0, u));
+      q[k] = (uint64_t)(u * scale);
+    }
+    uint64_t key = 0;
+    for (int bit = bits - 1; bit >= 0; --bit)
+      for (int k = dg - 1; k >= 0; --k) key = (key << 1) | ((q[k] >> bit) & 1ULL);
+    keys[i] = key;
+  }
+}
+
+// ---------------------------------------------------------------- max-min
+void order_maxmin(const double* locs, int n, int d, std::vector<int>& order) {
+  order.clear();
+  if (n <= 0) return;
+  order.reserve(n);
+  double cen[8] = {0};
+  for (int k = 0; k < d && k < 8; ++k) {
+    for (int i = 0; i < n; ++i) cen[k] += locs[i + (size_t)k * n];
+    cen[k] /= n;
+  }
+  int first = 0;
+  double best = std::numeric_limits<double>::infinity();
+  for (int i = 0; i < n; ++i) {
+    double s = 0;
+    for (int k = 0; k < d; ++k) { double t = locs[i + (size_t)k * n] - cen[k]; s += t * t; }
+    if (s < best) { best = s; first = i; }
+  }
+  Grid g;
+  g.build(locs, n, d, n, 2.0);
+  std::vector<double> dist(n, std::numeric_limits<double>::infinity());
+  std::vector<char> used(n, 0);
+  // indexed max-heap on (dist, -idx)
+  std::vector<int> heap, pos(n, -1);
+  auto better = [&](int a, int b) { return dist[a] > dist[b] || (dist[a] == dist[b] && a < b); };
+  auto sift_down = [&](int p) {
+    int sz = (int)heap.size();
+    for (;;) {
+      int l = 2 * p + 1, r = l + 1, t = p;
+      if (l < sz && better(heap[l], heap[t])) t = l;
+      if (r < sz && better(heap[r], heap[t])) t = r;
+      if (t == p) return;
+      std::swap(heap[p], heap[t]); pos[heap[p]] = p; pos[heap[t]] = t; p = t;
+    }
+  };
+  // first selection: every point's distance to `first`
+  order.push_back(first);
+  used[first] = 1;
+  for (int i = 0; i < n; ++i)
+    if (!used[i]) dist[i] = sqdist(locs, n, d, i, first);
+  heap.reserve(n);
+  for (int i = 0; i < n; ++i) if (!used[i]) { pos[i] = (int)heap.size(); heap.push_back(i); }
+  for (int p = (int)heap.size() / 2 - 1; p >= 0; --p) sift_down(p);
+  long long cc[3], lo_c[3], hi_c[3];
+  while (!heap.empty()) {
+    int p = heap[0];
+    int last = heap.back(); heap.pop_back();
+    pos[p] = -1;
+    if (!heap.empty()) { heap[0] = last; pos[last] = 0; sift_down(0); }
+    order.push_back(p);
+    used[p] = 1;
+    double r2 = dist[p];
+    double r = std::sqrt(r2);
+    g.cell_of(locs, n, p, cc);
+    for (int k = 0; k < 3; ++k) {
+      if (k < g.dg) {
+        double x = locs[p + (size_t)k * n];
+        lo_c[k] = g.coord(x - r, k);
+        hi_c[k] = g.coord(x + r, k);
+      } else { lo_c[k] = hi_c[k] = 0; }
+    }
+    long long q[3];
+    for (q[2] = lo_c[2]; q[2] <= hi_c[2]; ++q[2])
+      for (q[1] = lo_c[1]; q[1] <= hi_c[1]; ++q[1])
+        for (q[0] = lo_c[0]; q[0] <= hi_c[0]; ++q[0]) {
+          long long id = g.id_of(q);
+          for (int t = g.start[id]; t < g.start[id + 1]; ++t) {
+            int j = g.pts[t];
+            if (used[j]) continue;
+            double s = sqdist(locs, n, d, j, p);
+            if (s < dist[j]) { dist[j] = s; sift_down(pos[j]); }
+          }
+        }
+  }
+}
+
+// ---------------------------------------------------------------- ordered NN
+void find_ordered_nn(const double* locs, int n, int d, int m, std::vector<int>& nn) {
+  const int b = m + 1;
+  nn.assign((size_t)n * b, -1);
+  std::vector<Cand> buf(std::max(m, 1));
+  TopM top{m, 0, buf.data()};
+  auto write_row = [&](int i) {
+    nn[(size_t)i * b] = i;
+    for (int t = 0; t < top.cnt; ++t) nn[(size_t)i * b + 1 + t] = top.c[t].j;
+  };
+  const int brute = std::min(n, std::max(64, 4 * b));
+  for (int i = 0; i < brute; ++i) {
+    top.reset();
+    if (m > 0)
+      for (int j = 0; j < i; ++j) top.offer(sqdist(locs, n, d, i, j), j);
+    write_row(i);
+  }
+  if (m == 0) { for (int i = brute; i < n; ++i) nn[(size_t)i * b] = i; return; }
+  Grid g;
+  long long cc[3], q[3];
+  for (int lo = brute; lo < n;) {
+    int hi = (int)std::min<long long>((long long)n, 2LL * lo);
+    g.build(locs, n, d, hi, std::max(2.0, m / 3.0));
+    for (int i = lo; i < hi; ++i) {
+      top.reset();
+      g.cell_of(locs, n, i, cc);
+      long long maxR = std::max(g.nc[0], std::max(g.nc[1], g.nc[2]));
+      for (long long R = 0;; ++R) {
+        // visit cells at Chebyshev distance exactly R
+        long long lo_c[3], hi_c[3];
+        for (int k = 0; k < 3; ++k) {
+          if (k < g.dg) { lo_c[k] = std::max(0LL, cc[k] - R); hi_c[k] = std::min(g.nc[k] - 1, cc[k] + R); }
+          else { lo_c[k] = hi_c[k] = 0; }
+        }
+        auto scan_cell = [&](const long long* qq) {
+          long long id = g.id_of(qq);
+          for (int t = g.start[id]; t < g.start[id + 1]; ++t) {
+            int j = g.pts[t];
+            if (j >= i) break;  // pts ascending inside a cell
+            top.offer(sqdist(locs, n, d, i, j), j);
+          }
+        };
+        for (q[2] = lo_c[2]; q[2] <= hi_c[2]; ++q[2])
+          for (q[1] = lo_c[1]; q[1] <= hi_c[1]; ++q[1]) {
+            long long outer = 0;
+            if (g.dg >= 2) outer = std::max(outer, std::llabs(q[1] - cc[1]));
+            if (g.dg >= 3) outer = std::max(outer, std::llabs(q[2] - cc[2]));
+            if (outer == R) {
+              for (q[0] = lo_c[0]; q[0] <= hi_c[0]; ++q[0]) scan_cell(q);
+            } else {
+              // only the two cells at |dq0| == R are on the ring
+              q[0] = cc[0] - R;
+              if (q[0] >= 0) scan_cell(q);
+              q[0] = cc[0] + R;
+              if (R > 0 && q[0] < g.nc[0]) scan_cell(q);
+            }
+          }
+        if (R >= maxR) break;
+        // every unvisited point is >= R*cs away (tiny margin for cell rounding)
+        if (top.cnt == std::min(m, i)) {
+          double bound = ((double)R - 1e-6) * g.cs;
+          if (bound > 0 && bound * bound > top.worst()) break;
+        }
+      }
+      write_row(i);
+    }
+    lo = hi;
+  }
+}
+
+// ---------------------------------------------------------------- colouring
+int greedy_coloring(const int* nn, int n, int b, std::vector<int>& colors) {
+  // CSC of the pattern of B: column i -> rows k with i in row(k)
+  std::vector<int> cptr(n + 1, 0);
+  for (long long e = 0; e < (long long)n * b; ++e) if (nn[e] >= 0) cptr[nn[e] + 1]++;
+  for (int i = 0; i < n; ++i) cptr[i + 1] += cptr[i];
+  std::vector<int> crow(cptr[n]);
+  std::vector<int> fill(cptr.begin(), cptr.end() - 1);
+  for (int k = 0; k < n; ++k)
+    for (int t = 0; t < b; ++t) {
+      int a = nn[(size_t)k * b + t];
+      if (a >= 0) crow[fill[a]++] = k;
+    }
+  colors.assign(n, 0);
+  std::vector<int> mark(64, 0);
+  int K = 0;
+  for (int i = 0; i < n; ++i) {
+    int stamp = i + 1;
+    for (int p = cptr[i]; p < cptr[i + 1]; ++p) {
+      int k = crow[p];
+      for (int t = 0; t < b; ++t) {
+        int j = nn[(size_t)k * b + t];
+        if (j >= 0 && j < i) mark[colors[j]] = stamp;
+      }
+    }
+    int c = 1;
+    while (c < (int)mark.size() && mark[c] == stamp) ++c;
+    if (c + 1 >= (int)mark.size()) mark.resize(2 * mark.size() + 2, 0);
+    colors[i] = c;
+    K = std::max(K, c);
+  }
+  return K;
+}
+
+// ---------------------------------------------------------------- layout
+bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const double* locs, int d,
+                        SweepLayout& L, std::string& err) {
+  L = SweepLayout();
+  L.n = n; L.b = b;
+  int K = 0;
+  for (int i = 0; i < n; ++i) {
+    if (colors[i] < 1) { err = "coloring must be 1-based positive"; return false; }
+    K = std::max(K, colors[i]);
+  }
+  L.K = K;
+  std::vector<uint64_t> key;
+  morton_keys(locs, n, d, key);
+  // r positions: global Morton rank
+  std::vector<int> perm(n);
+  std::iota(perm.begin(), perm.end(), 0);
+  std::sort(perm.begin(), perm.end(), [&](int a, int c) { return key[a] < key[c] || (key[a] == key[c] && a < c); });
+  L.rpos.resize(n);
+  for (int r = 0; r < n; ++r) L.rpos[perm[r]] = r;
+  // CSC (rows ascending inside a column)
+  std::vector<long long> cptr(n + 1, 0);
+  for (long long e = 0; e < (long long)n * b; ++e) {
+    int a = nn[e];
+    if (a >= n) { err = "NNarray index out of range"; return false; }
+    if (a >= 0) cptr[a + 1]++;
+  }
+  for (int i = 0; i < n; ++i) cptr[i + 1] += cptr[i];
+  // slots: colour-major; inside a colour by descending column length, then
+  // Morton order.  Column lengths of a max-min Vecchia factor are very skewed
+  // (median ~m, max ~12m): equal lengths inside a 64-slot chunk remove the
+  // sliced-ELL padding, Morton order inside a length keeps the r gathers of a
+  // chunk spatially local.
+  L.color_slot_ptr.assign(K + 1, 0);
+  for (int i = 0; i < n; ++i) L.color_slot_ptr[colors[i]]++;
+  for (int c = 0; c < K; ++c) L.color_slot_ptr[c + 1] += L.color_slot_ptr[c];
+  for (int c = 0; c < K; ++c) {
+    if (L.color_slot_ptr[c + 1] == L.color_slot_ptr[c]) { err = "coloring has an empty colour class"; return false; }
+  }
+  L.slot_loc.resize(n);
+  L.loc_slot.resize(n);
+  {
+    std::vector<int> f(L.color_slot_ptr.begin(), L.color_slot_ptr.end() - 1);
+    for (int r = 0; r < n; ++r) { int i = perm[r]; int s = f[colors[i] - 1]++; L.slot_loc[s] = i; }
+    for (int c = 0; c < K; ++c) {
+      auto a = L.slot_loc.begin() + L.color_slot_ptr[c], e = L.slot_loc.begin() + L.color_slot_ptr[c + 1];
+      std::stable_sort(a, e, [&](int x, int y) { return cptr[x + 1] - cptr[x] > cptr[y + 1] - cptr[y]; });
+    }
+    for (int s = 0; s < n; ++s) L.loc_slot[L.slot_loc[s]] = s;
+  }
+  L.nnz = cptr[n];
+  std::vector<int> crow(L.nnz), csrc(L.nnz);
+  {
+    std::vector<long long> f(cptr.begin(), cptr.end() - 1);
+    for (int k = 0; k < n; ++k)
+      for (int t = 0; t < b; ++t) {
+        int a = nn[(size_t)k * b + t];
+        if (a < 0) continue;
+        long long p = f[a]++;
+        crow[p] = k; csrc[p] = k * b + t;
+      }
+  }
+  L.collen.resize(n);
+  for (int s = 0; s < n; ++s) {
+    int i = L.slot_loc[s];
+    L.collen[s] = (int)(cptr[i + 1] - cptr[i]);
+    L.max_collen = std::max(L.max_collen, L.collen[s]);
+  }
+  // chunks of 64 slots inside each colour
+  L.color_chunk_ptr.assign(K + 1, 0);
+  for (int c = 0; c < K; ++c) {
+    int sz = L.color_slot_ptr[c + 1] - L.color_slot_ptr[c];
+    L.color_chunk_ptr[c + 1] = L.color_chunk_ptr[c] + (sz + 63) / 64;
+  }
+  L.nchunks = L.color_chunk_ptr[K];
+  L.chunk_slot0.resize(L.nchunks);
+  L.chunk_len.resize(L.nchunks);
+  L.chunk_off.resize(L.nchunks + 1);
+  long long off = 0;
+  for (int c = 0; c < K; ++c) {
+    int s0 = L.color_slot_ptr[c], s1 = L.color_slot_ptr[c + 1];
+    for (int ch = L.color_chunk_ptr[c]; ch < L.color_chunk_ptr[c + 1]; ++ch) {
+      int a = s0 + (ch - L.color_chunk_ptr[c]) * 64;
+      int e = std::min(s1, a + 64);
+      int mx = 0;
+      for (int s = a; s < e; ++s) mx = std::max(mx, L.collen[s]);
+      L.chunk_slot0[ch] = a;
+      L.chunk_len[ch] = mx;
+      L.chunk_off[ch] = off;
+      off += (long long)mx * 64;
+    }
+  }
+  L.chunk_off[L.nchunks] = off;
+  L.n_entries = off;
+  L.ent_rowpos.assign(off, 0);
+  L.ent_src.assign(off, -1);
+  for (int c = 0; c < K; ++c) {
+    int s1 = L.color_slot_ptr[c + 1];
+    for (int ch = L.color_chunk_ptr[c]; ch < L.color_chunk_ptr[c + 1]; ++ch) {
+      for (int lane = 0; lane < 64; ++lane) {
+        int s = L.chunk_slot0[ch] + lane;
+        if (s >= s1) break;
+        int i = L.slot_loc[s];
+        for (long long p = cptr[i], jj = 0; p < cptr[i + 1]; ++p, ++jj) {
+          long long e = L.chunk_off[ch] + jj * 64 + lane;
+          L.ent_rowpos[e] = L.rpos[crow[p]];
+          L.ent_src[e] = csrc[p];
+        }
+      }
+    }
+  }
+  return true;
+}
+
+void dag_levels(const int* nn, int n, int b, std::vector<int>& level_ptr, std::vector<int>& level_rows) {
+  std::vector<int> lev(n, 0);
+  int maxl = 0;
+  for (int i = 0; i < n; ++i) {
+    int l = 0;
+    for (int t = 1; t < b; ++t) {
+      int j = nn[(size_t)i * b + t];
+      if (j >= 0) l = std::max(l, lev[j] + 1);
+    }
+    lev[i] = l;
+    maxl = std::max(maxl, l);
+  }
+  level_ptr.assign(maxl + 2, 0);
+  for (int i = 0; i < n; ++i) level_ptr[lev[i] + 1]++;
+  for (int l = 0; l <= maxl; ++l) level_ptr[l + 1] += level_ptr[l];
+  level_rows.resize(n);
+  std::vector<int> f(level_ptr.begin(), level_ptr.end() - 1);
+  for (int i = 0; i < n; ++i) level_rows[f[lev[i]]++] = i;
+}
+
+}  // namespace nngp

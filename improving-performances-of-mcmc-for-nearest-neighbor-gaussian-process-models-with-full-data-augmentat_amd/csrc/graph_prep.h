@@ -1,0 +1,58 @@
+// Host-side (C++) init-time graph preparation for the NNGP chromatic sweep.
+// Internal header: nothing here crosses the C ABI (see include/nngp.h).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace nngp {
+
+// Exact max-min ordering (first point closest to the centroid, then the point
+// farthest from the selected set; ties -> smaller index).  order: 0-based.
+void order_maxmin(const double* locs_colmajor, int n, int d, std::vector<int>& order);
+
+// Exact ordered nearest neighbours (GpGp::find_ordered_nn semantics without
+// GpGp's RNG jitter): nn[i*b + 0] = i, nn[i*b + 1..] = the m nearest j < i by
+// ascending squared Euclidean distance (ties -> smaller j), -1 padded.
+void find_ordered_nn(const double* locs_colmajor, int n, int d, int m, std::vector<int>& nn_rowmajor);
+
+// Greedy first-fit colouring of the moral graph pattern(B^T B) in index order
+// (Coloring.R:2-20).  nn: row-major 0-based, -1 = NA.  Returns K; colors 1-based.
+int greedy_coloring(const int* nn_rowmajor, int n, int b, std::vector<int>& colors);
+
+// Morton (Z-order) key of each location on a 21-bit-per-axis grid over the
+// bounding box of the first min(d,3) coordinates.
+void morton_keys(const double* locs_colmajor, int n, int d, std::vector<uint64_t>& keys);
+
+// Device layout of the chromatic sweep ("sliced-ELL by colour").
+//  - slots: locations re-indexed colour-major (colour 1 first), spatially
+//    (Morton) sorted inside a colour;
+//  - r positions: Morton rank of each Vecchia row;
+//  - chunks: 64 consecutive slots of one colour (one wavefront);
+//  - entries: column i of B stored at chunk_off[ch] + jj*64 + lane.
+struct SweepLayout {
+  int n = 0, b = 0, K = 0, nchunks = 0;
+  long long nnz = 0, n_entries = 0;
+  int max_collen = 0;
+  std::vector<int> color_slot_ptr;   // K+1
+  std::vector<int> color_chunk_ptr;  // K+1
+  std::vector<int> slot_loc;         // n
+  std::vector<int> loc_slot;         // n
+  std::vector<int> rpos;             // n: loc -> position in r
+  std::vector<int> collen;           // n (slot order)
+  std::vector<int> chunk_slot0;      // nchunks
+  std::vector<int> chunk_len;        // nchunks
+  std::vector<long long> chunk_off;  // nchunks
+  std::vector<int> ent_rowpos;       // n_entries (padding: 0)
+  std::vector<int> ent_src;          // n_entries (row-major Linv index k*b+j; padding: -1)
+};
+
+bool build_sweep_layout(const int* nn_rowmajor, int n, int b, const int* colors,
+                        const double* locs_colmajor, int d, SweepLayout& L, std::string& err);
+
+// Level sets of the Vecchia DAG for the sparse triangular solve:
+// level(i) = 1 + max level(NN(i)), level 0 rows have no neighbours.
+void dag_levels(const int* nn_rowmajor, int n, int b, std::vector<int>& level_ptr,
+                std::vector<int>& level_rows);
+
+}  // namespace nngp

@@ -1,0 +1,701 @@
+// HIP kernels of the NNGP chromatic-Gibbs hot path, written for gfx950
+// (MI355X, CDNA4: wave64, 256 CUs in 8 XCDs).  fp64 throughout.
+//
+// Kernel map (SURVEY.md §8a ids):
+//   scale_coords_kernel / factor_kernel  A4  GpGp::vecchia_Linv
+//   row_stats_kernel + reduce4_kernel    A6  ll_compressed_sparse_chol, B x, beta_0 stats
+//   sell_refresh_kernel                  A5  B values in sweep layout + precision_diag
+//   residual_sums_kernel                 A7  residuals_sum
+//   sweep_color_kernel                   A1  one colour of the chromatic sweep
+//   obs_reduce_kernel                    A8  SSR, dnorm ratio
+//   tri_level_kernel                     (next) Matrix::solve by DAG level
+#include "kernels.h"
+
+#include <cmath>
+
+namespace nngp {
+
+// ------------------------------------------------------------------ RNG
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+    uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    c[1] = (uint32_t)p1;
+    c[3] = (uint32_t)p0;
+    c[0] = n0;
+    c[2] = n2;
+  }
+}
+
+// N(0,1) for (seed, sweep, location): counter (loc, sweep_lo, sweep_hi, 0x5EED)
+__device__ __forceinline__ double normal_at(uint64_t seed, uint64_t sweep, uint32_t loc) {
+  uint32_t c[4] = {loc, (uint32_t)sweep, (uint32_t)(sweep >> 32), 0x5EEDu};
+  philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  uint64_t a = ((((uint64_t)c[1]) << 32) | c[0]) >> 11;
+  uint64_t b = ((((uint64_t)c[3]) << 32) | c[2]) >> 11;
+  double u1 = ((double)a + 0.5) * 0x1.0p-53;
+  double u2 = (double)b * 0x1.0p-53;
+  return sqrt(-2.0 * log(u1)) * cos(6.283185307179586476925286766559 * u2);
+}
+
+__global__ void normals_kernel(uint64_t seed, uint64_t sweep, int n, double* z) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) z[i] = normal_at(seed, sweep, (uint32_t)i);
+}
+
+// ------------------------------------------------------------------ Bessel K
+// K_nu(x): Temme's series (x < 2) / Steed's CF2 (x >= 2) for K_mu,
+// |mu| <= 1/2, then upward recurrence (Temme 1975; Press et al. bessik).
+__device__ void temme_gammas(double mu, double& gam1, double& gam2, double& gampl, double& gammi) {
+  gampl = 1.0 / tgamma(1.0 + mu);
+  gammi = 1.0 / tgamma(1.0 - mu);
+  gam2 = 0.5 * (gammi + gampl);
+  if (fabs(mu) < 0.05) {
+    // odd part of 1/Gamma(1+x) = sum c_k x^k (Abramowitz & Stegun 6.1.34)
+    double m2 = mu * mu;
+    gam1 = -(0.5772156649015329 +
+             m2 * (-0.0420026350340952 +
+                   m2 * (-0.0421977345555443 + m2 * (0.0072189432466630 + m2 * -0.0002152416741149))));
+  } else {
+    gam1 = (gammi - gampl) / (2.0 * mu);
+  }
+}
+
+__device__ double bessel_k(double nu, double x) {
+  const double EPS = 1e-16;
+  const double PI = 3.141592653589793238462643383;
+  int nl = (int)(nu + 0.5);
+  double xmu = nu - nl, xmu2 = xmu * xmu;
+  double xi = 1.0 / x, xi2 = 2.0 * xi;
+  double rkmu, rk1;
+  if (x < 2.0) {
+    double x2 = 0.5 * x, pimu = PI * xmu;
+    double fact = (fabs(pimu) < EPS) ? 1.0 : pimu / sin(pimu);
+    double dd = -log(x2);
+    double e = xmu * dd;
+    double fact2 = (fabs(e) < EPS) ? 1.0 : sinh(e) / e;
+    double gam1, gam2, gampl, gammi;
+    temme_gammas(xmu, gam1, gam2, gampl, gammi);
+    double ff = fact * (gam1 * cosh(e) + gam2 * fact2 * dd);
+    double sum = ff;
+    e = exp(e);
+    double p = 0.5 * e / gampl;
+    double q = 0.5 / (e * gammi);
+    double c = 1.0;
+    dd = x2 * x2;
+    double sum1 = p;
+    for (int i = 1; i <= 500; ++i) {
+      ff = (i * ff + p + q) / ((double)i * i - xmu2);
+      c *= dd / i;
+      p /= (i - xmu);
+      q /= (i + xmu);
+      double del = c * ff;
+      sum += del;
+      sum1 += c * (p - i * ff);
+      if (fabs(del) < fabs(sum) * EPS) break;
+    }
+    rkmu = sum;
+    rk1 = sum1 * xi2;
+  } else {
+    double bb = 2.0 * (1.0 + x);
+    double dd = 1.0 / bb;
+    double h = dd, delh = dd;
+    double q1 = 0.0, q2 = 1.0;
+    double a1 = 0.25 - xmu2;
+    double q = a1, c = a1;
+    double a = -a1;
+    double s = 1.0 + q * delh;
+    for (int i = 2; i <= 2000; ++i) {
+      a -= 2 * (i - 1);
+      c = -a * c / i;
+      double qnew = (q1 - bb * q2) / a;
+      q1 = q2;
+      q2 = qnew;
+      q += c * qnew;
+      bb += 2.0;
+      dd = 1.0 / (bb + a * dd);
+      delh = (bb * dd - 1.0) * delh;
+      h += delh;
+      double dels = q * delh;
+      s += dels;
+      if (fabs(dels / s) < EPS) break;
+    }
+    h = a1 * h;
+    rkmu = sqrt(PI / (2.0 * x)) * exp(-x) / s;
+    rk1 = rkmu * (xmu + x + 0.5 - h) * xi;
+  }
+  for (int i = 1; i <= nl; ++i) {
+    double t = (xmu + i) * xi2 * rk1 + rkmu;
+    rkmu = rk1;
+    rk1 = t;
+  }
+  return rkmu;
+}
+
+// correlation at unit-range distance dist.  FAM 0: exponential, 1: Matern 3/2,
+// 2: general Matern with norm = 2^(1-nu)/Gamma(nu)
+template <int FAM>
+__device__ __forceinline__ double corr(double dist, double nu, double norm) {
+  if (FAM == 0) return exp(-dist);
+  if (FAM == 1) return (1.0 + dist) * exp(-dist);
+  if (dist == 0.0) return 1.0;
+  return norm * pow(dist, nu) * bessel_k(nu, dist);
+}
+
+// ------------------------------------------------------------------ A4
+struct ScaleArgs {
+  double c[8];
+  int covfun;
+};
+
+__global__ void scale_coords_kernel(ScaleArgs a, const double* __restrict__ locs, int n, int d,
+                                    double* __restrict__ sc, int ds) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double x[4] = {0, 0, 0, 0}, o[4] = {0, 0, 0, 0};
+  for (int k = 0; k < d && k < 4; ++k) x[k] = locs[(size_t)i * d + k];
+  switch (a.covfun) {
+    case 1:
+    case 5: {  // lon/lat degrees -> unit sphere, chordal distance, range in radii
+      const double deg = 3.14159265358979323846 / 180.0;
+      double lon = x[0] * deg, lat = x[1] * deg;
+      o[0] = cos(lat) * cos(lon) / a.c[1];
+      o[1] = cos(lat) * sin(lon) / a.c[1];
+      o[2] = sin(lat) / a.c[1];
+      break;
+    }
+    case 2:
+    case 6:
+      for (int k = 0; k < d; ++k) o[k] = x[k] / a.c[1 + k];
+      break;
+    case 3:
+    case 7:
+      for (int k = 0; k < d - 1; ++k) o[k] = x[k] / a.c[1];
+      o[d - 1] = x[d - 1] / a.c[2];
+      break;
+    default:
+      for (int k = 0; k < d; ++k) o[k] = x[k] / a.c[1];
+  }
+  for (int k = 0; k < ds; ++k) sc[(size_t)i * ds + k] = o[k];
+}
+
+hipError_t launch_scale_coords(hipStream_t st, int covfun, const double* cp, int ncp,
+                               const double* locs_rm, int n, int d, double* sc, int ds) {
+  ScaleArgs a;
+  for (int k = 0; k < 8; ++k) a.c[k] = k < ncp ? cp[k] : 0.0;
+  a.covfun = covfun;
+  int g = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(scale_coords_kernel, dim3(g), dim3(kBlock), 0, st, a, locs_rm, n, d, sc, ds);
+  return hipGetLastError();
+}
+
+// One lane per Vecchia row i (GpGp::vecchia_Linv semantics): the local
+// covariance of locsub = locs[rev(NNarray[i,1:bs])] (self last) is factored
+// by an up-looking Cholesky held entirely in registers (compile-time indices);
+// rows of a short neighbourhood (bs < BM) are padded IN FRONT with identity
+// rows, which leaves the real block's factor and solution unchanged.
+// Linv[i, j] = x[BM-1-j] with L^T x = e_last.
+template <int BM, int FAM, int DS>
+__global__ __launch_bounds__(64) void factor_kernel(double var, double nugget, double nu, double norm,
+                                                   const double* __restrict__ sc,
+                                                   const int* __restrict__ nn, int n, int b,
+                                                   double* __restrict__ linv, int* __restrict__ fail) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  const int bs = min(i + 1, b);
+  double X[BM][DS];
+#pragma unroll
+  for (int r = 0; r < BM; ++r) {
+    const int j = BM - 1 - r;  // NNarray column feeding locsub row r
+    const int idx = (j < bs) ? nn[(size_t)i * b + j] : i;
+#pragma unroll
+    for (int k = 0; k < DS; ++k) X[r][k] = sc[(size_t)idx * DS + k];
+  }
+  constexpr int T = BM * (BM + 1) / 2;
+  double L[T];
+  double inv[BM];
+  bool bad = false;
+#pragma unroll
+  for (int t = 0; t < BM; ++t) {
+    const bool dt = (BM - 1 - t) >= bs;
+#pragma unroll
+    for (int q = 0; q <= t; ++q) {
+      const bool dq = (BM - 1 - q) >= bs;
+      double c;
+      if (q == t) {
+        c = dt ? 1.0 : var * (1.0 + nugget);
+      } else if (dt || dq) {
+        c = 0.0;
+      } else {
+        double s2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < DS; ++k) {
+          double u = X[t][k] - X[q][k];
+          s2 += u * u;
+        }
+        c = var * corr<FAM>(sqrt(s2), nu, norm);
+      }
+      double s = c;
+#pragma unroll
+      for (int p = 0; p < q; ++p) s -= L[t * (t + 1) / 2 + p] * L[q * (q + 1) / 2 + p];
+      if (q < t) {
+        L[t * (t + 1) / 2 + q] = s * inv[q];
+      } else {
+        if (!(s > 0.0)) { bad = true; s = 1.0; }
+        double l = sqrt(s);
+        L[t * (t + 1) / 2 + t] = l;
+        inv[t] = 1.0 / l;
+      }
+    }
+  }
+  double x[BM];
+  x[BM - 1] = inv[BM - 1];
+#pragma unroll
+  for (int r = BM - 2; r >= 0; --r) {
+    double s = 0.0;
+#pragma unroll
+    for (int q = r + 1; q < BM; ++q) s -= L[q * (q + 1) / 2 + r] * x[q];
+    x[r] = s * inv[r];
+  }
+  if (bad) atomicMin(fail, i + 1);
+#pragma unroll
+  for (int j = 0; j < BM; ++j)
+    if (j < b) linv[(size_t)i * b + j] = (j < bs) ? x[BM - 1 - j] : 0.0;
+}
+
+// Runtime-b variant (b <= 32, and the general Matern family whose Bessel
+// evaluation defeats full unrolling): same algorithm, private arrays indexed
+// at run time (held in scratch; correct for every b, slower than the
+// register-resident templates above).
+constexpr int kBMaxRt = 32;
+template <int FAM, int DS>
+__global__ __launch_bounds__(64) void factor_kernel_rt(double var, double nugget, double nu, double norm,
+                                                      const double* __restrict__ sc,
+                                                      const int* __restrict__ nn, int n, int b,
+                                                      double* __restrict__ linv, int* __restrict__ fail) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  const int bs = min(i + 1, b);
+  double X[kBMaxRt][DS];
+  double L[kBMaxRt * (kBMaxRt + 1) / 2];
+  double inv[kBMaxRt], x[kBMaxRt];
+  for (int r = 0; r < bs; ++r) {
+    const int idx = nn[(size_t)i * b + (bs - 1 - r)];
+    for (int k = 0; k < DS; ++k) X[r][k] = sc[(size_t)idx * DS + k];
+  }
+  bool bad = false;
+  for (int t = 0; t < bs; ++t) {
+    for (int q = 0; q <= t; ++q) {
+      double c;
+      if (q == t) {
+        c = var * (1.0 + nugget);
+      } else {
+        double s2 = 0.0;
+        for (int k = 0; k < DS; ++k) {
+          double u = X[t][k] - X[q][k];
+          s2 += u * u;
+        }
+        c = var * corr<FAM>(sqrt(s2), nu, norm);
+      }
+      double s = c;
+      for (int p = 0; p < q; ++p) s -= L[t * (t + 1) / 2 + p] * L[q * (q + 1) / 2 + p];
+      if (q < t) {
+        L[t * (t + 1) / 2 + q] = s * inv[q];
+      } else {
+        if (!(s > 0.0)) { bad = true; s = 1.0; }
+        double l = sqrt(s);
+        L[t * (t + 1) / 2 + t] = l;
+        inv[t] = 1.0 / l;
+      }
+    }
+  }
+  x[bs - 1] = inv[bs - 1];
+  for (int r = bs - 2; r >= 0; --r) {
+    double s = 0.0;
+    for (int q = r + 1; q < bs; ++q) s -= L[q * (q + 1) / 2 + r] * x[q];
+    x[r] = s * inv[r];
+  }
+  if (bad) atomicMin(fail, i + 1);
+  for (int j = 0; j < b; ++j) linv[(size_t)i * b + j] = (j < bs) ? x[bs - 1 - j] : 0.0;
+}
+
+#define NNGP_FACTOR_ARGS var, nugget, nu, norm, sc, nn, n, b, linv, fail
+template <int BM, int FAM>
+static hipError_t launch_factor_ds(hipStream_t st, int ds, double var, double nugget, double nu,
+                                   double norm, const double* sc, const int* nn, int n, int b,
+                                   double* linv, int* fail) {
+  int g = (n + 63) / 64;
+  switch (ds) {
+    case 2: hipLaunchKernelGGL((factor_kernel<BM, FAM, 2>), dim3(g), dim3(64), 0, st, NNGP_FACTOR_ARGS); break;
+    case 3: hipLaunchKernelGGL((factor_kernel<BM, FAM, 3>), dim3(g), dim3(64), 0, st, NNGP_FACTOR_ARGS); break;
+    case 4: hipLaunchKernelGGL((factor_kernel<BM, FAM, 4>), dim3(g), dim3(64), 0, st, NNGP_FACTOR_ARGS); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+template <int FAM>
+static hipError_t launch_factor_rt(hipStream_t st, int ds, double var, double nugget, double nu,
+                                   double norm, const double* sc, const int* nn, int n, int b,
+                                   double* linv, int* fail) {
+  int g = (n + 63) / 64;
+  switch (ds) {
+    case 2: hipLaunchKernelGGL((factor_kernel_rt<FAM, 2>), dim3(g), dim3(64), 0, st, NNGP_FACTOR_ARGS); break;
+    case 3: hipLaunchKernelGGL((factor_kernel_rt<FAM, 3>), dim3(g), dim3(64), 0, st, NNGP_FACTOR_ARGS); break;
+    case 4: hipLaunchKernelGGL((factor_kernel_rt<FAM, 4>), dim3(g), dim3(64), 0, st, NNGP_FACTOR_ARGS); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_factor(hipStream_t st, int family, double var, double nugget, double nu,
+                         const double* sc, int ds, const int* nn, int n, int b, double* linv,
+                         int* fail) {
+  double norm = 0.0;
+  if (b > kBMaxRt || b < 1) return hipErrorInvalidValue;
+  if (family == 2) {
+    norm = exp((1.0 - nu) * log(2.0) - lgamma(nu));
+    return launch_factor_rt<2>(st, ds, NNGP_FACTOR_ARGS);
+  }
+  if (b <= 16) {
+    if (family == 0) {
+      if (b <= 8) return launch_factor_ds<8, 0>(st, ds, NNGP_FACTOR_ARGS);
+      if (b <= 12) return launch_factor_ds<12, 0>(st, ds, NNGP_FACTOR_ARGS);
+      return launch_factor_ds<16, 0>(st, ds, NNGP_FACTOR_ARGS);
+    }
+    if (b <= 8) return launch_factor_ds<8, 1>(st, ds, NNGP_FACTOR_ARGS);
+    if (b <= 12) return launch_factor_ds<12, 1>(st, ds, NNGP_FACTOR_ARGS);
+    return launch_factor_ds<16, 1>(st, ds, NNGP_FACTOR_ARGS);
+  }
+  if (family == 0) return launch_factor_rt<0>(st, ds, NNGP_FACTOR_ARGS);
+  return launch_factor_rt<1>(st, ds, NNGP_FACTOR_ARGS);
+}
+#undef NNGP_FACTOR_ARGS
+
+// ------------------------------------------------------------------ reductions
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  return v;
+}
+
+// block of 256 threads: sum 4 values per thread into out[0..3] (thread 0)
+__device__ __forceinline__ void block_sum4(double v[4], double* out) {
+  __shared__ double sm[4][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    double s = wave_sum(v[k]);
+    if (lane == 0) sm[w][k] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) out[k] = ((sm[0][k] + sm[1][k]) + sm[2][k]) + sm[3][k];
+  }
+}
+
+__global__ __launch_bounds__(256) void row_stats_kernel(const double* __restrict__ linv,
+                                                        const int* __restrict__ nn, int n, int b,
+                                                        const double* __restrict__ x, double shift,
+                                                        double* __restrict__ out,
+                                                        const int* __restrict__ perm,
+                                                        double* __restrict__ partials,
+                                                        const double* __restrict__ shift_dev) {
+  if (shift_dev) shift = *shift_dev;
+  double acc[4] = {0, 0, 0, 0};
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+    const double* lr = linv + (size_t)k * b;
+    const int* nr = nn + (size_t)k * b;
+    double u = 0.0, a = 0.0;
+    for (int j = 0; j < b; ++j) {
+      int idx = nr[j];
+      if (idx < 0) continue;
+      double l = lr[j];
+      u += l * (x[idx] - shift);
+      a += l;
+    }
+    acc[0] += log(lr[0]);
+    acc[1] += u * u;
+    acc[2] += a * a;
+    acc[3] += a * u;
+    if (out) out[perm ? perm[k] : k] = u;
+  }
+  block_sum4(acc, partials + 4 * blockIdx.x);
+}
+
+int launch_row_stats(hipStream_t st, const double* linv, const int* nn, int n, int b,
+                     const double* x, double shift, double* out, const int* perm,
+                     double* partials, const double* shift_dev) {
+  int g = (n + kBlock - 1) / kBlock;
+  if (g > kRedBlocks) g = kRedBlocks;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(row_stats_kernel, dim3(g), dim3(kBlock), 0, st, linv, nn, n, b, x, shift, out,
+                     perm, partials, shift_dev);
+  return g;
+}
+
+__global__ __launch_bounds__(256) void reduce4_kernel(const double* __restrict__ partials,
+                                                      int nblocks, double* __restrict__ res) {
+  double acc[4] = {0, 0, 0, 0};
+  for (int p = threadIdx.x; p < nblocks; p += blockDim.x)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] += partials[4 * p + k];
+  block_sum4(acc, res);
+}
+
+hipError_t launch_reduce4(hipStream_t st, const double* partials, int nblocks, double* res) {
+  hipLaunchKernelGGL(reduce4_kernel, dim3(1), dim3(kBlock), 0, st, partials, nblocks, res);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ A5
+// refresh sweep-layout values of B from Linv and precision_diag per slot
+__global__ __launch_bounds__(256) void sell_refresh_kernel(const int* __restrict__ chunk_slot0,
+                                                           const long long* __restrict__ chunk_off,
+                                                           int nchunks, const int* __restrict__ collen,
+                                                           int n, const int* __restrict__ ent_src,
+                                                           const double* __restrict__ linv,
+                                                           double* __restrict__ ent_val,
+                                                           double* __restrict__ D_slot) {
+  const int ch = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (ch >= nchunks) return;
+  const int s = chunk_slot0[ch] + lane;
+  if (s >= n) return;
+  // slot s belongs to this chunk only if it is below the next chunk's first slot
+  if (ch + 1 < nchunks && s >= chunk_slot0[ch + 1]) return;
+  const int len = collen[s];
+  const long long base = chunk_off[ch] + lane;
+  double D = 0.0;
+  for (int j = 0; j < len; ++j) {
+    long long e = base + (long long)j * 64;
+    double v = linv[ent_src[e]];
+    ent_val[e] = v;
+    D += v * v;
+  }
+  D_slot[s] = D;
+}
+
+hipError_t launch_sell_refresh(hipStream_t st, const int* chunk_slot0, const long long* chunk_off,
+                               int nchunks, const int*, const int* collen, int n, const int* ent_src,
+                               const double* linv, double* ent_val, double* D_slot) {
+  int g = (nchunks + 3) / 4;
+  hipLaunchKernelGGL(sell_refresh_kernel, dim3(g), dim3(kBlock), 0, st, chunk_slot0, chunk_off,
+                     nchunks, collen, n, ent_src, linv, ent_val, D_slot);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ A7
+__global__ void residual_sums_kernel(int n, const int* __restrict__ slot_loc,
+                                     const int* __restrict__ obs_ptr, const int* __restrict__ obs_idx,
+                                     const double* __restrict__ y, const double* __restrict__ mu,
+                                     double beta0, double* __restrict__ R_slot) {
+  int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  int loc = slot_loc[s];
+  double R = 0.0;
+  for (int p = obs_ptr[loc]; p < obs_ptr[loc + 1]; ++p) {
+    int o = obs_idx[p];
+    R += y[o] - (mu ? mu[o] : beta0);
+  }
+  R_slot[s] = R;
+}
+
+hipError_t launch_residual_sums(hipStream_t st, int n, const int* slot_loc, const int* obs_ptr,
+                                const int* obs_idx, const double* y, const double* mu,
+                                double beta0, double* R_slot) {
+  int g = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(residual_sums_kernel, dim3(g), dim3(kBlock), 0, st, n, slot_loc, obs_ptr,
+                     obs_idx, y, mu, beta0, R_slot);
+  return hipGetLastError();
+}
+
+__global__ void field_to_slots_kernel(int n, const int* __restrict__ slot_loc,
+                                      const double* __restrict__ field,
+                                      const SweepScalars* __restrict__ sc, double* __restrict__ w) {
+  int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < n) w[s] = field[slot_loc[s]] - sc->beta0;
+}
+__global__ void slots_to_field_kernel(int n, const int* __restrict__ slot_loc,
+                                      const double* __restrict__ w,
+                                      const SweepScalars* __restrict__ sc, double* __restrict__ field) {
+  int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < n) field[slot_loc[s]] = w[s] + sc->beta0;
+}
+
+hipError_t launch_field_to_slots(hipStream_t st, int n, const int* slot_loc, const double* field,
+                                 const SweepScalars* sc, double* w_slot) {
+  int g = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(field_to_slots_kernel, dim3(g), dim3(kBlock), 0, st, n, slot_loc, field, sc, w_slot);
+  return hipGetLastError();
+}
+hipError_t launch_slots_to_field(hipStream_t st, int n, const int* slot_loc, const double* w_slot,
+                                 const SweepScalars* sc, double* field) {
+  int g = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(slots_to_field_kernel, dim3(g), dim3(kBlock), 0, st, n, slot_loc, w_slot, sc, field);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ A1
+// One colour of the chromatic sweep, local form.  One wavefront per chunk
+// of 64 same-colour slots, one lane per location:
+//   acc  = sum_{k in col(i)} B[k,i] r_k - D_i w_i      (= (B^T B w_{!c})_i)
+//   P    = D_i/s2 + n_i/t2
+//   w_i' = (R_i/t2 - acc/s2)/P + z_i/sqrt(P)
+//   r_k += B[k,i] (w_i' - w_i)                          (conflict-free in a colour)
+// Blocks are remapped so that consecutive (spatially adjacent) chunks run on
+// the same XCD and share its L2 for the r gathers.
+template <bool INJECT>
+__global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, int chunk_begin, int nchunks_color,
+                                                          int slot_end,
+                                                          const SweepScalars* __restrict__ scal,
+                                                          int sweep_local, const double* __restrict__ z,
+                                                          int n) {
+  const int nb = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nb >> 3, rm = nb & 7;
+  const int lb = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + (bid >> 3);
+  const int lch = lb * 4 + (threadIdx.x >> 6);
+  if (lch >= nchunks_color) return;
+  const int lane = threadIdx.x & 63;
+  const int ch = chunk_begin + lch;
+  const int s = L.chunk_slot0[ch] + lane;
+  const bool valid = s < slot_end;
+  const int len = valid ? L.collen[s] : 0;
+  const int clen = L.chunk_len[ch];
+  const double* __restrict__ vp = L.ent_val + L.chunk_off[ch] + lane;
+  const int* __restrict__ pp = L.ent_rowpos + L.chunk_off[ch] + lane;
+  const double* r = L.r;  // r is also written below: no __restrict__
+
+  double acc = 0.0;
+  int j = 0;
+  for (; j + 4 <= clen; j += 4) {
+    double v0 = vp[(j + 0) * 64], v1 = vp[(j + 1) * 64], v2 = vp[(j + 2) * 64], v3 = vp[(j + 3) * 64];
+    int p0 = pp[(j + 0) * 64], p1 = pp[(j + 1) * 64], p2 = pp[(j + 2) * 64], p3 = pp[(j + 3) * 64];
+    double r0 = r[p0], r1 = r[p1], r2 = r[p2], r3 = r[p3];
+    acc += (j + 0 < len) ? v0 * r0 : 0.0;
+    acc += (j + 1 < len) ? v1 * r1 : 0.0;
+    acc += (j + 2 < len) ? v2 * r2 : 0.0;
+    acc += (j + 3 < len) ? v3 * r3 : 0.0;
+  }
+  for (; j < clen; ++j) {
+    double v = vp[j * 64];
+    int p = pp[j * 64];
+    double rv = r[p];
+    acc += (j < len) ? v * rv : 0.0;
+  }
+  if (!valid) return;
+  const double inv_s2 = scal->inv_s2, inv_t2 = scal->inv_t2;
+  const double D = L.D_slot[s];
+  const double w = L.w_slot[s];
+  acc -= D * w;
+  const double P = D * inv_s2 + (double)L.nobs_slot[s] * inv_t2;
+  const int loc = L.slot_loc[s];
+  double zz;
+  if (INJECT) zz = z[(size_t)sweep_local * n + loc];
+  else zz = normal_at(scal->seed, scal->counter_base + (uint64_t)sweep_local, (uint32_t)loc);
+  const double wn = (inv_t2 * L.R_slot[s] - inv_s2 * acc) / P + zz / sqrt(P);
+  const double dw = wn - w;
+  L.w_slot[s] = wn;
+  double* rw = L.r;
+  for (int jj = 0; jj < len; ++jj) {
+    int p = pp[jj * 64];
+    rw[p] += vp[jj * 64] * dw;
+  }
+}
+
+hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, int chunk_begin, int nchunks_color,
+                              int slot_end, const SweepScalars* sc, int sweep_local,
+                              const double* z, int n) {
+  int g = (nchunks_color + 3) / 4;
+  if (z)
+    hipLaunchKernelGGL((sweep_color_kernel<true>), dim3(g), dim3(kBlock), 0, st, L, chunk_begin,
+                       nchunks_color, slot_end, sc, sweep_local, z, n);
+  else
+    hipLaunchKernelGGL((sweep_color_kernel<false>), dim3(g), dim3(kBlock), 0, st, L, chunk_begin,
+                       nchunks_color, slot_end, sc, sweep_local, z, n);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ A8
+__global__ __launch_bounds__(256) void obs_reduce_kernel(int mode, int n_obs, const double* __restrict__ y,
+                                                         const double* __restrict__ mu, double beta0,
+                                                         const int* __restrict__ lm,
+                                                         const double* __restrict__ f,
+                                                         const double* __restrict__ fnew,
+                                                         double inv_2var, double* __restrict__ partials) {
+  double acc[4] = {0, 0, 0, 0};
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < n_obs; o += gridDim.x * blockDim.x) {
+    double m = mu ? mu[o] : beta0;
+    int loc = lm[o];
+    if (mode == 0) {
+      double e = y[o] - f[loc] - m + beta0;
+      acc[0] += e * e;
+    } else {
+      double ea = y[o] - (fnew[loc] + m - beta0);
+      double eb = y[o] - (f[loc] + m - beta0);
+      acc[0] += (eb * eb - ea * ea) * inv_2var;
+    }
+  }
+  block_sum4(acc, partials + 4 * blockIdx.x);
+}
+
+int launch_obs_reduce(hipStream_t st, int mode, int n_obs, const double* y, const double* mu,
+                      double beta0, const int* lm, const double* field, const double* field_new,
+                      double inv_2var, double* partials) {
+  int g = (n_obs + kBlock - 1) / kBlock;
+  if (g > kRedBlocks) g = kRedBlocks;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(obs_reduce_kernel, dim3(g), dim3(kBlock), 0, st, mode, n_obs, y, mu, beta0, lm,
+                     field, field_new, inv_2var, partials);
+  return g;
+}
+
+// ------------------------------------------------------------------ tri solve
+__global__ void tri_level_kernel(const int* __restrict__ rows, int nrows, const double* __restrict__ linv,
+                                 const int* __restrict__ nn, int b, const double* __restrict__ u,
+                                 double* __restrict__ x) {
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nrows) return;
+  int i = rows[t];
+  const double* lr = linv + (size_t)i * b;
+  const int* nr = nn + (size_t)i * b;
+  double s = u[i];
+  for (int j = 1; j < b; ++j) {
+    int idx = nr[j];
+    if (idx >= 0) s -= lr[j] * x[idx];
+  }
+  x[i] = s / lr[0];
+}
+
+hipError_t launch_tri_level(hipStream_t st, const int* rows, int nrows, const double* linv,
+                            const int* nn, int b, const double* u, double* x) {
+  int g = (nrows + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(tri_level_kernel, dim3(g), dim3(kBlock), 0, st, rows, nrows, linv, nn, b, u, x);
+  return hipGetLastError();
+}
+
+__global__ void axpby_shift_kernel(int n, const double* __restrict__ x, double scale, double shift,
+                                   double* __restrict__ y) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = shift + scale * x[i];
+}
+
+hipError_t launch_axpby_shift(hipStream_t st, int n, const double* x, double scale, double shift,
+                              double* y) {
+  int g = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(axpby_shift_kernel, dim3(g), dim3(kBlock), 0, st, n, x, scale, shift, y);
+  return hipGetLastError();
+}
+
+hipError_t launch_normals(hipStream_t st, uint64_t seed, uint64_t sweep, int n, double* z) {
+  int g = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(normals_kernel, dim3(g), dim3(kBlock), 0, st, seed, sweep, n, z);
+  return hipGetLastError();
+}
+
+}  // namespace nngp

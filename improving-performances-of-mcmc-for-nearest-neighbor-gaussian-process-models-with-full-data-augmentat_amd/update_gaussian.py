@@ -1,0 +1,225 @@
+"""mcmc_nngp_update_Gaussian -- host mirror of
+Scripts/mcmc_nngp_update_Gaussian.R:14-317 (and ll_compressed_sparse_chol,
+:8-12).
+
+The scalar Metropolis-Hastings / adaptation logic stays on the
+host exactly as in the reference; every O(n) / O(nnz) array operation is a
+call into the device context of the chain:
+
+=====================================  =====================================
+reference (update_Gaussian.R)          device call (include/nngp.h)
+=====================================  =====================================
+vecchia_Linv + sparseMatrix :72-73     ctx.factor(0, ...)
+precision_diag :74,142,197             (inside nngp_factor / nngp_accept_factor)
+vecchia_Linv :123 / :179               ctx.factor(1, ...)
+solve(new_B, B %*% (field-b0)) :127    ctx.ancillary_propose
+sum(dnorm(.)) - sum(dnorm(.)) :129-131 ctx.field_response_ratio
+ll_compressed_sparse_chol :184-186     ctx.loglik(1, .) - ctx.loglik(0, .)
+crossprod(B 1), (B f, B 1) :221-222    ctx.beta0_stats
+residuals_sum + chromatic loop :257-275 ctx.sweep(n_chromatic, ...)
+sum_squared_residuals :281             ctx.sum_squared_residuals
+sparse_chol %*% X :79,82,147,241       ctx.spmv
+=====================================  =====================================
+
+Chains are contexts (one per chain, possibly on distinct devices) instead of
+forked ``mclapply`` workers: HIP must never be initialised before a fork.
+Seeds: numpy PCG64 seeded with ``iter_start + i`` (the reference's
+``set.seed(iter_start + i)``, :34-36); the chromatic sweep's normals come from
+the device Philox stream keyed by the same value, so a resumed run is
+reproducible.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .context import ChainContext
+from .model import covparms
+
+
+def ll_compressed_sparse_chol(ctx: ChainContext, which: int, beta0: float, log_scale: float) -> float:
+    """Vecchia log-likelihood of field - beta_0 (update_Gaussian.R:8-12)."""
+    return ctx.loglik(which, beta0, log_scale)
+
+
+def _philox_key(iter_start: int, chain: int, seed: int) -> int:
+    return ((int(seed) & 0xFFFFFFFF) << 32) ^ ((int(iter_start) + int(chain)) & 0xFFFFFFFF) ^ 0x9E3779B97F4A7C15
+
+
+def _interweave_prep(ctx, X, va):
+    """beta_interweaved_* (update_Gaussian.R:77-83,145-151)."""
+    Xl = X["X"][va["hctam_scol_1"] - 1][:, X["locs"]]
+    M = np.column_stack([np.ones(va["n_locs"]), Xl])
+    SX = ctx.spmv(0, M)
+    prec = SX.T @ SX
+    cov = np.linalg.inv(prec)
+    return {"Xl": Xl, "SX": SX, "covmat": cov, "covmat_chol": np.linalg.cholesky(cov).T}
+
+
+def _run_chain(i, state, ctx, X, observed_field, space_time_model, va, n_iterations_update,
+               field_thinning, ancillary, n_chromatic, iter_start, seed):
+    rng = np.random.default_rng(int(iter_start) + i + 1)
+    key = _philox_key(iter_start, i + 1, seed)
+    covfun = space_time_model["covfun"]["stationary_covfun"]
+    sp_names = space_time_model["covfun"]["shape_params"]
+    params = {k: (np.array(v, copy=True) if isinstance(v, np.ndarray) else v) for k, v in state["params"].items()}
+    tk = {k: dict(v) for k, v in state["transition_kernels"].items()}
+    n_obs = va["n_obs"]
+    var_y = float(np.var(observed_field, ddof=1))
+    has_X = X.get("X") is not None
+    has_locs = has_X and len(X["locs"]) > 0
+    n_shape = len(sp_names)
+
+    rec = {"beta_0": np.zeros((n_iterations_update, 1)),
+           "log_scale": np.zeros((n_iterations_update, 1)),
+           "log_noise_variance": np.zeros((n_iterations_update, 1)),
+           "shape": np.zeros((n_iterations_update, n_shape)),
+           "field": np.zeros((int(round(n_iterations_update * field_thinning)), va["n_locs"]))}
+    if has_X:
+        rec["beta"] = np.zeros((n_iterations_update, X["X"].shape[1]))
+    acc_suf = np.zeros(n_iterations_update)
+    acc_anc = np.zeros(n_iterations_update)
+
+    # Vecchia factor of the current state (:67-74)
+    ctx.factor(0, covfun, covparms(sp_names, params["shape"]))
+    ctx.set_field(params["field"])
+    iw = _interweave_prep(ctx, X, va) if has_locs else None
+
+    def mu_of():
+        if has_X:
+            return params["beta_0"] + X["X"] @ params["beta"]
+        return None
+
+    ctx.set_mu(mu_of(), params["beta_0"])
+    adapt = 0 <= iter_start <= 2000
+
+    for it in range(1, n_iterations_update + 1):
+        # ---- ancillary covariance update (:113-157)
+        if ancillary:
+            innov = rng.normal(0.0, np.exp(0.5 * tk["covariance_params_ancillary"]["logvar"]), n_shape + 1)
+            new_ls = params["log_scale"] + innov[0]
+            new_shape = params["shape"] + innov[1:]
+            ok = True
+            try:
+                ctx.factor(1, covfun, covparms(sp_names, new_shape))
+            except Exception:
+                ok = False  # non-PD local covariance: the proposal is rejected
+            if ok:
+                ctx.ancillary_propose(params["beta_0"], new_ls - params["log_scale"])
+                ratio = ctx.field_response_ratio(params["beta_0"], params["log_noise_variance"])
+                if ratio > np.log(rng.uniform()):
+                    params["shape"] = new_shape
+                    params["log_scale"] = new_ls
+                    ctx.accept_field()
+                    ctx.accept_factor()
+                    acc_anc[it - 1] = 1
+                    if has_locs:
+                        iw = _interweave_prep(ctx, X, va)
+            if adapt and it % 25 == 0:
+                a = acc_anc[it - 25:it].mean()
+                if a < 0.05:
+                    tk["covariance_params_ancillary"]["logvar"] -= rng.normal(0.4, 0.05)
+                if a > 0.15:
+                    tk["covariance_params_ancillary"]["logvar"] += rng.normal(0.4, 0.05)
+
+        # ---- sufficient covariance update (:165-213)
+        innov = rng.normal(0.0, np.exp(0.5 * tk["covariance_params_sufficient"]["logvar"]), n_shape + 1)
+        new_ls = params["log_scale"] + innov[0]
+        if np.exp(new_ls) < var_y:
+            new_shape = params["shape"] + innov[1:]
+            ok = True
+            try:
+                ctx.factor(1, covfun, covparms(sp_names, new_shape))
+            except Exception:
+                ok = False
+            if ok:
+                gp_ratio = (ctx.loglik(1, params["beta_0"], new_ls)
+                            - ctx.loglik(0, params["beta_0"], params["log_scale"]))
+                if gp_ratio > np.log(rng.uniform()):
+                    params["shape"] = new_shape
+                    params["log_scale"] = new_ls
+                    ctx.accept_factor()
+                    acc_suf[it - 1] = 1
+                    if has_locs:
+                        iw = _interweave_prep(ctx, X, va)
+        if adapt and it % 25 == 0:
+            a = acc_suf[it - 25:it].mean()
+            if a < 0.05:
+                tk["covariance_params_sufficient"]["logvar"] -= rng.normal(0.2, 0.05)
+            if a > 0.15:
+                tk["covariance_params_sufficient"]["logvar"] += rng.normal(0.2, 0.05)
+
+        # ---- field mean (:219-247)
+        if (not has_locs) or (not has_X):
+            oqo, oqf = ctx.beta0_stats()
+            beta_covmat = np.exp(params["log_scale"]) / oqo
+            beta_mean = np.exp(-params["log_scale"]) * oqf * beta_covmat
+            params["beta_0"] = float(beta_mean + np.sqrt(beta_covmat) * rng.normal())
+        if has_X:
+            field = ctx.get_field()
+            X1 = np.column_stack([np.ones(n_obs), X["X"]])
+            resid = observed_field - field[va["locs_match"] - 1] + params["beta_0"]
+            beta_mean = (resid @ X1) @ X["solve_1XT1X"]
+            innov = beta_mean + np.exp(0.5 * params["log_noise_variance"]) * (
+                X["chol_solve_1XT1X"].T @ rng.normal(size=X1.shape[1]))
+            field = field - params["beta_0"] + innov[0]
+            params["beta_0"] = float(innov[0])
+            params["beta"] = innov[1:].copy()
+            if has_locs:
+                locs_cols = X["locs"]
+                other = field + iw["Xl"] @ params["beta"][locs_cols]
+                Bo = ctx.spmv(0, other)
+                bm = iw["covmat"] @ (Bo @ iw["SX"])
+                innov = bm + np.exp(0.5 * params["log_scale"]) * (iw["covmat_chol"].T @ rng.normal(size=len(locs_cols) + 1))
+                params["beta_0"] = float(innov[0])
+                params["beta"][locs_cols] = innov[1:]
+                field = other - iw["Xl"] @ params["beta"][locs_cols]
+            ctx.set_field(field)
+        ctx.set_mu(mu_of(), params["beta_0"])
+
+        # ---- chromatic sampling of the field (:257-275)
+        ctx.sweep(n_chromatic, params["beta_0"], params["log_scale"], params["log_noise_variance"],
+                  key, (int(iter_start) + it - 1) * n_chromatic)
+
+        # ---- noise variance (:281-293)
+        ssr = ctx.sum_squared_residuals(params["beta_0"])
+        for _ in range(10):
+            innov = rng.normal(0.0, 0.01)
+            if np.exp(params["log_noise_variance"] + innov) < var_y:
+                lnv = params["log_noise_variance"]
+                if -0.5 * n_obs * innov - 0.5 * ssr * (np.exp(-lnv - innov) - np.exp(-lnv)) > np.log(rng.uniform()):
+                    params["log_noise_variance"] = lnv + innov
+
+        # ---- records (:305-311)
+        if has_X:
+            rec["beta"][it - 1] = params["beta"]
+        rec["beta_0"][it - 1] = params["beta_0"]
+        rec["log_noise_variance"][it - 1] = params["log_noise_variance"]
+        rec["log_scale"][it - 1] = params["log_scale"]
+        rec["shape"][it - 1] = params["shape"]
+        if round(it * field_thinning) == it * field_thinning:
+            rec["field"][int(it * field_thinning) - 1] = ctx.get_field()
+
+    params["field"] = ctx.get_field()
+    return {"state": {"params": params, "transition_kernels": tk}, "records": rec,
+            "acceptance": {"covariance_acceptance_sufficient": acc_suf,
+                           "covariance_acceptance_ancillary": acc_anc}}
+
+
+def mcmc_nngp_update_Gaussian(locs, X, observed_field, space_time_model, vecchia_approx, states,
+                              n_iterations_update, n_cores=None, field_thinning=1.0, ancillary=True,
+                              n_chromatic=10, iterations=None, contexts=None, seed=1, devices=None):
+    """Returns one {"state", "records"} per chain (update_Gaussian.R:315)."""
+    iter_start = int(iterations[-1, 0]) if iterations is not None else 0
+    names = list(states.keys()) if isinstance(states, dict) else [f"chain_{i + 1}" for i in range(len(states))]
+    st_list = list(states.values()) if isinstance(states, dict) else list(states)
+    if contexts is None:
+        devices = devices or [-1]
+        contexts = [ChainContext(locs, vecchia_approx["NNarray"], vecchia_approx["coloring"],
+                                 vecchia_approx["locs_match"], observed_field, device=devices[i % len(devices)])
+                    for i in range(len(st_list))]
+    out = {}
+    for i, (nm, st) in enumerate(zip(names, st_list)):
+        out[nm] = _run_chain(i, st, contexts[i], X, np.asarray(observed_field, np.float64), space_time_model,
+                             vecchia_approx, int(n_iterations_update), float(field_thinning), bool(ancillary),
+                             int(n_chromatic), iter_start, seed)
+    return out

@@ -1,0 +1,171 @@
+/*
+ * nngp.h -- C ABI of the MI355X-native NNGP chromatic-Gibbs hot path.
+ *
+ * Drop-in boundary for the reference's L1/L0 calls on the hot path (SURVEY.md
+ * §8b).  Plain pointers and sizes only; no torch / C++ types cross it.  All
+ * host arrays use R's conventions: matrices column-major, indices 1-based,
+ * NA_integer_ == INT_MIN.  Every entry point returns 0 (NNGP_OK) or an
+ * nngp_status; a context keeps the message of its last error
+ * (nngp_ctx_last_error).  Host inputs are read-only for the call; outputs are
+ * caller-allocated.  Device state is owned by the context and freed only by
+ * nngp_ctx_destroy.  Calls on one context are serialised by the caller;
+ * distinct contexts may live on distinct devices.  HIP is initialised lazily
+ * by nngp_ctx_create: never fork() after it (replaces parallel::mclapply,
+ * Scripts/mcmc_nngp_update_Gaussian.R:25, by one context per chain).
+ *
+ * Reference interface each entry point replaces (path:line under the
+ * reference tree):
+ *   nngp_order_maxmin ........ GpGp::order_maxmin, Scripts/mcmc_nngp_initialize.R:29
+ *   nngp_find_ordered_nn ..... GpGp::find_ordered_nn, Scripts/mcmc_nngp_initialize.R:93
+ *   nngp_greedy_coloring ..... moral graph Scripts/mcmc_nngp_initialize.R:97-109 +
+ *                              naive_greedy_coloring Scripts/Coloring.R:2-20
+ *   nngp_factor .............. GpGp::vecchia_Linv + Matrix::sparseMatrix,
+ *                              Scripts/mcmc_nngp_update_Gaussian.R:72-73,123-124,179-180
+ *   nngp_accept_factor ....... precision_diag refresh, update_Gaussian.R:140-142,195-197
+ *   nngp_loglik .............. ll_compressed_sparse_chol (+GpGp::Linv_mult),
+ *                              Scripts/mcmc_nngp_update_Gaussian.R:8-12,184-186
+ *   nngp_set_mu .............. mu + residuals_sum, update_Gaussian.R:85-90,249-250,260
+ *   nngp_sweep ............... chromatic sampling, update_Gaussian.R:257-275
+ *   nngp_ancillary_propose ... new_field, update_Gaussian.R:127 (SpMV + sparse
+ *                              triangular solve)
+ *   nngp_field_response_ratio  dnorm ratio, update_Gaussian.R:129-131
+ *   nngp_beta0_stats ......... beta_0 Gibbs block, update_Gaussian.R:221-222
+ *   nngp_sum_squared_residuals update_Gaussian.R:281
+ *   nngp_spmv / nngp_tri_solve sparse_chol %*% X (update_Gaussian.R:79,147) /
+ *                              Matrix::solve (initialize.R:208, predict.R:46)
+ */
+#ifndef NNGP_H_
+#define NNGP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NNGP_ABI_VERSION 1
+
+typedef enum {
+  NNGP_OK = 0,
+  NNGP_ERR_ARG = 1,     /* invalid argument / shape */
+  NNGP_ERR_HIP = 2,     /* HIP runtime error (message in the context) */
+  NNGP_ERR_CHOL = 3,    /* local covariance not positive definite */
+  NNGP_ERR_STATE = 4,   /* call out of order (e.g. sweep before factor) */
+  NNGP_ERR_NOMEM = 5,   /* host or device allocation failed */
+  NNGP_ERR_NODEV = 6,   /* no HIP device available */
+  NNGP_ERR_COMM = 7     /* RCCL error */
+} nngp_status;
+
+/* Covariance functions (GpGp names; covparms = c(variance, shape..., nugget)). */
+typedef enum {
+  NNGP_EXPONENTIAL_ISOTROPIC = 0, /* (var, range, nugget)                */
+  NNGP_EXPONENTIAL_SPHERE = 1,    /* (var, range[Earth radii], nugget)   */
+  NNGP_EXPONENTIAL_SCALEDIM = 2,  /* (var, range_1..range_d, nugget)     */
+  NNGP_EXPONENTIAL_SPACETIME = 3, /* (var, range_space, range_time, nug) */
+  NNGP_MATERN_ISOTROPIC = 4,      /* (var, range, smoothness, nugget)    */
+  NNGP_MATERN_SPHERE = 5,         /* (var, range, smoothness, nugget)    */
+  NNGP_MATERN_SCALEDIM = 6,       /* (var, range_1..range_d, smooth, nug)*/
+  NNGP_MATERN_SPACETIME = 7,      /* (var, r_space, r_time, smooth, nug) */
+  NNGP_MATERN15_ISOTROPIC = 8     /* (var, range, nugget); extension     */
+} nngp_covfun;
+
+typedef struct nngp_ctx nngp_ctx;
+
+typedef struct {
+  int n;           /* locations */
+  int b;           /* m + 1 */
+  int d;           /* coordinate dimension */
+  int n_obs;       /* observations */
+  int n_colors;    /* K */
+  int n_levels;    /* depth of the Vecchia DAG (triangular solve) */
+  long long nnz;   /* nonzeros of B */
+  long long n_entries; /* sliced-ELL entries incl. padding */
+  int max_collen;  /* longest column of B */
+  int device;      /* HIP device ordinal */
+} nngp_info;
+
+/* ---------- library ---------- */
+int nngp_abi_version(void);
+const char* nngp_status_string(int status);
+
+/* ---------- host-side graph preparation (init-time, C++) ---------- */
+/* locs: n x d column-major.  order: 1-based permutation (length n). */
+int nngp_order_maxmin(const double* locs, int n, int d, int* order);
+/* NNarray: n x (m+1) column-major, 1-based, NA = INT_MIN. Exact NN on the raw
+ * coordinates, ties broken by the smaller index. */
+int nngp_find_ordered_nn(const double* locs, int n, int d, int m, int* NNarray);
+/* coloring: length n, 1-based colours; *n_colors = K. */
+int nngp_greedy_coloring(const int* NNarray, int n, int b, int* coloring, int* n_colors);
+
+/* ---------- device context ---------- */
+/* locs n x d col-major (ordered); NNarray n x b col-major 1-based (NA=INT_MIN);
+ * coloring 1-based (length n); locs_match 1-based (length n_obs);
+ * observed_field length n_obs.  device: HIP ordinal (-1: current). */
+int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
+                    const int* coloring, const int* locs_match,
+                    const double* observed_field, int n_obs, int device,
+                    nngp_ctx** out);
+void nngp_ctx_destroy(nngp_ctx* ctx);
+const char* nngp_ctx_last_error(const nngp_ctx* ctx);
+int nngp_ctx_info(const nngp_ctx* ctx, nngp_info* info);
+
+/* Vecchia factor (A4).  which: 0 = current factor, 1 = proposal. */
+int nngp_factor(nngp_ctx* ctx, int which, int covfun, const double* covparms, int ncovparms);
+/* copy a factor out as GpGp's Linv (n x b column-major, unfilled entries 0) */
+int nngp_get_linv(nngp_ctx* ctx, int which, double* Linv);
+/* upload an externally computed Linv (n x b col-major) into `which` */
+int nngp_set_linv(nngp_ctx* ctx, int which, const double* Linv);
+/* proposal factor becomes current; refreshes the sweep values + precision_diag (A5) */
+int nngp_accept_factor(nngp_ctx* ctx);
+/* precision_diag = colSums(B o B) of the current factor (length n) */
+int nngp_get_precision_diag(nngp_ctx* ctx, double* D);
+
+/* latent field (length n, location order) */
+int nngp_set_field(nngp_ctx* ctx, const double* field);
+int nngp_get_field(nngp_ctx* ctx, double* field);
+/* mu (length n_obs): beta_0 + X beta; recomputes residuals_sum (A7).
+ * mu == NULL means mu = beta0 for every observation. */
+int nngp_set_mu(nngp_ctx* ctx, const double* mu, double beta0);
+
+/* Vecchia log-likelihood (A6) of z = field - beta0 under factor `which` */
+int nngp_loglik(nngp_ctx* ctx, int which, double beta0, double log_scale, double* ll);
+
+/* n_sweeps chromatic sweeps (A1).  Normals: Philox4x32-10 with key = seed,
+ * counter = (location, counter_base + sweep, 0x5EED) unless z != NULL, in which
+ * case z (n_sweeps x n row-major, z[s*n + i]) supplies them. */
+int nngp_sweep(nngp_ctx* ctx, int n_sweeps, double beta0, double log_scale,
+               double log_noise_variance, uint64_t seed, uint64_t counter_base,
+               const double* z);
+
+/* Ancillary proposal: proposal field = beta0 + exp(0.5*dlog_scale) *
+ * B_prop^{-1} (B_cur (field - beta0)) (update_Gaussian.R:127). */
+int nngp_ancillary_propose(nngp_ctx* ctx, double beta0, double dlog_scale);
+/* sum dnorm(y | proposal) - sum dnorm(y | field), sd = exp(lnv/2) (A8) */
+int nngp_field_response_ratio(nngp_ctx* ctx, double beta0, double log_noise_variance,
+                              double* ratio);
+/* proposal field becomes current */
+int nngp_accept_field(nngp_ctx* ctx);
+/* 1'B'B1 and 1'B'B field (current factor) -- beta_0 Gibbs (update_Gaussian.R:221-222) */
+int nngp_beta0_stats(nngp_ctx* ctx, double* ones_Q_ones, double* ones_Q_field);
+/* sum (y - field[loc] - mu + beta0)^2 (update_Gaussian.R:281) */
+int nngp_sum_squared_residuals(nngp_ctx* ctx, double beta0, double* ssr);
+/* Y = B X for X n x ncols column-major (host buffers) */
+int nngp_spmv(nngp_ctx* ctx, int which, const double* X, int ncols, double* Y);
+/* x = B^{-1} u (host buffers, length n) */
+int nngp_tri_solve(nngp_ctx* ctx, int which, const double* u, double* x);
+
+/* ---------- measurement ---------- */
+/* Runs n_sweeps sweeps on the context's stream bracketed by HIP events;
+ * *ms = elapsed; per-colour-kernel durations are summed into *kernel_ms when
+ * kernel_ms != NULL (each colour launch bracketed by its own events). */
+int nngp_sweep_timed(nngp_ctx* ctx, int n_sweeps, double beta0, double log_scale,
+                     double log_noise_variance, uint64_t seed, uint64_t counter_base,
+                     double* ms, double* kernel_ms);
+/* Philox normals generated by the device code path (test hook). */
+int nngp_device_normals(int device, uint64_t seed, uint64_t sweep, int n, double* z);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NNGP_H_ */

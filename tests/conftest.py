@@ -1,0 +1,56 @@
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "oracle"))
+GOLDEN = ROOT / "tests" / "golden"
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (runs the HIP path)")
+    config.addinivalue_line("markers", "slow: long statistical test")
+
+
+@pytest.fixture(scope="session")
+def P():
+    import _pkgload
+
+    return _pkgload.load()
+
+
+@pytest.fixture(scope="session")
+def O():
+    import oracle
+
+    return oracle
+
+
+@pytest.fixture(scope="session")
+def printed():
+    return json.loads((GOLDEN / "vignette_printed.json").read_text())
+
+
+@pytest.fixture(scope="session")
+def toy():
+    return dict(np.load(GOLDEN / "vignette_toy.npz"))
+
+
+def make_problem(P, n, m, d=2, seed=0, order=True, dup_frac=0.0):
+    """Synthetic ordered locations + NNarray + colouring (+ duplicated obs)."""
+    rng = np.random.default_rng(seed)
+    locs = rng.uniform(size=(n, d))
+    if order:
+        locs = locs[P.order_maxmin(locs) - 1]
+    NN = P.find_ordered_nn(locs, m)
+    col = P.naive_greedy_coloring(NN)
+    lm = np.arange(1, n + 1, dtype=np.int32)
+    if dup_frac > 0:
+        extra = rng.choice(n, int(dup_frac * n), replace=False) + 1
+        lm = np.concatenate([lm, extra.astype(np.int32)])
+    y = rng.normal(size=len(lm))
+    return locs, NN, col, lm, y

@@ -1,0 +1,118 @@
+"""CPU-side checks of the product library: it loads, exports every symbol
+the C ABI header declares, and its host-side graph preparation is bit-exact
+against the oracle (no GPU compute is called here)."""
+import ctypes as C
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def test_header_symbols_exported(P):
+    hdr = (ROOT / "include" / "nngp.h").read_text()
+    declared = set(re.findall(r"\b(nngp_[a-z0-9_]+)\s*\(", hdr))
+    from nngp_amd import _lib
+
+    assert declared == set(_lib.ABI_SYMBOLS)
+    lib = C.CDLL(str(_lib.LIB_PATH))
+    for s in sorted(declared):
+        assert hasattr(lib, s), s
+    assert P.lib.nngp_abi_version() == 1
+
+
+def test_library_has_gfx950_code_object():
+    from nngp_amd import _lib
+
+    blob = Path(_lib.LIB_PATH).read_bytes()
+    assert b"gfx950" in blob
+
+
+@pytest.mark.parametrize("n,d,m,seed", [(1, 2, 3, 0), (2, 2, 3, 0), (7, 2, 10, 1), (500, 2, 5, 2),
+                                        (3000, 2, 10, 3), (2000, 3, 15, 4), (1500, 1, 4, 5),
+                                        (800, 4, 8, 6), (2500, 2, 30, 7)])
+def test_graph_prep_bit_exact_vs_oracle(P, O, n, d, m, seed):
+    rng = np.random.default_rng(seed)
+    locs = rng.uniform(size=(n, d))
+    o1 = P.order_maxmin(locs)
+    np.testing.assert_array_equal(o1, O.order_maxmin_exact(locs))
+    L = locs[o1 - 1]
+    a = P.find_ordered_nn(L, m)
+    b = O.find_ordered_nn(L, min(m, n - 1))
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(P.naive_greedy_coloring(a), O.greedy_coloring(b))
+
+
+def test_nn_ties_and_duplicates(P, O):
+    # integer grid: many equal distances -> ties broken by the smaller index
+    g = np.array([(x, y) for x in range(20) for y in range(20)], np.float64)
+    g = g[np.random.default_rng(0).permutation(len(g))]
+    for m in [4, 8, 12]:
+        np.testing.assert_array_equal(P.find_ordered_nn(g, m), O.find_ordered_nn(g, m))
+    dup = np.vstack([g[:50], g[:50]])  # exact duplicates (distance 0)
+    np.testing.assert_array_equal(P.find_ordered_nn(dup, 5), O.find_ordered_nn(dup, 5))
+    np.testing.assert_array_equal(P.order_maxmin(g), O.order_maxmin_exact(g))
+
+
+def test_product_nn_on_vignette_prefix(P, printed, toy, O):
+    h = np.array(printed["hctam_scol_1_100"]) - 1
+    NN = P.find_ordered_nn(toy["locs"][h], 5)
+    head = np.array([[O.NA if v is None else v for v in r] for r in printed["NNarray_head"]])
+    np.testing.assert_array_equal(NN[:6], head)
+
+
+def test_vignette_full_toy_graph(P, O, toy):
+    """Full 2000-point toy (our exact max-min ordering of the regenerated
+    locations): product NN + colouring == oracle."""
+    locs = toy["locs"]
+    o = P.order_maxmin(locs)
+    L = locs[o - 1]
+    NN = P.find_ordered_nn(L, 5)
+    np.testing.assert_array_equal(NN, O.find_ordered_nn(L, 5))
+    col = P.naive_greedy_coloring(NN)
+    np.testing.assert_array_equal(col, O.greedy_coloring(NN))
+    n = len(L)
+    assert (NN != O.NA).sum() == n * 6 - 15  # nnz(B) = n(m+1) - m(m+1)/2
+
+
+def test_sparse_chol_indices(P):
+    NN = np.array([[1, P.find_ordered_nn.__globals__["NA_INTEGER"], -2 ** 31], [2, 1, -2 ** 31], [3, 1, 2]], np.int32)
+    non_na, row_idx, col_idx = P.sparse_chol_indices(NN)
+    # column-major vectorisation: self column first (initialize.R:97-101)
+    np.testing.assert_array_equal(col_idx, [1, 2, 3, 1, 1, 2])
+    np.testing.assert_array_equal(row_idx, [1, 2, 3, 2, 3, 3])
+
+
+def test_ctx_create_without_gpu_fails_loudly(P):
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    locs = np.random.default_rng(0).uniform(size=(10, 2))
+    NN = P.find_ordered_nn(locs, 3)
+    with pytest.raises(P.NNGPError) as e:
+        P.ChainContext(locs, NN, P.naive_greedy_coloring(NN), np.arange(1, 11, dtype=np.int32), np.zeros(10))
+    assert e.value.status == 6  # NNGP_ERR_NODEV: no silent CPU fallback
+
+
+def test_shape_transforms():
+    import _pkgload
+
+    M = _pkgload.load().model
+    sp = M.shape_params_of("matern_isotropic", 2)
+    assert sp == ["log_range", "qlogis_smoothness"]
+    np.testing.assert_allclose(M.covparms(sp, [np.log(3.0), 0.0]), [1.0, 3.0, 0.75, 0.0])
+    np.testing.assert_allclose(M.covparms(sp, [0.0, 0.0], 0.4, 0.7), [1.0, 1.0, 0.75, 0.0])
+    assert M.shape_params_of("exponential_scaledim", 3) == ["log_range_1", "log_range_2", "log_range_3"]
+
+
+def test_gelman_rubin_on_identical_chains(P):
+    rng = np.random.default_rng(0)
+    recs = {f"chain_{i}": {"params": {"beta_0": rng.normal(size=(400, 1)), "log_scale": rng.normal(size=(400, 1))}}
+            for i in range(3)}
+    g = P.Gelman_Rubin_Brooks(recs, 0.5)
+    assert np.all(g["R_hat"] < 1.05)
+    E, _ = P.ESS(recs, 0.5)
+    assert np.all(E[:-1] > 100)

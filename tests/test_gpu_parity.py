@@ -1,0 +1,295 @@
+"""HIP path vs the CPU oracle, through the C ABI (needs an MI355X).
+
+Tolerances (fp64 everywhere; the oracle is a textbook-order restatement, the
+device uses a different summation / factorisation order):
+  * Vecchia factor Linv ........ rtol 1e-10, atol 1e-12 (well-conditioned
+                                  synthetic fields); 1e-8 for general Matern
+  * log-likelihood ............. rel 1e-10
+  * chromatic sweep field ...... rtol 1e-9, atol 1e-10 after <= 3 sweeps
+  * neighbour indices, colours . bit-exact (integer)
+"""
+import numpy as np
+import pytest
+
+from conftest import make_problem
+
+pytestmark = pytest.mark.gpu
+
+COVS = {
+    "exponential_isotropic": [1.0, 0.08, 0.0],
+    "matern15_isotropic": [1.0, 0.05, 0.0],
+    "matern_isotropic": [1.0, 0.06, 0.7, 0.0],
+}
+
+
+def _ctx(P, locs, NN, col, lm, y):
+    return P.ChainContext(locs, NN, col, lm, y, device=0)
+
+
+def test_device_normals_match_oracle(P, O):
+    from nngp_amd.context import device_normals
+
+    for seed, sweep in [(0, 0), (12345678901234, 7), (2 ** 64 - 1, 2 ** 40 + 3)]:
+        z = device_normals(seed, sweep, 4096)
+        zo = O.normals(seed, sweep, 4096)
+        assert np.allclose(z, zo, rtol=1e-14, atol=1e-14)
+        assert abs(z.mean()) < 0.1 and abs(z.std() - 1) < 0.05
+
+
+@pytest.mark.parametrize("m", [1, 5, 10, 15, 20, 31])
+@pytest.mark.parametrize("covfun", list(COVS))
+def test_factor_matches_oracle(P, O, m, covfun):
+    locs, NN, col, lm, y = make_problem(P, 700, m, seed=m)
+    cp = COVS[covfun]
+    with _ctx(P, locs, NN, col, lm, y) as ctx:
+        ctx.factor(0, covfun, cp)
+        got = ctx.get_linv(0)
+        ref = O.vecchia_linv(covfun, cp, locs, NN)
+        tol = 1e-8 if covfun == "matern_isotropic" else 1e-10
+        np.testing.assert_allclose(got, ref, rtol=tol, atol=tol * 1e-2)
+        # unfilled (NA) entries are exactly 0 like GpGp's zeros(n, m)
+        assert np.all(got[NN == O.NA] == 0.0)
+        np.testing.assert_allclose(ctx.precision_diag(), O.precision_diag(ref, NN), rtol=1e-10)
+
+
+@pytest.mark.parametrize("covfun,cp,d", [
+    ("exponential_scaledim", [1.3, 0.1, 0.3, 0.0], 2),
+    ("exponential_spacetime", [0.7, 0.1, 0.5, 0.0], 3),
+    ("matern_scaledim", [1.0, 0.1, 0.2, 1.4, 0.0], 2),
+    ("matern_spacetime", [1.0, 0.1, 0.3, 0.9, 0.0], 3),
+    ("exponential_isotropic", [2.0, 0.2, 0.1], 3),  # nugget + variance
+    ("matern_isotropic", [1.0, 0.1, 2.6, 0.0], 2),
+])
+def test_factor_other_covfuns(P, O, covfun, cp, d):
+    locs, NN, col, lm, y = make_problem(P, 500, 10, d=d, seed=3)
+    with _ctx(P, locs, NN, col, lm, y) as ctx:
+        ctx.factor(0, covfun, cp)
+        np.testing.assert_allclose(ctx.get_linv(0), O.vecchia_linv(covfun, cp, locs, NN), rtol=1e-8, atol=1e-10)
+
+
+def test_factor_sphere(P, O):
+    rng = np.random.default_rng(5)
+    locs = np.column_stack([rng.uniform(-124, -67, 800), rng.uniform(25, 49, 800)])
+    locs = locs[P.order_maxmin(locs) - 1]
+    NN = P.find_ordered_nn(locs, 5)
+    col = P.naive_greedy_coloring(NN)
+    lm = np.arange(1, 801, dtype=np.int32)
+    for covfun, cp in [("exponential_sphere", [1.0, 0.05, 0.0]), ("matern_sphere", [1.0, 0.05, 0.8, 0.0])]:
+        with _ctx(P, locs, NN, col, lm, rng.normal(size=800)) as ctx:
+            ctx.factor(0, covfun, cp)
+            np.testing.assert_allclose(ctx.get_linv(0), O.vecchia_linv(covfun, cp, locs, NN), rtol=1e-8, atol=1e-10)
+
+
+def test_factor_not_pd_reports_row(P):
+    locs, NN, col, lm, y = make_problem(P, 200, 5, seed=1)
+    locs = locs.copy()
+    with _ctx(P, locs, NN, col, lm, y) as ctx:
+        # absurdly long range -> numerically singular local covariances
+        with pytest.raises(P.NNGPError) as e:
+            ctx.factor(0, "matern15_isotropic", [1.0, 1e9, 0.0])
+        assert e.value.status == 3 and "row" in str(e.value)
+
+
+@pytest.mark.parametrize("covfun", ["exponential_isotropic", "matern15_isotropic"])
+def test_loglik_matches_oracle(P, O, covfun):
+    locs, NN, col, lm, y = make_problem(P, 1500, 10, seed=2)
+    cp = COVS[covfun]
+    field = np.random.default_rng(0).normal(size=1500) + 0.7
+    with _ctx(P, locs, NN, col, lm, y) as ctx:
+        ctx.factor(0, covfun, cp)
+        ctx.set_field(field)
+        for ls in [-0.3, 0.0, 1.2]:
+            got = ctx.loglik(0, 0.7, ls)
+            ref = O.loglik(O.vecchia_linv(covfun, cp, locs, NN), field - 0.7, NN, ls)
+            assert abs(got - ref) <= 1e-10 * abs(ref)
+
+
+def _sweep_case(P, O, n, m, n_sweeps, dup, mu_vec, covfun="exponential_isotropic", seed=0, form="masked"):
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=seed, dup_frac=dup)
+    cp = COVS[covfun]
+    rng = np.random.default_rng(seed + 1)
+    field = rng.normal(size=n)
+    beta0, ls, lnv = 0.4, 0.3, -0.2
+    mu = (beta0 + 0.1 * rng.normal(size=len(lm))) if mu_vec else np.full(len(lm), beta0)
+    z = rng.normal(size=(n_sweeps, n))
+    with _ctx(P, locs, NN, col, lm, y) as ctx:
+        ctx.factor(0, covfun, cp)
+        ctx.set_field(field)
+        ctx.set_mu(mu if mu_vec else None, beta0)
+        ctx.sweep(n_sweeps, beta0, ls, lnv, 1, 0, z=z)
+        got = ctx.get_field()
+    Lo = O.vecchia_linv(covfun, cp, locs, NN)
+    D = O.precision_diag(Lo, NN)
+    opl = np.bincount(lm - 1, minlength=n).astype(np.int32)
+    ref = O.sweep(form, field, Lo, NN, col, D, opl, y, mu, lm, beta0, ls, lnv, z)
+    return got, ref
+
+
+@pytest.mark.parametrize("n,m,dup,mu_vec", [(2000, 5, 0.0, False), (3000, 10, 0.1, True),
+                                            (1500, 15, 0.0, True), (900, 20, 0.05, False)])
+def test_sweep_matches_masked_reference_form(P, O, n, m, dup, mu_vec):
+    got, ref = _sweep_case(P, O, n, m, 3, dup, mu_vec)
+    np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-10)
+
+
+def test_sweep_matern15_local_form(P, O):
+    got, ref = _sweep_case(P, O, 20000, 15, 2, 0.0, False, covfun="matern15_isotropic", form="local")
+    np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-10)
+
+
+def test_sweep_philox_stream_matches_oracle(P, O):
+    locs, NN, col, lm, y = make_problem(P, 2500, 10, seed=9)
+    cp = COVS["exponential_isotropic"]
+    field = np.random.default_rng(3).normal(size=2500)
+    seed, base = 987654321, 40
+    with _ctx(P, locs, NN, col, lm, y) as ctx:
+        ctx.factor(0, "exponential_isotropic", cp)
+        ctx.set_field(field)
+        ctx.set_mu(None, 0.1)
+        ctx.sweep(3, 0.1, 0.0, 0.1, seed, base)  # graph-captured path
+        got = ctx.get_field()
+        ctx.set_field(field)
+        ctx.sweep(3, 0.1, 0.0, 0.1, seed, base)  # replay of the cached graph
+        np.testing.assert_array_equal(ctx.get_field(), got)  # deterministic replay
+    Lo = O.vecchia_linv("exponential_isotropic", cp, locs, NN)
+    z = O.sweep_normals(seed, base, 3, 2500)
+    ref = O.sweep("masked", field, Lo, NN, col, O.precision_diag(Lo, NN), np.ones(2500, np.int32), y,
+                  np.full(2500, 0.1), lm, 0.1, 0.0, 0.1, z)
+    np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-10)
+
+
+def test_graph_replay_sees_new_scalars(P, O):
+    """Scalars (beta0, scales, counter) live in device memory: a replayed graph
+    must use the current values, not the captured ones."""
+    locs, NN, col, lm, y = make_problem(P, 1200, 8, seed=4)
+    cp = COVS["exponential_isotropic"]
+    field = np.random.default_rng(8).normal(size=1200)
+    Lo = O.vecchia_linv("exponential_isotropic", cp, locs, NN)
+    D = O.precision_diag(Lo, NN)
+    with _ctx(P, locs, NN, col, lm, y) as ctx:
+        ctx.factor(0, "exponential_isotropic", cp)
+        for (b0, ls, lnv, base) in [(0.1, 0.0, 0.1, 0), (-0.5, 0.4, -0.3, 10)]:
+            ctx.set_field(field)
+            ctx.set_mu(None, b0)
+            ctx.sweep(2, b0, ls, lnv, 5, base)
+            z = O.sweep_normals(5, base, 2, 1200)
+            ref = O.sweep("masked", field, Lo, NN, col, D, np.ones(1200, np.int32), y, np.full(1200, b0), lm,
+                          b0, ls, lnv, z)
+            np.testing.assert_allclose(ctx.get_field(), ref, rtol=1e-9, atol=1e-10)
+
+
+def test_accept_factor_refreshes_sweep_values(P, O):
+    locs, NN, col, lm, y = make_problem(P, 1500, 10, seed=6)
+    c0, c1 = [1.0, 0.05, 0.0], [1.0, 0.12, 0.0]
+    field = np.random.default_rng(2).normal(size=1500)
+    with _ctx(P, locs, NN, col, lm, y) as ctx:
+        ctx.factor(0, "exponential_isotropic", c0)
+        ctx.set_field(field)
+        ctx.set_mu(None, 0.0)
+        ctx.sweep(1, 0.0, 0.0, 0.0, 3, 0)  # captures a graph on factor 0
+        ctx.set_field(field)
+        ctx.factor(1, "exponential_isotropic", c1)
+        ctx.accept_factor()
+        ctx.sweep(1, 0.0, 0.0, 0.0, 3, 0)
+        got = ctx.get_field()
+        np.testing.assert_allclose(ctx.precision_diag(), O.precision_diag(O.vecchia_linv("exponential_isotropic", c1, locs, NN), NN), rtol=1e-10)
+    L1 = O.vecchia_linv("exponential_isotropic", c1, locs, NN)
+    z = O.sweep_normals(3, 0, 1, 1500)
+    ref = O.sweep("masked", field, L1, NN, col, O.precision_diag(L1, NN), np.ones(1500, np.int32), y,
+                  np.zeros(1500), lm, 0.0, 0.0, 0.0, z)
+    np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-10)
+
+
+def test_mh_building_blocks(P, O):
+    locs, NN, col, lm, y = make_problem(P, 1800, 10, seed=11, dup_frac=0.1)
+    n = 1800
+    rng = np.random.default_rng(4)
+    field = rng.normal(size=n) + 1.0
+    beta0, lnv = 1.0, -0.4
+    mu = beta0 + 0.2 * rng.normal(size=len(lm))
+    c0, c1 = [1.0, 0.05, 0.0], [1.0, 0.09, 0.0]
+    L0 = O.vecchia_linv("exponential_isotropic", c0, locs, NN)
+    L1 = O.vecchia_linv("exponential_isotropic", c1, locs, NN)
+    with _ctx(P, locs, NN, col, lm, y) as ctx:
+        ctx.factor(0, "exponential_isotropic", c0)
+        ctx.factor(1, "exponential_isotropic", c1)
+        ctx.set_field(field)
+        ctx.set_mu(mu, beta0)
+        # ancillary proposal: beta0 + exp(dls/2) B1^{-1} B0 (field - beta0)  (update_Gaussian.R:127)
+        ctx.ancillary_propose(beta0, 0.3)
+        w = O.tri_solve(L1, NN, O.linv_mult(L0, field - beta0, NN))
+        prop = beta0 + np.exp(0.15) * w
+        ratio = ctx.field_response_ratio(beta0, lnv)
+        sd = np.exp(0.5 * lnv)
+        ll = lambda f: -0.5 * ((y - (f[lm - 1] + mu - beta0)) / sd) ** 2
+        np.testing.assert_allclose(ratio, (ll(prop) - ll(field)).sum(), rtol=1e-8)
+        ssr = ctx.sum_squared_residuals(beta0)
+        np.testing.assert_allclose(ssr, ((y - field[lm - 1] - mu + beta0) ** 2).sum(), rtol=1e-11)
+        oqo, oqf = ctx.beta0_stats()
+        u1 = O.linv_mult(L0, np.ones(n), NN)
+        uf = O.linv_mult(L0, field, NN)
+        np.testing.assert_allclose([oqo, oqf], [u1 @ u1, u1 @ uf], rtol=1e-11)
+        X = rng.normal(size=(n, 3))
+        np.testing.assert_allclose(ctx.spmv(1, X), np.column_stack([O.linv_mult(L1, X[:, k], NN) for k in range(3)]),
+                                   rtol=1e-12, atol=1e-12)
+        u = rng.normal(size=n)
+        np.testing.assert_allclose(ctx.tri_solve(0, u), O.tri_solve(L0, NN, u), rtol=1e-9, atol=1e-10)
+        ctx.accept_field()
+        np.testing.assert_allclose(ctx.get_field(), prop, rtol=1e-9, atol=1e-10)
+
+
+def test_edge_cases(P, O):
+    # n <= m+1 (every row short), single-location colours, m = 0 neighbourhood impossible (b>=1)
+    for n, m in [(1, 3), (2, 3), (5, 10), (40, 1)]:
+        locs, NN, col, lm, y = make_problem(P, n, m, seed=n)
+        got, ref = None, None
+        with _ctx(P, locs, NN, col, lm, y) as ctx:
+            ctx.factor(0, "exponential_isotropic", [1.0, 0.3, 0.0])
+            Lo = O.vecchia_linv("exponential_isotropic", [1.0, 0.3, 0.0], locs, NN)
+            np.testing.assert_allclose(ctx.get_linv(0), Lo, rtol=1e-11, atol=1e-13)
+            f = np.linspace(-1, 1, n)
+            ctx.set_field(f)
+            ctx.set_mu(None, 0.0)
+            z = np.ones((1, n))
+            ctx.sweep(1, 0.0, 0.0, 0.0, 0, 0, z=z)
+            got = ctx.get_field()
+        ref = O.sweep("masked", f, Lo, NN, col, O.precision_diag(Lo, NN), np.ones(n, np.int32), y,
+                      np.zeros(n), lm, 0.0, 0.0, 0.0, z)
+        np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-12)
+
+
+def test_bad_inputs_fail_loudly(P):
+    locs, NN, col, lm, y = make_problem(P, 300, 5, seed=2)
+    bad = col.copy()
+    bad[:] = 1  # not a proper colouring
+    with pytest.raises(P.NNGPError):
+        P.ChainContext(locs, NN, bad, lm, y, device=0)
+    with _ctx(P, locs, NN, col, lm, y) as ctx:
+        with pytest.raises(P.NNGPError):
+            ctx.sweep(1, 0.0, 0.0, 0.0, 0, 0)  # no factor yet
+        with pytest.raises(P.NNGPError):
+            ctx.factor(0, "exponential_isotropic", [1.0, 0.1])  # wrong covparms length
+
+
+def test_size_independent_properties_large(P, O):
+    """n = 2e5, m = 15: local-form oracle agreement + stationarity of the
+    sweep map (zero noise, huge noise variance => Gibbs on the prior is a
+    contraction towards 0)."""
+    n, m = 200_000, 15
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=21)
+    cp = COVS["matern15_isotropic"]
+    rng = np.random.default_rng(1)
+    field = rng.normal(size=n)
+    z = rng.normal(size=(1, n))
+    with _ctx(P, locs, NN, col, lm, y) as ctx:
+        ctx.factor(0, "matern15_isotropic", cp)
+        ctx.set_field(field)
+        ctx.set_mu(None, 0.0)
+        ctx.sweep(1, 0.0, 0.0, 0.0, 0, 0, z=z)
+        got = ctx.get_field()
+        info = ctx.info
+    Lo = O.vecchia_linv("matern15_isotropic", cp, locs, NN)
+    ref = O.sweep("local", field, Lo, NN, col, O.precision_diag(Lo, NN), np.ones(n, np.int32), y,
+                  np.zeros(n), lm, 0.0, 0.0, 0.0, z)
+    np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-10)
+    assert info["nnz"] == n * (m + 1) - m * (m + 1) // 2
