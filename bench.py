@@ -1,0 +1,202 @@
+#!/usr/bin/env python
+"""Headline benchmark: full-field chromatic Gibbs sweeps/sec at n=1e6, m=15
+(synthetic 2-D Matern-3/2 field, fp64, one chain per GPU), with the sweep
+kernel's achieved bandwidth against the MI355X HBM roofline and the CPU
+oracle's reference-faithful sweep timed on the host beside it.
+
+Contract: python bench.py --gpus N --steps K --warmup W  (N>1 under
+torch.distributed.run; one rank per GPU).  A step = one chromatic sweep (all K
+colours, all n latents, update_Gaussian.R:257-275 with n_chromatic = 1).  The
+timed region runs the reference's per-iteration call shape: nngp_sweep with
+n_chromatic = 10 sweeps per call (r = B w refresh + 10 sweeps).
+Multi-GPU: every rank runs an independent chain on its own synthetic field
+(the reference's chain-level parallelism, mclapply -> ranks): weak scaling,
+no data-path collective (DESIGN.md "Multi-GPU").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def log(msg, rank=0):
+    if rank == 0:
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def make_workload(P, n, m, covfun, cp, seed, device):
+    rng = np.random.default_rng(seed)
+    t = time.time()
+    locs = rng.uniform(size=(n, 2))
+    locs = locs[P.order_maxmin(locs) - 1]
+    NN = P.find_ordered_nn(locs, m)
+    col = P.naive_greedy_coloring(NN)
+    t_graph = time.time() - t
+    lm = np.arange(1, n + 1, dtype=np.int32)
+    beta0, tau2 = 1.0, 0.25
+    # truth: w = B^{-1} z (sigma^2 = 1), y = beta0 + w + eps
+    ctx = P.ChainContext(locs, NN, col, lm, np.zeros(n), device=device)
+    ctx.factor(0, covfun, cp)
+    w = ctx.tri_solve(0, rng.normal(size=n))
+    y = beta0 + w + np.sqrt(tau2) * rng.normal(size=n)
+    ctx.close()
+    ctx = P.ChainContext(locs, NN, col, lm, y, device=device)
+    ctx.factor(0, covfun, cp)
+    ctx.set_field(beta0 + w + 0.1 * rng.normal(size=n))
+    ctx.set_mu(None, beta0)
+    return ctx, dict(locs=locs, NN=NN, col=col, lm=lm, y=y, beta0=beta0, log_noise_variance=np.log(tau2),
+                     log_scale=0.0, t_graph=t_graph)
+
+
+def cpu_baseline(P, wl, covfun, cp, budget_s):
+    """Reference-faithful masked-form sweep (update_Gaussian.R:269) of the CPU
+    oracle (a C restatement, 1 core) on the same workload, bounded in time."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle as O
+
+    n = len(wl["y"])
+    t = time.time()
+    Lo = O.vecchia_linv(covfun, cp, wl["locs"], wl["NN"])
+    D = O.precision_diag(Lo, wl["NN"])
+    t_factor = time.time() - t
+    field = np.asarray(wl["field0"])
+    opl = np.ones(n, np.int32)
+    mu = np.full(n, wl["beta0"])
+    res = {}
+    for form in ("masked", "local"):
+        z = O.sweep_normals(3, 0, 1, n)
+        done, t0 = 0, time.time()
+        while True:
+            O.sweep(form, field, Lo, wl["NN"], wl["col"], D, opl, wl["y"], mu, wl["lm"], wl["beta0"],
+                    wl["log_scale"], wl["log_noise_variance"], z)
+            done += 1
+            if time.time() - t0 > budget_s / 2 or done >= 20:
+                break
+        res[form] = done / (time.time() - t0)
+    return {"value": res["masked"], "unit": "sweeps/s", "cores": 1, "kind": "port",
+            "sample": (f"oracle C restatement of the reference's masked-form chromatic sweep "
+                       f"(update_Gaussian.R:257-275), same n={n} workload, whole sweeps until "
+                       f"~{budget_s / 2:.0f}s; local-form oracle {res['local']:.3g} sweeps/s; "
+                       f"oracle factor build {t_factor:.1f}s"),
+            "local_form_value": res["local"]}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--m", type=int, default=15)
+    ap.add_argument("--covfun", default="matern15_isotropic")
+    ap.add_argument("--range", type=float, default=0.05)
+    ap.add_argument("--n-chromatic", type=int, default=10)
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")
+    import _pkgload
+
+    P = _pkgload.load()
+    covfun = args.covfun
+    cp = [1.0, args.range, 0.0]
+    log(f"setup n={args.n} m={args.m} {covfun} world={world}", rank)
+    ctx, wl = make_workload(P, args.n, args.m, covfun, cp, seed=1000 + rank, device=local_rank)
+    wl["field0"] = ctx.get_field()
+    info = ctx.info
+    log(f"graph prep {wl['t_graph']:.1f}s colours={info['n_colors']} nnz={info['nnz']} "
+        f"entries={info['n_entries']} max_collen={info['max_collen']}", rank)
+    nc = args.n_chromatic
+    b0, ls, lnv = wl["beta0"], wl["log_scale"], wl["log_noise_variance"]
+    seed = 77 + rank
+
+    def run_sweeps(k, base):
+        done = 0
+        while done < k:
+            s = min(nc, k - done)
+            ctx.sweep(s, b0, ls, lnv, seed, base + done)
+            done += s
+        return base + done
+
+    ctr = run_sweeps(args.warmup, 0)
+    torch.cuda.synchronize(local_rank) if torch.cuda.is_available() else None
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    ctr = run_sweeps(args.steps, ctr)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize(local_rank)
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-kernel timing (HIP events around every colour launch, on the
+    # context's own stream) -> sweep kernel time per sweep
+    n, nnz = args.n, info["nnz"]
+    bytes_sweep = 12 * nnz + 40 * n  # SURVEY §8(d) algorithmic bytes per sweep
+    roofline = None
+    if not args.no_kernel_timing:
+        ksw = max(4, min(20, args.steps))
+        try:
+            ms_tot, kms = ctx.sweep_timed(ksw, b0, ls, lnv, seed, ctr, per_kernel=True)
+        except Exception as e:  # report, do not hide the throughput line
+            log(f"per-kernel timing failed: {e}", rank)
+            kms = float("nan")
+        per_sweep_ms = kms / ksw
+        achieved = bytes_sweep / (per_sweep_ms * 1e-3) / 1e9
+        launches = ksw * info["n_colors"]
+        roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                    "kernel": "sweep_color_kernel", "kernel_avg_us": kms * 1e3 / launches,
+                    "algorithmic_bytes_per_sweep": bytes_sweep,
+                    "launches_per_sweep": info["n_colors"]}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline (oracle, 1 core)...", rank)
+        cpu = cpu_baseline(P, wl, covfun, cp, args.cpu_budget)
+    ctx.close()
+    total_sweeps = args.steps * world
+    value = total_sweeps / elapsed
+    out = {"metric": "full-field Gibbs sweeps/sec at n=1e6, m=15; achieved HBM GB/s vs roofline",
+           "value": value, "unit": "sweeps/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+           "data": "synthetic (U[0,1]^2 locations, exact max-min order, field drawn from the Vecchia prior)",
+           "config": {"workload": f"chromatic sweep n={n} m={args.m} {covfun} range={args.range}, one chain per GPU",
+                      "n": n, "m": args.m, "n_colors": info["n_colors"], "nnz": nnz,
+                      "n_chromatic_per_call": nc, "parallelism": f"chains x{world} (independent)"},
+           "roofline": roofline, "cpu_baseline": cpu}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -19,12 +19,17 @@
 
 using namespace nngp;
 
+// Device row order: every row-indexed device array (locations, NNarray,
+// Linv, field, r) is stored in Morton order ("dpos" = lay.rpos[loc]) so the
+// neighbour gathers of the factor build, the SpMV and the sweep hit nearby
+// lines; the host boundary converts to and from the Vecchia (location) order.
 struct nngp_ctx {
   int device = 0;
   hipStream_t st = nullptr;
   int n = 0, d = 0, b = 0, n_obs = 0, ds = 2;
   std::string err;
   SweepLayout lay;
+  std::vector<int> dpos;   // loc -> device row (== lay.rpos)
   std::vector<int> level_ptr, level_rows;
   // device buffers
   double* locs_d = nullptr;  // n x d row-major
@@ -32,18 +37,12 @@ struct nngp_ctx {
   int* nn_d = nullptr;       // n x b row-major, 0-based, -1 = NA
   double* linv_d[2] = {nullptr, nullptr};
   int* fail_d = nullptr;
-  int* chunk_slot0_d = nullptr;
-  int* chunk_len_d = nullptr;
-  long long* chunk_off_d = nullptr;
-  int* collen_d = nullptr;
-  int* slot_loc_d = nullptr;
-  int* rpos_d = nullptr;
+  ChunkMeta* meta_d = nullptr;
+  SlotData* slots_d = nullptr;
+  int* slot_dpos_d = nullptr;
   int* ent_rowpos_d = nullptr;
   int* ent_src_d = nullptr;
   double* ent_val_d = nullptr;
-  double* D_slot_d = nullptr;
-  double* R_slot_d = nullptr;
-  int* nobs_slot_d = nullptr;
   double* w_slot_d = nullptr;
   double* r_d = nullptr;
   int* level_rows_d = nullptr;
@@ -112,25 +111,18 @@ int set_device(nngp_ctx* c) {
 // sweep-layout pointers
 SweepDev sweep_dev(nngp_ctx* c) {
   SweepDev L;
-  L.chunk_slot0 = c->chunk_slot0_d;
-  L.chunk_len = c->chunk_len_d;
-  L.chunk_off = c->chunk_off_d;
-  L.collen = c->collen_d;
-  L.slot_loc = c->slot_loc_d;
+  L.meta = c->meta_d;
+  L.slots = c->slots_d;
   L.ent_val = c->ent_val_d;
   L.ent_rowpos = c->ent_rowpos_d;
-  L.D_slot = c->D_slot_d;
-  L.R_slot = c->R_slot_d;
-  L.nobs_slot = c->nobs_slot_d;
   L.w_slot = c->w_slot_d;
   L.r = c->r_d;
   return L;
 }
 
 int refresh_sweep_values(nngp_ctx* c) {
-  HIPCHK(c, launch_sell_refresh(c->st, c->chunk_slot0_d, c->chunk_off_d, c->lay.nchunks, nullptr,
-                                c->collen_d, c->n, c->ent_src_d, c->linv_d[0], c->ent_val_d,
-                                c->D_slot_d));
+  HIPCHK(c, launch_sell_refresh(c->st, sweep_dev(c), c->lay.nchunks, c->ent_src_d, c->linv_d[0],
+                                c->ent_val_d));
   return NNGP_OK;
 }
 
@@ -220,9 +212,7 @@ void nngp_ctx_destroy(nngp_ctx* c) {
   for (auto& kv : c->graphs) hipGraphExecDestroy(kv.second);
   for (auto g : c->graph_objs) hipGraphDestroy(g);
   void* ptrs[] = {c->locs_d, c->sc_d, c->nn_d, c->linv_d[0], c->linv_d[1], c->fail_d,
-                  c->chunk_slot0_d, c->chunk_len_d, c->chunk_off_d, c->collen_d, c->slot_loc_d,
-                  c->rpos_d, c->ent_rowpos_d, c->ent_src_d, c->ent_val_d, c->D_slot_d, c->R_slot_d,
-                  c->nobs_slot_d, c->w_slot_d, c->r_d, c->level_rows_d, c->obs_ptr_d, c->obs_idx_d,
+                  c->meta_d, c->slots_d, c->slot_dpos_d, c->ent_rowpos_d, c->ent_src_d, c->ent_val_d, c->w_slot_d, c->r_d, c->level_rows_d, c->obs_ptr_d, c->obs_idx_d,
                   c->lm_d, c->y_d, c->mu_d, c->field_d, c->field_prop_d, c->tmp_d, c->tmp2_d,
                   c->partials_d, c->res_d, c->z_d, c->scal_d};
   for (void* p : ptrs) if (p) hipFree(p);
@@ -287,11 +277,24 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
     return fail_msg(nullptr, NNGP_ERR_ARG, err);
   }
   dag_levels(nn.data(), n, b, c->level_ptr, c->level_rows);
+  c->dpos = c->lay.rpos;
+  const std::vector<int>& dp = c->dpos;
+  for (auto& r : c->level_rows) r = dp[r];
   std::vector<int> nobs_slot(n);
   for (int s = 0; s < n; ++s) { int i = c->lay.slot_loc[s]; nobs_slot[s] = obs_cnt[i + 1] - obs_cnt[i]; }
+  // device-order copies
   std::vector<double> locs_rm((size_t)n * d);
   for (int i = 0; i < n; ++i)
-    for (int k = 0; k < d; ++k) locs_rm[(size_t)i * d + k] = locs[i + (size_t)k * n];
+    for (int k = 0; k < d; ++k) locs_rm[(size_t)dp[i] * d + k] = locs[i + (size_t)k * n];
+  std::vector<int> nn_dev((size_t)n * b);
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < b; ++j) {
+      int a = nn[(size_t)i * b + j];
+      nn_dev[(size_t)dp[i] * b + j] = a < 0 ? -1 : dp[a];
+    }
+  std::vector<int> lm_dev(n_obs), slot_dpos(n);
+  for (int o = 0; o < n_obs; ++o) lm_dev[o] = dp[lm0[o]];
+  for (int s = 0; s < n; ++s) slot_dpos[s] = dp[c->lay.slot_loc[s]];
 
   if ((rc = set_device(c))) { delete c; return rc; }
 #define CK(x)                                                     \
@@ -311,18 +314,12 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
   CK(dalloc(&c->linv_d[0], (size_t)n * b));
   CK(dalloc(&c->linv_d[1], (size_t)n * b));
   CK(dalloc(&c->fail_d, 1));
-  CK(dalloc(&c->chunk_slot0_d, L.nchunks));
-  CK(dalloc(&c->chunk_len_d, L.nchunks));
-  CK(dalloc(&c->chunk_off_d, (size_t)L.nchunks + 1));
-  CK(dalloc(&c->collen_d, n));
-  CK(dalloc(&c->slot_loc_d, n));
-  CK(dalloc(&c->rpos_d, n));
+  CK(dalloc(&c->meta_d, L.nchunks));
+  CK(dalloc(&c->slots_d, n));
+  CK(dalloc(&c->slot_dpos_d, n));
   CK(dalloc(&c->ent_rowpos_d, (size_t)L.n_entries));
   CK(dalloc(&c->ent_src_d, (size_t)L.n_entries));
   CK(dalloc(&c->ent_val_d, (size_t)L.n_entries));
-  CK(dalloc(&c->D_slot_d, n));
-  CK(dalloc(&c->R_slot_d, n));
-  CK(dalloc(&c->nobs_slot_d, n));
   CK(dalloc(&c->w_slot_d, n));
   CK(dalloc(&c->r_d, n));
   CK(dalloc(&c->level_rows_d, n));
@@ -341,21 +338,34 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
   CK(hipHostMalloc((void**)&c->scal_h, sizeof(SweepScalars), hipHostMallocDefault));
   CK(hipHostMalloc((void**)&c->res_h, 8 * sizeof(double), hipHostMallocDefault));
   CK(upload(c->locs_d, locs_rm.data(), locs_rm.size(), c->st));
-  CK(upload(c->nn_d, nn.data(), nn.size(), c->st));
-  CK(upload(c->chunk_slot0_d, L.chunk_slot0.data(), L.nchunks, c->st));
-  CK(upload(c->chunk_len_d, L.chunk_len.data(), L.nchunks, c->st));
-  CK(upload(c->chunk_off_d, L.chunk_off.data(), (size_t)L.nchunks + 1, c->st));
-  CK(upload(c->collen_d, L.collen.data(), n, c->st));
-  CK(upload(c->slot_loc_d, L.slot_loc.data(), n, c->st));
-  CK(upload(c->rpos_d, L.rpos.data(), n, c->st));
+  CK(upload(c->nn_d, nn_dev.data(), nn_dev.size(), c->st));
+  {
+    std::vector<ChunkMeta> meta(L.nchunks);
+    for (int ch = 0; ch < L.nchunks; ++ch) {
+      meta[ch].slot0 = L.chunk_slot0[ch];
+      meta[ch].packed = L.chunk_len[ch] | (L.chunk_nslot[ch] << 8) | (L.chunk_lk[ch] << 16);
+      meta[ch].off = L.chunk_off[ch];
+    }
+    std::vector<SlotData> sd(n);
+    for (int s = 0; s < n; ++s) {
+      sd[s].D = 0.0;
+      sd[s].R = 0.0;
+      sd[s].nobs = nobs_slot[s];
+      sd[s].loc = L.slot_loc[s];
+      sd[s].collen = L.collen[s];
+      sd[s].dpos = slot_dpos[s];
+    }
+    CK(hipMemcpy(c->meta_d, meta.data(), sizeof(ChunkMeta) * meta.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(c->slots_d, sd.data(), sizeof(SlotData) * sd.size(), hipMemcpyHostToDevice));
+  }
+  CK(upload(c->slot_dpos_d, slot_dpos.data(), n, c->st));
   CK(upload(c->ent_rowpos_d, L.ent_rowpos.data(), (size_t)L.n_entries, c->st));
   CK(upload(c->ent_src_d, L.ent_src.data(), (size_t)L.n_entries, c->st));
   CK(hipMemsetAsync(c->ent_val_d, 0, sizeof(double) * std::max<long long>(1, L.n_entries), c->st));
-  CK(upload(c->nobs_slot_d, nobs_slot.data(), n, c->st));
   CK(upload(c->level_rows_d, c->level_rows.data(), n, c->st));
   CK(upload(c->obs_ptr_d, obs_cnt.data(), (size_t)n + 1, c->st));
   CK(upload(c->obs_idx_d, obs_idx.data(), n_obs, c->st));
-  CK(upload(c->lm_d, lm0.data(), n_obs, c->st));
+  CK(upload(c->lm_d, lm_dev.data(), n_obs, c->st));
   CK(upload(c->y_d, observed_field, n_obs, c->st));
   CK(hipStreamSynchronize(c->st));
 #undef CK
@@ -449,7 +459,7 @@ int nngp_get_linv(nngp_ctx* c, int which, double* Linv) {
   HIPCHK(c, hipMemcpyAsync(rm.data(), c->linv_d[which], rm.size() * sizeof(double), hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
   for (int i = 0; i < c->n; ++i)
-    for (int j = 0; j < c->b; ++j) Linv[i + (size_t)j * c->n] = rm[(size_t)i * c->b + j];
+    for (int j = 0; j < c->b; ++j) Linv[i + (size_t)j * c->n] = rm[(size_t)c->dpos[i] * c->b + j];
   return NNGP_OK;
 }
 
@@ -459,7 +469,7 @@ int nngp_set_linv(nngp_ctx* c, int which, const double* Linv) {
   if ((rc = set_device(c))) return rc;
   std::vector<double> rm((size_t)c->n * c->b);
   for (int i = 0; i < c->n; ++i)
-    for (int j = 0; j < c->b; ++j) rm[(size_t)i * c->b + j] = Linv[i + (size_t)j * c->n];
+    for (int j = 0; j < c->b; ++j) rm[(size_t)c->dpos[i] * c->b + j] = Linv[i + (size_t)j * c->n];
   HIPCHK(c, hipMemcpyAsync(c->linv_d[which], rm.data(), rm.size() * sizeof(double), hipMemcpyHostToDevice, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
   c->have_factor[which] = true;
@@ -487,10 +497,10 @@ int nngp_get_precision_diag(nngp_ctx* c, double* D) {
   if (!c->have_factor[0]) return fail_msg(c, NNGP_ERR_STATE, "precision_diag: no factor");
   int rc;
   if ((rc = set_device(c))) return rc;
-  std::vector<double> Ds(c->n);
-  HIPCHK(c, hipMemcpyAsync(Ds.data(), c->D_slot_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
+  std::vector<SlotData> sd(c->n);
+  HIPCHK(c, hipMemcpyAsync(sd.data(), c->slots_d, c->n * sizeof(SlotData), hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
-  for (int s = 0; s < c->n; ++s) D[c->lay.slot_loc[s]] = Ds[s];
+  for (int s = 0; s < c->n; ++s) D[c->lay.slot_loc[s]] = sd[s].D;
   return NNGP_OK;
 }
 
@@ -499,7 +509,9 @@ int nngp_set_field(nngp_ctx* c, const double* field) {
   if (!c || !field) return NNGP_ERR_ARG;
   int rc;
   if ((rc = set_device(c))) return rc;
-  HIPCHK(c, hipMemcpyAsync(c->field_d, field, c->n * sizeof(double), hipMemcpyHostToDevice, c->st));
+  std::vector<double> f(c->n);
+  for (int i = 0; i < c->n; ++i) f[c->dpos[i]] = field[i];
+  HIPCHK(c, hipMemcpyAsync(c->field_d, f.data(), c->n * sizeof(double), hipMemcpyHostToDevice, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
   c->have_field = true;
   return NNGP_OK;
@@ -510,8 +522,10 @@ int nngp_get_field(nngp_ctx* c, double* field) {
   if (!c->have_field) return fail_msg(c, NNGP_ERR_STATE, "get_field: no field");
   int rc;
   if ((rc = set_device(c))) return rc;
-  HIPCHK(c, hipMemcpyAsync(field, c->field_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
+  std::vector<double> f(c->n);
+  HIPCHK(c, hipMemcpyAsync(f.data(), c->field_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
+  for (int i = 0; i < c->n; ++i) field[i] = f[c->dpos[i]];
   return NNGP_OK;
 }
 
@@ -522,8 +536,8 @@ int nngp_set_mu(nngp_ctx* c, const double* mu, double beta0) {
   if (mu) HIPCHK(c, hipMemcpyAsync(c->mu_d, mu, c->n_obs * sizeof(double), hipMemcpyHostToDevice, c->st));
   c->mu_is_const = (mu == nullptr);
   c->mu_beta0 = beta0;
-  HIPCHK(c, launch_residual_sums(c->st, c->n, c->slot_loc_d, c->obs_ptr_d, c->obs_idx_d, c->y_d,
-                                 mu ? c->mu_d : nullptr, beta0, c->R_slot_d));
+  HIPCHK(c, launch_residual_sums(c->st, c->n, c->slots_d, c->obs_ptr_d, c->obs_idx_d, c->y_d,
+                                 mu ? c->mu_d : nullptr, beta0));
   HIPCHK(c, hipStreamSynchronize(c->st));
   c->have_mu = true;
   return NNGP_OK;
@@ -536,7 +550,7 @@ int nngp_loglik(nngp_ctx* c, int which, double beta0, double log_scale, double* 
   int rc;
   if ((rc = set_device(c))) return rc;
   int nb = launch_row_stats(c->st, c->linv_d[which], c->nn_d, c->n, c->b, c->field_d, beta0, nullptr,
-                            nullptr, c->partials_d);
+                            c->partials_d);
   HIPCHK(c, hipGetLastError());
   double r[4];
   if ((rc = fetch4(c, nb, r))) return rc;
@@ -551,8 +565,8 @@ static int sweep_prepare(nngp_ctx* c, double beta0, double log_scale, double lnv
     return fail_msg(c, NNGP_ERR_STATE, "sweep: need factor, field and mu");
   if (c->mu_is_const && c->mu_beta0 != beta0) {
     // residual sums depend on beta0 when mu = beta0
-    HIPCHK(c, launch_residual_sums(c->st, c->n, c->slot_loc_d, c->obs_ptr_d, c->obs_idx_d, c->y_d,
-                                   nullptr, beta0, c->R_slot_d));
+    HIPCHK(c, launch_residual_sums(c->st, c->n, c->slots_d, c->obs_ptr_d, c->obs_idx_d, c->y_d,
+                                   nullptr, beta0));
     c->mu_beta0 = beta0;
   }
   c->scal_h->inv_s2 = std::exp(-log_scale);
@@ -569,23 +583,22 @@ static int sweep_prepare(nngp_ctx* c, double beta0, double log_scale, double lnv
 static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, const double* z_dev,
                               std::vector<hipEvent_t>* evs) {
   const int n = c->n;
-  HIPCHK(c, launch_field_to_slots(c->st, n, c->slot_loc_d, c->field_d, c->scal_d, c->w_slot_d));
+  HIPCHK(c, launch_field_to_slots(c->st, n, c->slot_dpos_d, c->field_d, c->scal_d, c->w_slot_d));
   // shift read from device memory so a replayed graph sees the current beta0
-  launch_row_stats(c->st, c->linv_d[0], c->nn_d, n, c->b, c->field_d, 0.0, c->r_d, c->rpos_d,
-                   c->partials_d, &c->scal_d->beta0);
+  launch_row_stats(c->st, c->linv_d[0], c->nn_d, n, c->b, c->field_d, 0.0, c->r_d, c->partials_d,
+                   &c->scal_d->beta0);
   HIPCHK(c, hipGetLastError());
   SweepDev L = sweep_dev(c);
   for (int s = 0; s < n_sweeps; ++s) {
     for (int col = 0; col < c->lay.K; ++col) {
       int ch0 = c->lay.color_chunk_ptr[col];
       int nch = c->lay.color_chunk_ptr[col + 1] - ch0;
-      int slot_end = c->lay.color_slot_ptr[col + 1];
       if (evs) HIPCHK(c, hipEventRecord((*evs)[2 * ((size_t)s * c->lay.K + col)], c->st));
-      HIPCHK(c, launch_sweep_color(c->st, L, ch0, nch, slot_end, c->scal_d, s, z_dev, n));
+      HIPCHK(c, launch_sweep_color(c->st, L, ch0, nch, c->scal_d, s, z_dev, n));
       if (evs) HIPCHK(c, hipEventRecord((*evs)[2 * ((size_t)s * c->lay.K + col) + 1], c->st));
     }
   }
-  HIPCHK(c, launch_slots_to_field(c->st, n, c->slot_loc_d, c->w_slot_d, c->scal_d, c->field_d));
+  HIPCHK(c, launch_slots_to_field(c->st, n, c->slot_dpos_d, c->w_slot_d, c->scal_d, c->field_d));
   return NNGP_OK;
 }
 
@@ -641,6 +654,10 @@ int nngp_sweep_timed(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, 
   if (kernel_ms) {
     evs.resize(2 * (size_t)n_sweeps * c->lay.K);
     for (auto& e : evs) HIPCHK(c, hipEventCreate(&e));
+    // a bounded spin kernel keeps the GPU busy while the host enqueues the
+    // event-bracketed launches, so no host submission gap lands inside a
+    // measured interval
+    HIPCHK(c, launch_spin(c->st, 0.05 + 2e-5 * (double)evs.size()));
     HIPCHK(c, hipEventRecord(e0, c->st));
     rc = enqueue_sweep_body(c, n_sweeps, nullptr, &evs);
     HIPCHK(c, hipEventRecord(e1, c->st));
@@ -698,7 +715,7 @@ int nngp_ancillary_propose(nngp_ctx* c, double beta0, double dlog_scale) {
   int rc;
   if ((rc = set_device(c))) return rc;
   // tmp = B_cur (field - beta0)
-  launch_row_stats(c->st, c->linv_d[0], c->nn_d, c->n, c->b, c->field_d, beta0, c->tmp_d, nullptr,
+  launch_row_stats(c->st, c->linv_d[0], c->nn_d, c->n, c->b, c->field_d, beta0, c->tmp_d,
                    c->partials_d);
   HIPCHK(c, hipGetLastError());
   if ((rc = tri_solve_dev(c, c->linv_d[1], c->tmp_d, c->tmp2_d))) return rc;
@@ -735,7 +752,7 @@ int nngp_beta0_stats(nngp_ctx* c, double* oqo, double* oqf) {
   if (!c->have_factor[0] || !c->have_field) return fail_msg(c, NNGP_ERR_STATE, "beta0_stats: need factor and field");
   int rc;
   if ((rc = set_device(c))) return rc;
-  int nb = launch_row_stats(c->st, c->linv_d[0], c->nn_d, c->n, c->b, c->field_d, 0.0, nullptr, nullptr,
+  int nb = launch_row_stats(c->st, c->linv_d[0], c->nn_d, c->n, c->b, c->field_d, 0.0, nullptr,
                             c->partials_d);
   HIPCHK(c, hipGetLastError());
   double r[4];
@@ -764,12 +781,15 @@ int nngp_spmv(nngp_ctx* c, int which, const double* X, int ncols, double* Y) {
   if (!c->have_factor[which]) return fail_msg(c, NNGP_ERR_STATE, "spmv: no factor");
   int rc;
   if ((rc = set_device(c))) return rc;
+  std::vector<double> in(c->n), outv(c->n);
   for (int col = 0; col < ncols; ++col) {
-    HIPCHK(c, hipMemcpyAsync(c->tmp2_d, X + (size_t)col * c->n, c->n * sizeof(double), hipMemcpyHostToDevice, c->st));
-    launch_row_stats(c->st, c->linv_d[which], c->nn_d, c->n, c->b, c->tmp2_d, 0.0, c->tmp_d, nullptr, c->partials_d);
+    for (int i = 0; i < c->n; ++i) in[c->dpos[i]] = X[(size_t)col * c->n + i];
+    HIPCHK(c, hipMemcpyAsync(c->tmp2_d, in.data(), c->n * sizeof(double), hipMemcpyHostToDevice, c->st));
+    launch_row_stats(c->st, c->linv_d[which], c->nn_d, c->n, c->b, c->tmp2_d, 0.0, c->tmp_d, c->partials_d);
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipMemcpyAsync(Y + (size_t)col * c->n, c->tmp_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipMemcpyAsync(outv.data(), c->tmp_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
     HIPCHK(c, hipStreamSynchronize(c->st));
+    for (int i = 0; i < c->n; ++i) Y[(size_t)col * c->n + i] = outv[c->dpos[i]];
   }
   return NNGP_OK;
 }
@@ -779,10 +799,13 @@ int nngp_tri_solve(nngp_ctx* c, int which, const double* u, double* x) {
   if (!c->have_factor[which]) return fail_msg(c, NNGP_ERR_STATE, "tri_solve: no factor");
   int rc;
   if ((rc = set_device(c))) return rc;
-  HIPCHK(c, hipMemcpyAsync(c->tmp_d, u, c->n * sizeof(double), hipMemcpyHostToDevice, c->st));
+  std::vector<double> in(c->n), outv(c->n);
+  for (int i = 0; i < c->n; ++i) in[c->dpos[i]] = u[i];
+  HIPCHK(c, hipMemcpyAsync(c->tmp_d, in.data(), c->n * sizeof(double), hipMemcpyHostToDevice, c->st));
   if ((rc = tri_solve_dev(c, c->linv_d[which], c->tmp_d, c->tmp2_d))) return rc;
-  HIPCHK(c, hipMemcpyAsync(x, c->tmp2_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipMemcpyAsync(outv.data(), c->tmp2_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
+  for (int i = 0; i < c->n; ++i) x[i] = outv[c->dpos[i]];
   return NNGP_OK;
 }
 

@@ -350,11 +350,12 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
     if (a >= 0) cptr[a + 1]++;
   }
   for (int i = 0; i < n; ++i) cptr[i + 1] += cptr[i];
-  // slots: colour-major; inside a colour by descending column length, then
-  // Morton order.  Column lengths of a max-min Vecchia factor are very skewed
-  // (median ~m, max ~12m): equal lengths inside a 64-slot chunk remove the
-  // sliced-ELL padding, Morton order inside a length keeps the r gathers of a
-  // chunk spatially local.
+  // slots: colour-major.  Inside a colour the Morton-sorted list is cut into
+  // groups of kSlotGroup slots and each group is sorted by descending column
+  // length.  Column lengths of a max-min Vecchia factor are very skewed
+  // (median ~m, max ~12m): similar lengths inside a 64-lane chunk keep the
+  // sliced-ELL padding low, while a group stays spatially compact so the r
+  // gathers/scatters of its chunks hit a small, Morton-contiguous range of r.
   L.color_slot_ptr.assign(K + 1, 0);
   for (int i = 0; i < n; ++i) L.color_slot_ptr[colors[i]]++;
   for (int c = 0; c < K; ++c) L.color_slot_ptr[c + 1] += L.color_slot_ptr[c];
@@ -363,13 +364,19 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
   }
   L.slot_loc.resize(n);
   L.loc_slot.resize(n);
+  std::vector<int> group_starts;  // slot index where a group starts (all colours)
   {
     std::vector<int> f(L.color_slot_ptr.begin(), L.color_slot_ptr.end() - 1);
     for (int r = 0; r < n; ++r) { int i = perm[r]; int s = f[colors[i] - 1]++; L.slot_loc[s] = i; }
     for (int c = 0; c < K; ++c) {
-      auto a = L.slot_loc.begin() + L.color_slot_ptr[c], e = L.slot_loc.begin() + L.color_slot_ptr[c + 1];
-      std::stable_sort(a, e, [&](int x, int y) { return cptr[x + 1] - cptr[x] > cptr[y + 1] - cptr[y]; });
+      for (int g0 = L.color_slot_ptr[c]; g0 < L.color_slot_ptr[c + 1]; g0 += kSlotGroup) {
+        int g1 = std::min(g0 + kSlotGroup, L.color_slot_ptr[c + 1]);
+        group_starts.push_back(g0);
+        std::stable_sort(L.slot_loc.begin() + g0, L.slot_loc.begin() + g1,
+                         [&](int x, int y) { return cptr[x + 1] - cptr[x] > cptr[y + 1] - cptr[y]; });
+      }
     }
+    group_starts.push_back(n);
     for (int s = 0; s < n; ++s) L.loc_slot[L.slot_loc[s]] = s;
   }
   L.nnz = cptr[n];
@@ -381,7 +388,7 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
         int a = nn[(size_t)k * b + t];
         if (a < 0) continue;
         long long p = f[a]++;
-        crow[p] = k; csrc[p] = k * b + t;
+        crow[p] = k; csrc[p] = L.rpos[k] * b + t;  // device rows are Morton-ordered
       }
   }
   L.collen.resize(n);
@@ -390,46 +397,49 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
     L.collen[s] = (int)(cptr[i + 1] - cptr[i]);
     L.max_collen = std::max(L.max_collen, L.collen[s]);
   }
-  // chunks of 64 slots inside each colour
+  // chunks: walk each colour's slots (descending column length); a chunk
+  // starting at a slot of length l uses k = 2^lk lanes per slot with
+  // ceil(l/k) <= kRowsMax and takes up to 64/k slots.
   L.color_chunk_ptr.assign(K + 1, 0);
-  for (int c = 0; c < K; ++c) {
-    int sz = L.color_slot_ptr[c + 1] - L.color_slot_ptr[c];
-    L.color_chunk_ptr[c + 1] = L.color_chunk_ptr[c] + (sz + 63) / 64;
-  }
-  L.nchunks = L.color_chunk_ptr[K];
-  L.chunk_slot0.resize(L.nchunks);
-  L.chunk_len.resize(L.nchunks);
-  L.chunk_off.resize(L.nchunks + 1);
+  L.chunk_slot0.clear(); L.chunk_len.clear(); L.chunk_nslot.clear(); L.chunk_lk.clear(); L.chunk_off.clear();
   long long off = 0;
+  size_t gi = 0;
   for (int c = 0; c < K; ++c) {
-    int s0 = L.color_slot_ptr[c], s1 = L.color_slot_ptr[c + 1];
-    for (int ch = L.color_chunk_ptr[c]; ch < L.color_chunk_ptr[c + 1]; ++ch) {
-      int a = s0 + (ch - L.color_chunk_ptr[c]) * 64;
-      int e = std::min(s1, a + 64);
-      int mx = 0;
-      for (int s = a; s < e; ++s) mx = std::max(mx, L.collen[s]);
-      L.chunk_slot0[ch] = a;
-      L.chunk_len[ch] = mx;
-      L.chunk_off[ch] = off;
-      off += (long long)mx * 64;
+    while (group_starts[gi] < L.color_slot_ptr[c + 1]) {
+      int s = group_starts[gi], s1 = group_starts[gi + 1];
+      while (s < s1) {
+        int l = std::max(1, L.collen[s]);
+        int lk = 0;
+        while (lk < 6 && (l + (1 << lk) - 1) >> lk > kRowsMax) ++lk;
+        int k = 1 << lk;
+        int ns = std::min(64 >> lk, s1 - s);
+        int rows = (l + k - 1) / k;
+        L.chunk_slot0.push_back(s);
+        L.chunk_len.push_back(rows);
+        L.chunk_nslot.push_back(ns);
+        L.chunk_lk.push_back(lk);
+        L.chunk_off.push_back(off);
+        off += (long long)rows * 64;
+        s += ns;
+      }
+      ++gi;
     }
+    L.color_chunk_ptr[c + 1] = (int)L.chunk_slot0.size();
   }
-  L.chunk_off[L.nchunks] = off;
+  L.nchunks = (int)L.chunk_slot0.size();
+  L.chunk_off.push_back(off);
   L.n_entries = off;
   L.ent_rowpos.assign(off, 0);
   L.ent_src.assign(off, -1);
-  for (int c = 0; c < K; ++c) {
-    int s1 = L.color_slot_ptr[c + 1];
-    for (int ch = L.color_chunk_ptr[c]; ch < L.color_chunk_ptr[c + 1]; ++ch) {
-      for (int lane = 0; lane < 64; ++lane) {
-        int s = L.chunk_slot0[ch] + lane;
-        if (s >= s1) break;
-        int i = L.slot_loc[s];
-        for (long long p = cptr[i], jj = 0; p < cptr[i + 1]; ++p, ++jj) {
-          long long e = L.chunk_off[ch] + jj * 64 + lane;
-          L.ent_rowpos[e] = L.rpos[crow[p]];
-          L.ent_src[e] = csrc[p];
-        }
+  for (int ch = 0; ch < L.nchunks; ++ch) {
+    const int lk = L.chunk_lk[ch], k = 1 << lk;
+    for (int t = 0; t < L.chunk_nslot[ch]; ++t) {
+      int s = L.chunk_slot0[ch] + t;
+      int i = L.slot_loc[s];
+      for (long long p = cptr[i], j = 0; p < cptr[i + 1]; ++p, ++j) {
+        long long e = L.chunk_off[ch] + (j >> lk) * 64 + t * k + (j & (k - 1));
+        L.ent_rowpos[e] = L.rpos[crow[p]];
+        L.ent_src[e] = csrc[p];
       }
     }
   }

@@ -28,8 +28,13 @@ void morton_keys(const double* locs_colmajor, int n, int d, std::vector<uint64_t
 //  - slots: locations re-indexed colour-major (colour 1 first), spatially
 //    (Morton) sorted inside a colour;
 //  - r positions: Morton rank of each Vecchia row;
-//  - chunks: 64 consecutive slots of one colour (one wavefront);
-//  - entries: column i of B stored at chunk_off[ch] + jj*64 + lane.
+//  - chunks: one wavefront over 64/k consecutive slots of one colour, k =
+//    lanes per slot (power of two) chosen so that no chunk has more than
+//    kRowsMax rows (long columns of coarse max-min points are split over lanes);
+//  - entries: entry j of the t-th slot of a chunk stored at
+//    chunk_off[ch] + (j / k) * 64 + t * k + (j % k).
+constexpr int kRowsMax = 16;
+constexpr int kSlotGroup = 512;  // spatial group of same-colour slots (see build_sweep_layout)
 struct SweepLayout {
   int n = 0, b = 0, K = 0, nchunks = 0;
   long long nnz = 0, n_entries = 0;
@@ -38,13 +43,15 @@ struct SweepLayout {
   std::vector<int> color_chunk_ptr;  // K+1
   std::vector<int> slot_loc;         // n
   std::vector<int> loc_slot;         // n
-  std::vector<int> rpos;             // n: loc -> position in r
+  std::vector<int> rpos;             // n: loc -> device row (Morton rank): r, field, Linv rows
   std::vector<int> collen;           // n (slot order)
   std::vector<int> chunk_slot0;      // nchunks
-  std::vector<int> chunk_len;        // nchunks
+  std::vector<int> chunk_len;        // nchunks: rows of the chunk
+  std::vector<int> chunk_nslot;      // nchunks: slots in the chunk (<= 64/k)
+  std::vector<int> chunk_lk;         // nchunks: log2(k)
   std::vector<long long> chunk_off;  // nchunks
   std::vector<int> ent_rowpos;       // n_entries (padding: 0)
-  std::vector<int> ent_src;          // n_entries (row-major Linv index k*b+j; padding: -1)
+  std::vector<int> ent_src;          // n_entries (device Linv index rpos[k]*b+j; padding: -1)
 };
 
 bool build_sweep_layout(const int* nn_rowmajor, int n, int b, const int* colors,

@@ -19,17 +19,29 @@ struct SweepScalars {
   uint64_t counter_base;
 };
 
+constexpr int kSweepRows = 16;  // == kRowsMax of the layout planner
+
+// one wavefront's chunk of the sweep layout, loaded with one 16-byte scalar load
+struct __attribute__((aligned(16))) ChunkMeta {
+  int slot0;       // first slot
+  int packed;      // rows | nslot << 8 | lk << 16
+  long long off;   // first entry
+};
+// per-slot constants of the sweep, one 32-byte record per slot
+struct __attribute__((aligned(32))) SlotData {
+  double D;        // precision_diag
+  double R;        // residuals_sum
+  int nobs;        // obs_per_loc
+  int loc;         // location index (0-based, Vecchia order)
+  int collen;      // length of column loc of B
+  int dpos;        // device row of the location (Morton rank)
+};
+
 struct SweepDev {  // device pointers of the sliced-ELL layout
-  const int* chunk_slot0;
-  const int* chunk_len;
-  const long long* chunk_off;
-  const int* collen;
-  const int* slot_loc;
+  const ChunkMeta* meta;
+  SlotData* slots;
   const double* ent_val;
   const int* ent_rowpos;
-  const double* D_slot;
-  const double* R_slot;
-  const int* nobs_slot;
   double* w_slot;
   double* r;
 };
@@ -46,31 +58,28 @@ hipError_t launch_factor(hipStream_t st, int family, double var, double nugget, 
 
 // per-row statistics of B x (x shifted): partial sums of
 // {log L[k][0], u_k^2, a_k^2, a_k*u_k} with u = B (x - shift), a = B 1.
-// If out != nullptr, out[perm ? perm[k] : k] = u_k.  Returns #blocks used.
+// If out != nullptr, out[k] = u_k.  All arrays in device row order.
+// Returns #blocks used.
 int launch_row_stats(hipStream_t st, const double* linv, const int* nn, int n, int b,
-                     const double* x, double shift, double* out, const int* perm,
+                     const double* x, double shift, double* out,
                      double* partials /* kRedBlocks x 4 */,
                      const double* shift_dev = nullptr /* overrides shift when set */);
 // reduce `nblocks` x 4 partials into res[4] (deterministic order)
 hipError_t launch_reduce4(hipStream_t st, const double* partials, int nblocks, double* res);
 
-hipError_t launch_sell_refresh(hipStream_t st, const int* chunk_slot0, const long long* chunk_off,
-                               int nchunks, const int* slot_chunk_end_unused, const int* collen,
-                               int n, const int* ent_src, const double* linv, double* ent_val,
-                               double* D_slot);
+hipError_t launch_sell_refresh(hipStream_t st, const SweepDev& L, int nchunks, const int* ent_src,
+                               const double* linv, double* ent_val);
 
-hipError_t launch_residual_sums(hipStream_t st, int n, const int* slot_loc, const int* obs_ptr,
-                                const int* obs_idx, const double* y, const double* mu,
-                                double beta0, double* R_slot);
+hipError_t launch_residual_sums(hipStream_t st, int n, SlotData* slots, const int* obs_ptr,
+                                const int* obs_idx, const double* y, const double* mu, double beta0);
 
-hipError_t launch_field_to_slots(hipStream_t st, int n, const int* slot_loc, const double* field,
+hipError_t launch_field_to_slots(hipStream_t st, int n, const int* slot_dpos, const double* field,
                                  const SweepScalars* sc, double* w_slot);
-hipError_t launch_slots_to_field(hipStream_t st, int n, const int* slot_loc, const double* w_slot,
+hipError_t launch_slots_to_field(hipStream_t st, int n, const int* slot_dpos, const double* w_slot,
                                  const SweepScalars* sc, double* field);
 
 hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, int chunk_begin, int nchunks_color,
-                              int slot_end, const SweepScalars* sc, int sweep_local,
-                              const double* z, int n);
+                              const SweepScalars* sc, int sweep_local, const double* z, int n);
 
 // obs reductions: mode 0 -> partial[0] += (y - f[loc] - mu + beta0)^2
 //                 mode 1 -> partial[0] += ((y-b)^2 - (y-a)^2) / (2 sd^2),
@@ -83,6 +92,9 @@ hipError_t launch_tri_level(hipStream_t st, const int* rows, int nrows, const do
                             const int* nn, int b, const double* u, double* x);
 hipError_t launch_axpby_shift(hipStream_t st, int n, const double* x, double scale, double shift,
                               double* y);
+
+// busy-wait on the device for `seconds` (bounded; measurement helper)
+hipError_t launch_spin(hipStream_t st, double seconds);
 
 hipError_t launch_normals(hipStream_t st, uint64_t seed, uint64_t sweep, int n, double* z);
 

@@ -206,7 +206,8 @@ __global__ __launch_bounds__(64) void factor_kernel(double var, double nugget, d
                                                    double* __restrict__ linv, int* __restrict__ fail) {
   const int i = blockIdx.x * 64 + threadIdx.x;
   if (i >= n) return;
-  const int bs = min(i + 1, b);
+  int bs = b;  // rows are in device (Morton) order: count the valid neighbours
+  while (bs > 1 && nn[(size_t)i * b + bs - 1] < 0) --bs;
   double X[BM][DS];
 #pragma unroll
   for (int r = 0; r < BM; ++r) {
@@ -279,7 +280,8 @@ __global__ __launch_bounds__(64) void factor_kernel_rt(double var, double nugget
                                                       double* __restrict__ linv, int* __restrict__ fail) {
   const int i = blockIdx.x * 64 + threadIdx.x;
   if (i >= n) return;
-  const int bs = min(i + 1, b);
+  int bs = b;
+  while (bs > 1 && nn[(size_t)i * b + bs - 1] < 0) --bs;
   double X[kBMaxRt][DS];
   double L[kBMaxRt * (kBMaxRt + 1) / 2];
   double inv[kBMaxRt], x[kBMaxRt];
@@ -399,43 +401,59 @@ __device__ __forceinline__ void block_sum4(double v[4], double* out) {
   }
 }
 
+// G lanes per row (G >= b, power of two): lane g of a row reads entry g, so a
+// wave reads G*8 contiguous bytes of Linv per row; a G-lane butterfly sums it.
+template <int G>
 __global__ __launch_bounds__(256) void row_stats_kernel(const double* __restrict__ linv,
                                                         const int* __restrict__ nn, int n, int b,
                                                         const double* __restrict__ x, double shift,
                                                         double* __restrict__ out,
-                                                        const int* __restrict__ perm,
                                                         double* __restrict__ partials,
                                                         const double* __restrict__ shift_dev) {
   if (shift_dev) shift = *shift_dev;
   double acc[4] = {0, 0, 0, 0};
-  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-    const double* lr = linv + (size_t)k * b;
-    const int* nr = nn + (size_t)k * b;
-    double u = 0.0, a = 0.0;
-    for (int j = 0; j < b; ++j) {
-      int idx = nr[j];
-      if (idx < 0) continue;
-      double l = lr[j];
-      u += l * (x[idx] - shift);
-      a += l;
+  const int g = threadIdx.x & (G - 1);
+  const int rows_per_grid = gridDim.x * (blockDim.x / G);
+  for (int k = blockIdx.x * (blockDim.x / G) + threadIdx.x / G; k < n; k += rows_per_grid) {
+    double l = 0.0, xv = 0.0;
+    if (g < b) {
+      const int idx = nn[(size_t)k * b + g];
+      if (idx >= 0) {
+        l = linv[(size_t)k * b + g];
+        xv = x[idx] - shift;
+      }
     }
-    acc[0] += log(lr[0]);
-    acc[1] += u * u;
-    acc[2] += a * a;
-    acc[3] += a * u;
-    if (out) out[perm ? perm[k] : k] = u;
+    double u = l * xv, a = l;
+#pragma unroll
+    for (int off = 1; off < G; off <<= 1) {
+      u += __shfl_xor(u, off, 64);
+      a += __shfl_xor(a, off, 64);
+    }
+    if (g == 0) {
+      acc[0] += log(linv[(size_t)k * b]);
+      acc[1] += u * u;
+      acc[2] += a * a;
+      acc[3] += a * u;
+      if (out) out[k] = u;
+    }
   }
   block_sum4(acc, partials + 4 * blockIdx.x);
 }
 
 int launch_row_stats(hipStream_t st, const double* linv, const int* nn, int n, int b,
-                     const double* x, double shift, double* out, const int* perm,
-                     double* partials, const double* shift_dev) {
-  int g = (n + kBlock - 1) / kBlock;
+                     const double* x, double shift, double* out, double* partials,
+                     const double* shift_dev) {
+  const int G = b <= 4 ? 4 : b <= 8 ? 8 : b <= 16 ? 16 : 32;
+  long long rows_per_block = kBlock / G;
+  int g = (int)((n + rows_per_block - 1) / rows_per_block);
   if (g > kRedBlocks) g = kRedBlocks;
   if (g < 1) g = 1;
-  hipLaunchKernelGGL(row_stats_kernel, dim3(g), dim3(kBlock), 0, st, linv, nn, n, b, x, shift, out,
-                     perm, partials, shift_dev);
+  switch (G) {
+    case 4: hipLaunchKernelGGL(row_stats_kernel<4>, dim3(g), dim3(kBlock), 0, st, linv, nn, n, b, x, shift, out, partials, shift_dev); break;
+    case 8: hipLaunchKernelGGL(row_stats_kernel<8>, dim3(g), dim3(kBlock), 0, st, linv, nn, n, b, x, shift, out, partials, shift_dev); break;
+    case 16: hipLaunchKernelGGL(row_stats_kernel<16>, dim3(g), dim3(kBlock), 0, st, linv, nn, n, b, x, shift, out, partials, shift_dev); break;
+    default: hipLaunchKernelGGL(row_stats_kernel<32>, dim3(g), dim3(kBlock), 0, st, linv, nn, n, b, x, shift, out, partials, shift_dev); break;
+  }
   return g;
 }
 
@@ -454,105 +472,137 @@ hipError_t launch_reduce4(hipStream_t st, const double* partials, int nblocks, d
 }
 
 // ------------------------------------------------------------------ A5
-// refresh sweep-layout values of B from Linv and precision_diag per slot
-__global__ __launch_bounds__(256) void sell_refresh_kernel(const int* __restrict__ chunk_slot0,
-                                                           const long long* __restrict__ chunk_off,
-                                                           int nchunks, const int* __restrict__ collen,
-                                                           int n, const int* __restrict__ ent_src,
-                                                           const double* __restrict__ linv,
-                                                           double* __restrict__ ent_val,
-                                                           double* __restrict__ D_slot) {
-  const int ch = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (ch >= nchunks) return;
-  const int s = chunk_slot0[ch] + lane;
-  if (s >= n) return;
-  // slot s belongs to this chunk only if it is below the next chunk's first slot
-  if (ch + 1 < nchunks && s >= chunk_slot0[ch + 1]) return;
-  const int len = collen[s];
-  const long long base = chunk_off[ch] + lane;
-  double D = 0.0;
-  for (int j = 0; j < len; ++j) {
-    long long e = base + (long long)j * 64;
-    double v = linv[ent_src[e]];
-    ent_val[e] = v;
-    D += v * v;
-  }
-  D_slot[s] = D;
+// lane -> (slot, sub-lane) of a chunk: k = 2^lk lanes per slot.  The chunk
+// index is wave-uniform (readfirstlane) so its metadata is a scalar load.
+struct ChunkLane {
+  int lk, k, t, u, s, rows;
+  bool valid;
+  long long base;
+};
+__device__ __forceinline__ ChunkLane chunk_lane(const SweepDev& L, int ch, int lane) {
+  ch = __builtin_amdgcn_readfirstlane(ch);
+  const ChunkMeta m = L.meta[ch];
+  ChunkLane c;
+  c.rows = m.packed & 0xFF;
+  const int nslot = (m.packed >> 8) & 0xFF;
+  c.lk = (m.packed >> 16) & 0xFF;
+  c.k = 1 << c.lk;
+  c.t = lane >> c.lk;
+  c.u = lane & (c.k - 1);
+  c.valid = c.t < nslot;
+  c.s = m.slot0 + (c.valid ? c.t : 0);
+  c.base = m.off + lane;
+  return c;
 }
 
-hipError_t launch_sell_refresh(hipStream_t st, const int* chunk_slot0, const long long* chunk_off,
-                               int nchunks, const int*, const int* collen, int n, const int* ent_src,
-                               const double* linv, double* ent_val, double* D_slot) {
+// sum over the k lanes of a slot; xor butterfly => bitwise-identical result
+// in every lane of the group (IEEE addition is commutative)
+__device__ __forceinline__ double group_sum(double v, int k) {
+  for (int off = 1; off < k; off <<= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// refresh sweep-layout values of B from Linv and precision_diag per slot
+__global__ __launch_bounds__(256) void sell_refresh_kernel(SweepDev L, int nchunks,
+                                                           const int* __restrict__ ent_src,
+                                                           const double* __restrict__ linv,
+                                                           double* __restrict__ ent_val) {
+  const int ch = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ch >= nchunks) return;
+  const ChunkLane c = chunk_lane(L, ch, threadIdx.x & 63);
+  const int len = c.valid ? L.slots[c.s].collen : 0;
+  // all loads first (clamped rows, unconditional), then the stores: no
+  // per-row round trip (padding entries have src -1 -> read linv[0], unused)
+  int src[kSweepRows];
+  double v[kSweepRows];
+#pragma unroll
+  for (int j = 0; j < kSweepRows; ++j) src[j] = ent_src[c.base + (long long)min(j, c.rows - 1) * 64];
+#pragma unroll
+  for (int j = 0; j < kSweepRows; ++j) v[j] = linv[max(src[j], 0)];
+  double D = 0.0;
+#pragma unroll
+  for (int j = 0; j < kSweepRows; ++j) D += (j * c.k + c.u < len) ? v[j] * v[j] : 0.0;
+#pragma unroll
+  for (int j = 0; j < kSweepRows; ++j)
+    if (j * c.k + c.u < len) ent_val[c.base + (long long)j * 64] = v[j];
+  D = group_sum(D, c.k);
+  if (c.valid && c.u == 0) L.slots[c.s].D = D;
+}
+
+hipError_t launch_sell_refresh(hipStream_t st, const SweepDev& L, int nchunks, const int* ent_src,
+                               const double* linv, double* ent_val) {
   int g = (nchunks + 3) / 4;
-  hipLaunchKernelGGL(sell_refresh_kernel, dim3(g), dim3(kBlock), 0, st, chunk_slot0, chunk_off,
-                     nchunks, collen, n, ent_src, linv, ent_val, D_slot);
+  hipLaunchKernelGGL(sell_refresh_kernel, dim3(g), dim3(kBlock), 0, st, L, nchunks, ent_src, linv,
+                     ent_val);
   return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ A7
-__global__ void residual_sums_kernel(int n, const int* __restrict__ slot_loc,
+__global__ void residual_sums_kernel(int n, SlotData* __restrict__ slots,
                                      const int* __restrict__ obs_ptr, const int* __restrict__ obs_idx,
                                      const double* __restrict__ y, const double* __restrict__ mu,
-                                     double beta0, double* __restrict__ R_slot) {
+                                     double beta0) {
   int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;
-  int loc = slot_loc[s];
+  int loc = slots[s].loc;
   double R = 0.0;
   for (int p = obs_ptr[loc]; p < obs_ptr[loc + 1]; ++p) {
     int o = obs_idx[p];
     R += y[o] - (mu ? mu[o] : beta0);
   }
-  R_slot[s] = R;
+  slots[s].R = R;
 }
 
-hipError_t launch_residual_sums(hipStream_t st, int n, const int* slot_loc, const int* obs_ptr,
-                                const int* obs_idx, const double* y, const double* mu,
-                                double beta0, double* R_slot) {
+hipError_t launch_residual_sums(hipStream_t st, int n, SlotData* slots, const int* obs_ptr,
+                                const int* obs_idx, const double* y, const double* mu, double beta0) {
   int g = (n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(residual_sums_kernel, dim3(g), dim3(kBlock), 0, st, n, slot_loc, obs_ptr,
-                     obs_idx, y, mu, beta0, R_slot);
+  hipLaunchKernelGGL(residual_sums_kernel, dim3(g), dim3(kBlock), 0, st, n, slots, obs_ptr, obs_idx,
+                     y, mu, beta0);
   return hipGetLastError();
 }
 
-__global__ void field_to_slots_kernel(int n, const int* __restrict__ slot_loc,
+__global__ void field_to_slots_kernel(int n, const int* __restrict__ slot_dpos,
                                       const double* __restrict__ field,
                                       const SweepScalars* __restrict__ sc, double* __restrict__ w) {
   int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < n) w[s] = field[slot_loc[s]] - sc->beta0;
+  if (s < n) w[s] = field[slot_dpos[s]] - sc->beta0;
 }
-__global__ void slots_to_field_kernel(int n, const int* __restrict__ slot_loc,
+__global__ void slots_to_field_kernel(int n, const int* __restrict__ slot_dpos,
                                       const double* __restrict__ w,
                                       const SweepScalars* __restrict__ sc, double* __restrict__ field) {
   int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < n) field[slot_loc[s]] = w[s] + sc->beta0;
+  if (s < n) field[slot_dpos[s]] = w[s] + sc->beta0;
 }
 
-hipError_t launch_field_to_slots(hipStream_t st, int n, const int* slot_loc, const double* field,
+hipError_t launch_field_to_slots(hipStream_t st, int n, const int* slot_dpos, const double* field,
                                  const SweepScalars* sc, double* w_slot) {
   int g = (n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(field_to_slots_kernel, dim3(g), dim3(kBlock), 0, st, n, slot_loc, field, sc, w_slot);
+  hipLaunchKernelGGL(field_to_slots_kernel, dim3(g), dim3(kBlock), 0, st, n, slot_dpos, field, sc, w_slot);
   return hipGetLastError();
 }
-hipError_t launch_slots_to_field(hipStream_t st, int n, const int* slot_loc, const double* w_slot,
+hipError_t launch_slots_to_field(hipStream_t st, int n, const int* slot_dpos, const double* w_slot,
                                  const SweepScalars* sc, double* field) {
   int g = (n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(slots_to_field_kernel, dim3(g), dim3(kBlock), 0, st, n, slot_loc, w_slot, sc, field);
+  hipLaunchKernelGGL(slots_to_field_kernel, dim3(g), dim3(kBlock), 0, st, n, slot_dpos, w_slot, sc, field);
   return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ A1
-// One colour of the chromatic sweep, local form.  One wavefront per chunk
-// of 64 same-colour slots, one lane per location:
+// One colour of the chromatic sweep, local form.  One wavefront per chunk;
+// k lanes per location (k = 1 for typical columns, up to 16 for the long
+// columns of coarse max-min points), so every lane owns <= kSweepRows entries
+// and issues all its loads at once (clamped duplicate loads keep the loads
+// unconditional; the duplicates hit in cache).  Three dependent memory round
+// trips per wave: chunk metadata (scalar) -> entries + slot record + w ->
+// r gathers; then compute and the conflict-free scatter:
 //   acc  = sum_{k in col(i)} B[k,i] r_k - D_i w_i      (= (B^T B w_{!c})_i)
 //   P    = D_i/s2 + n_i/t2
 //   w_i' = (R_i/t2 - acc/s2)/P + z_i/sqrt(P)
-//   r_k += B[k,i] (w_i' - w_i)                          (conflict-free in a colour)
+//   r_k += B[k,i] (w_i' - w_i)
 // Blocks are remapped so that consecutive (spatially adjacent) chunks run on
 // the same XCD and share its L2 for the r gathers.
 template <bool INJECT>
 __global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, int chunk_begin, int nchunks_color,
-                                                          int slot_end,
                                                           const SweepScalars* __restrict__ scal,
                                                           int sweep_local, const double* __restrict__ z,
                                                           int n) {
@@ -561,63 +611,49 @@ __global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, int chunk_
   const int lb = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + (bid >> 3);
   const int lch = lb * 4 + (threadIdx.x >> 6);
   if (lch >= nchunks_color) return;
-  const int lane = threadIdx.x & 63;
-  const int ch = chunk_begin + lch;
-  const int s = L.chunk_slot0[ch] + lane;
-  const bool valid = s < slot_end;
-  const int len = valid ? L.collen[s] : 0;
-  const int clen = L.chunk_len[ch];
-  const double* __restrict__ vp = L.ent_val + L.chunk_off[ch] + lane;
-  const int* __restrict__ pp = L.ent_rowpos + L.chunk_off[ch] + lane;
-  const double* r = L.r;  // r is also written below: no __restrict__
-
-  double acc = 0.0;
-  int j = 0;
-  for (; j + 4 <= clen; j += 4) {
-    double v0 = vp[(j + 0) * 64], v1 = vp[(j + 1) * 64], v2 = vp[(j + 2) * 64], v3 = vp[(j + 3) * 64];
-    int p0 = pp[(j + 0) * 64], p1 = pp[(j + 1) * 64], p2 = pp[(j + 2) * 64], p3 = pp[(j + 3) * 64];
-    double r0 = r[p0], r1 = r[p1], r2 = r[p2], r3 = r[p3];
-    acc += (j + 0 < len) ? v0 * r0 : 0.0;
-    acc += (j + 1 < len) ? v1 * r1 : 0.0;
-    acc += (j + 2 < len) ? v2 * r2 : 0.0;
-    acc += (j + 3 < len) ? v3 * r3 : 0.0;
+  const ChunkLane c = chunk_lane(L, chunk_begin + lch, threadIdx.x & 63);
+  double* r = L.r;  // gathered then scattered: no __restrict__
+  const SlotData sd = L.slots[c.s];
+  const double w = L.w_slot[c.s];
+  const int len = c.valid ? sd.collen : 0;
+  double v[kSweepRows], rv[kSweepRows];
+  int p[kSweepRows];
+#pragma unroll
+  for (int j = 0; j < kSweepRows; ++j) {
+    const long long e = c.base + (long long)min(j, c.rows - 1) * 64;
+    v[j] = L.ent_val[e];
+    p[j] = L.ent_rowpos[e];
   }
-  for (; j < clen; ++j) {
-    double v = vp[j * 64];
-    int p = pp[j * 64];
-    double rv = r[p];
-    acc += (j < len) ? v * rv : 0.0;
-  }
-  if (!valid) return;
   const double inv_s2 = scal->inv_s2, inv_t2 = scal->inv_t2;
-  const double D = L.D_slot[s];
-  const double w = L.w_slot[s];
-  acc -= D * w;
-  const double P = D * inv_s2 + (double)L.nobs_slot[s] * inv_t2;
-  const int loc = L.slot_loc[s];
   double zz;
-  if (INJECT) zz = z[(size_t)sweep_local * n + loc];
-  else zz = normal_at(scal->seed, scal->counter_base + (uint64_t)sweep_local, (uint32_t)loc);
-  const double wn = (inv_t2 * L.R_slot[s] - inv_s2 * acc) / P + zz / sqrt(P);
+  if (INJECT) zz = z[(size_t)sweep_local * n + sd.loc];
+  else zz = normal_at(scal->seed, scal->counter_base + (uint64_t)sweep_local, (uint32_t)sd.loc);
+#pragma unroll
+  for (int j = 0; j < kSweepRows; ++j) rv[j] = r[p[j]];
+  double acc = 0.0;
+#pragma unroll
+  for (int j = 0; j < kSweepRows; ++j) acc += (j * c.k + c.u < len) ? v[j] * rv[j] : 0.0;
+  acc = group_sum(acc, c.k);
+  if (!c.valid) return;
+  acc -= sd.D * w;
+  const double P = sd.D * inv_s2 + (double)sd.nobs * inv_t2;
+  const double wn = (inv_t2 * sd.R - inv_s2 * acc) / P + zz / sqrt(P);
   const double dw = wn - w;
-  L.w_slot[s] = wn;
-  double* rw = L.r;
-  for (int jj = 0; jj < len; ++jj) {
-    int p = pp[jj * 64];
-    rw[p] += vp[jj * 64] * dw;
-  }
+  if (c.u == 0) L.w_slot[c.s] = wn;
+#pragma unroll
+  for (int j = 0; j < kSweepRows; ++j)
+    if (j * c.k + c.u < len) r[p[j]] = rv[j] + v[j] * dw;
 }
 
 hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, int chunk_begin, int nchunks_color,
-                              int slot_end, const SweepScalars* sc, int sweep_local,
-                              const double* z, int n) {
+                              const SweepScalars* sc, int sweep_local, const double* z, int n) {
   int g = (nchunks_color + 3) / 4;
   if (z)
     hipLaunchKernelGGL((sweep_color_kernel<true>), dim3(g), dim3(kBlock), 0, st, L, chunk_begin,
-                       nchunks_color, slot_end, sc, sweep_local, z, n);
+                       nchunks_color, sc, sweep_local, z, n);
   else
     hipLaunchKernelGGL((sweep_color_kernel<false>), dim3(g), dim3(kBlock), 0, st, L, chunk_begin,
-                       nchunks_color, slot_end, sc, sweep_local, z, n);
+                       nchunks_color, sc, sweep_local, z, n);
   return hipGetLastError();
 }
 
@@ -689,6 +725,21 @@ hipError_t launch_axpby_shift(hipStream_t st, int n, const double* x, double sca
                               double* y) {
   int g = (n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(axpby_shift_kernel, dim3(g), dim3(kBlock), 0, st, n, x, scale, shift, y);
+  return hipGetLastError();
+}
+
+__global__ void spin_kernel(unsigned long long ticks) {
+  // wall_clock64(): constant 100 MHz counter on gfx950
+  unsigned long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+hipError_t launch_spin(hipStream_t st, double seconds) {
+  if (seconds > 1.0) seconds = 1.0;
+  int rate = 0;
+  if (hipDeviceGetAttribute(&rate, hipDeviceAttributeWallClockRate, 0) != hipSuccess || rate <= 0) rate = 100000;
+  unsigned long long ticks = (unsigned long long)(seconds * rate * 1e3);  // rate in kHz
+  hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, st, ticks);
   return hipGetLastError();
 }
 
