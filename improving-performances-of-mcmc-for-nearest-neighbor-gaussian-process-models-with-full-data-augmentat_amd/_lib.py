@@ -44,7 +44,8 @@ class NNGPError(RuntimeError):
 class Info(C.Structure):
     _fields_ = [("n", C.c_int), ("b", C.c_int), ("d", C.c_int), ("n_obs", C.c_int),
                 ("n_colors", C.c_int), ("n_levels", C.c_int), ("nnz", C.c_longlong),
-                ("n_entries", C.c_longlong), ("max_collen", C.c_int), ("device", C.c_int)]
+                ("n_entries", C.c_longlong), ("max_collen", C.c_int), ("device", C.c_int),
+                ("n_tiles", C.c_int), ("n_boundary", C.c_longlong), ("sweep_mode", C.c_int)]
 
 
 _dp = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")

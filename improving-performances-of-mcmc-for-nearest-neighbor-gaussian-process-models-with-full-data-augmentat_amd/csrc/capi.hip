@@ -7,6 +7,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <new>
@@ -38,12 +39,19 @@ struct nngp_ctx {
   double* linv_d[2] = {nullptr, nullptr};
   int* fail_d = nullptr;
   ChunkMeta* meta_d = nullptr;
+  int* lane_tab_d = nullptr;
   SlotData* slots_d = nullptr;
   int* slot_dpos_d = nullptr;
   int* ent_rowpos_d = nullptr;
   int* ent_src_d = nullptr;
   double* ent_val_d = nullptr;
   double* w_slot_d = nullptr;
+  int* tile_chunks_d = nullptr;
+  int* nbr_ptr_d = nullptr;
+  int* nbr_idx_d = nullptr;
+  int* progress_d = nullptr;  // n_tiles progress counters + 1 error word
+  int n_tiles = 1;
+  bool persistent = true;     // NNGP_SWEEP=launch selects one kernel per colour
   double* r_d = nullptr;
   int* level_rows_d = nullptr;
   int* obs_ptr_d = nullptr;
@@ -112,6 +120,7 @@ int set_device(nngp_ctx* c) {
 SweepDev sweep_dev(nngp_ctx* c) {
   SweepDev L;
   L.meta = c->meta_d;
+  L.lane_tab = c->lane_tab_d;
   L.slots = c->slots_d;
   L.ent_val = c->ent_val_d;
   L.ent_rowpos = c->ent_rowpos_d;
@@ -212,7 +221,8 @@ void nngp_ctx_destroy(nngp_ctx* c) {
   for (auto& kv : c->graphs) hipGraphExecDestroy(kv.second);
   for (auto g : c->graph_objs) hipGraphDestroy(g);
   void* ptrs[] = {c->locs_d, c->sc_d, c->nn_d, c->linv_d[0], c->linv_d[1], c->fail_d,
-                  c->meta_d, c->slots_d, c->slot_dpos_d, c->ent_rowpos_d, c->ent_src_d, c->ent_val_d, c->w_slot_d, c->r_d, c->level_rows_d, c->obs_ptr_d, c->obs_idx_d,
+                  c->meta_d, c->lane_tab_d, c->slots_d, c->slot_dpos_d, c->ent_rowpos_d, c->tile_chunks_d, c->nbr_ptr_d,
+                  c->nbr_idx_d, c->progress_d, c->ent_src_d, c->ent_val_d, c->w_slot_d, c->r_d, c->level_rows_d, c->obs_ptr_d, c->obs_idx_d,
                   c->lm_d, c->y_d, c->mu_d, c->field_d, c->field_prop_d, c->tmp_d, c->tmp2_d,
                   c->partials_d, c->res_d, c->z_d, c->scal_d};
   for (void* p : ptrs) if (p) hipFree(p);
@@ -272,9 +282,33 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
     std::vector<int> f(obs_cnt.begin(), obs_cnt.end() - 1);
     for (int o = 0; o < n_obs; ++o) obs_idx[f[lm0[o]]++] = o;
   }
-  if (!build_sweep_layout(nn.data(), n, b, coloring, locs, d, c->lay, err)) {
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1) ncu = 1;
+    c->n_tiles = std::max(1, std::min(ncu, n / 1024));
+    const char* mode = std::getenv("NNGP_SWEEP");
+    c->persistent = !(mode && std::string(mode) == "launch");
+  }
+  if (!build_sweep_layout(nn.data(), n, b, coloring, locs, d, c->n_tiles, c->lay, err)) {
     delete c;
     return fail_msg(nullptr, NNGP_ERR_ARG, err);
+  }
+  {
+    // every chunk of colour c belongs to exactly one tile range of colour c
+    const SweepLayout& Ly = c->lay;
+    std::vector<int> owner(Ly.nchunks, 0);
+    for (int col = 0; col < Ly.K; ++col)
+      for (int t = 0; t < Ly.n_tiles; ++t) {
+        const int* tc = &Ly.tile_chunks[((size_t)col * Ly.n_tiles + t) * 3];
+        if (!(Ly.color_chunk_ptr[col] <= tc[0] && tc[0] <= tc[1] && tc[1] <= tc[2] &&
+              tc[2] <= Ly.color_chunk_ptr[col + 1])) {
+          delete c;
+          return fail_msg(nullptr, NNGP_ERR_ARG, "internal: bad tile chunk range");
+        }
+        for (int ch = tc[0]; ch < tc[2]; ++ch) owner[ch]++;
+      }
+    for (int ch = 0; ch < Ly.nchunks; ++ch)
+      if (owner[ch] != 1) { delete c; return fail_msg(nullptr, NNGP_ERR_ARG, "internal: tile ranges do not partition the chunks"); }
   }
   dag_levels(nn.data(), n, b, c->level_ptr, c->level_rows);
   c->dpos = c->lay.rpos;
@@ -315,8 +349,13 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
   CK(dalloc(&c->linv_d[1], (size_t)n * b));
   CK(dalloc(&c->fail_d, 1));
   CK(dalloc(&c->meta_d, L.nchunks));
+  CK(dalloc(&c->lane_tab_d, L.lane_tab.size()));
   CK(dalloc(&c->slots_d, n));
   CK(dalloc(&c->slot_dpos_d, n));
+  CK(dalloc(&c->tile_chunks_d, L.tile_chunks.size()));
+  CK(dalloc(&c->nbr_ptr_d, L.nbr_ptr.size()));
+  CK(dalloc(&c->nbr_idx_d, std::max<size_t>(1, L.nbr_idx.size())));
+  CK(dalloc(&c->progress_d, (size_t)c->n_tiles + 4));
   CK(dalloc(&c->ent_rowpos_d, (size_t)L.n_entries));
   CK(dalloc(&c->ent_src_d, (size_t)L.n_entries));
   CK(dalloc(&c->ent_val_d, (size_t)L.n_entries));
@@ -343,7 +382,7 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
     std::vector<ChunkMeta> meta(L.nchunks);
     for (int ch = 0; ch < L.nchunks; ++ch) {
       meta[ch].slot0 = L.chunk_slot0[ch];
-      meta[ch].packed = L.chunk_len[ch] | (L.chunk_nslot[ch] << 8) | (L.chunk_lk[ch] << 16);
+      meta[ch].packed = L.chunk_len[ch] | (std::min(L.chunk_nslot[ch], 255) << 8) | (L.chunk_lk[ch] << 16);
       meta[ch].off = L.chunk_off[ch];
     }
     std::vector<SlotData> sd(n);
@@ -356,9 +395,13 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
       sd[s].dpos = slot_dpos[s];
     }
     CK(hipMemcpy(c->meta_d, meta.data(), sizeof(ChunkMeta) * meta.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(c->lane_tab_d, L.lane_tab.data(), sizeof(int) * L.lane_tab.size(), hipMemcpyHostToDevice));
     CK(hipMemcpy(c->slots_d, sd.data(), sizeof(SlotData) * sd.size(), hipMemcpyHostToDevice));
   }
   CK(upload(c->slot_dpos_d, slot_dpos.data(), n, c->st));
+  CK(upload(c->tile_chunks_d, L.tile_chunks.data(), L.tile_chunks.size(), c->st));
+  CK(upload(c->nbr_ptr_d, L.nbr_ptr.data(), L.nbr_ptr.size(), c->st));
+  CK(upload(c->nbr_idx_d, L.nbr_idx.data(), L.nbr_idx.size(), c->st));
   CK(upload(c->ent_rowpos_d, L.ent_rowpos.data(), (size_t)L.n_entries, c->st));
   CK(upload(c->ent_src_d, L.ent_src.data(), (size_t)L.n_entries, c->st));
   CK(hipMemsetAsync(c->ent_val_d, 0, sizeof(double) * std::max<long long>(1, L.n_entries), c->st));
@@ -382,6 +425,9 @@ int nngp_ctx_info(const nngp_ctx* c, nngp_info* info) {
   info->n_entries = c->lay.n_entries;
   info->max_collen = c->lay.max_collen;
   info->device = c->device;
+  info->n_tiles = c->n_tiles;
+  info->n_boundary = c->lay.n_boundary;
+  info->sweep_mode = c->persistent ? 1 : 0;
   return NNGP_OK;
 }
 
@@ -589,6 +635,16 @@ static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, const double* z_dev,
                    &c->scal_d->beta0);
   HIPCHK(c, hipGetLastError());
   SweepDev L = sweep_dev(c);
+  if (c->persistent) {
+    // zero the progress counters + error word every call (graph memset node)
+    HIPCHK(c, launch_fill_int(c->st, c->progress_d, c->n_tiles + 4, 0));
+    if (evs) HIPCHK(c, hipEventRecord((*evs)[0], c->st));
+    HIPCHK(c, launch_sweep_persistent(c->st, L, c->tile_chunks_d, c->n_tiles, c->lay.K, n_sweeps, c->nbr_ptr_d,
+                                      c->nbr_idx_d, c->progress_d, c->progress_d + c->n_tiles, c->scal_d, z_dev, n));
+    if (evs) HIPCHK(c, hipEventRecord((*evs)[1], c->st));
+    HIPCHK(c, launch_slots_to_field(c->st, n, c->slot_dpos_d, c->w_slot_d, c->scal_d, c->field_d));
+    return NNGP_OK;
+  }
   for (int s = 0; s < n_sweeps; ++s) {
     for (int col = 0; col < c->lay.K; ++col) {
       int ch0 = c->lay.color_chunk_ptr[col];
@@ -599,6 +655,23 @@ static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, const double* z_dev,
     }
   }
   HIPCHK(c, launch_slots_to_field(c->st, n, c->slot_dpos_d, c->w_slot_d, c->scal_d, c->field_d));
+  return NNGP_OK;
+}
+
+static int check_persistent(nngp_ctx* c) {
+  if (!c->persistent) return NNGP_OK;
+  std::vector<int> prog(c->n_tiles + 4);
+  HIPCHK(c, hipMemcpy(prog.data(), c->progress_d, sizeof(int) * prog.size(), hipMemcpyDeviceToHost));
+  const int e = prog[c->n_tiles];
+  if (e) {
+    int mn = prog[0], mx = prog[0];
+    for (int t = 0; t < c->n_tiles; ++t) { mn = std::min(mn, prog[t]); mx = std::max(mx, prog[t]); }
+    char buf[200];
+    std::snprintf(buf, sizeof buf,
+                  "persistent sweep: error word 0x%08x (tile %d timed out); progress min %d max %d of %d tiles",
+                  (unsigned)e, e - 1, mn, mx, c->n_tiles);
+    return fail_msg(c, NNGP_ERR_HIP, buf);
+  }
   return NNGP_OK;
 }
 
@@ -638,7 +711,7 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
     HIPCHK(c, hipGraphLaunch(it->second, c->st));
   }
   HIPCHK(c, hipStreamSynchronize(c->st));
-  return NNGP_OK;
+  return check_persistent(c);
 }
 
 int nngp_sweep_timed(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double lnv,
@@ -652,7 +725,7 @@ int nngp_sweep_timed(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, 
   HIPCHK(c, hipEventCreate(&e1));
   std::vector<hipEvent_t> evs;
   if (kernel_ms) {
-    evs.resize(2 * (size_t)n_sweeps * c->lay.K);
+    evs.resize(c->persistent ? 2 : 2 * (size_t)n_sweeps * c->lay.K);
     for (auto& e : evs) HIPCHK(c, hipEventCreate(&e));
     // a bounded spin kernel keeps the GPU busy while the host enqueues the
     // event-bracketed launches, so no host submission gap lands inside a

@@ -325,7 +325,7 @@ int greedy_coloring(const int* nn, int n, int b, std::vector<int>& colors) {
 
 // ---------------------------------------------------------------- layout
 bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const double* locs, int d,
-                        SweepLayout& L, std::string& err) {
+                        int n_tiles, SweepLayout& L, std::string& err) {
   L = SweepLayout();
   L.n = n; L.b = b;
   int K = 0;
@@ -350,12 +350,45 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
     if (a >= 0) cptr[a + 1]++;
   }
   for (int i = 0; i < n; ++i) cptr[i + 1] += cptr[i];
-  // slots: colour-major.  Inside a colour the Morton-sorted list is cut into
-  // groups of kSlotGroup slots and each group is sorted by descending column
-  // length.  Column lengths of a max-min Vecchia factor are very skewed
-  // (median ~m, max ~12m): similar lengths inside a 64-lane chunk keep the
-  // sliced-ELL padding low, while a group stays spatially compact so the r
-  // gathers/scatters of its chunks hit a small, Morton-contiguous range of r.
+  // tiles: contiguous Morton ranges; boundary = a moral neighbour in another tile
+  const int T = std::max(1, std::min(n_tiles, n));
+  L.n_tiles = T;
+  std::vector<int> tile(n);
+  for (int i = 0; i < n; ++i) tile[i] = (int)((long long)L.rpos[i] * T / n);
+  std::vector<long long> crow_ptr(cptr);  // rows of column i: built below (needs crow)
+  std::vector<int> rows_of(cptr[n]);
+  {
+    std::vector<long long> f(cptr.begin(), cptr.end() - 1);
+    for (int k = 0; k < n; ++k)
+      for (int t = 0; t < b; ++t) {
+        int a2 = nn[(size_t)k * b + t];
+        if (a2 >= 0) rows_of[f[a2]++] = k;
+      }
+  }
+  std::vector<char> boundary(n, 0);
+  std::vector<std::vector<int>> nbrs(T);
+  for (int i = 0; i < n; ++i) {
+    for (long long q = cptr[i]; q < cptr[i + 1]; ++q) {
+      int k = rows_of[q];
+      for (int t = 0; t < b; ++t) {
+        int j = nn[(size_t)k * b + t];
+        if (j >= 0 && tile[j] != tile[i]) { boundary[i] = 1; nbrs[tile[i]].push_back(tile[j]); }
+      }
+    }
+  }
+  L.nbr_ptr.assign(T + 1, 0);
+  L.nbr_idx.clear();
+  for (int t = 0; t < T; ++t) {
+    auto& v = nbrs[t];
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+    L.nbr_idx.insert(L.nbr_idx.end(), v.begin(), v.end());
+    L.nbr_ptr[t + 1] = (int)L.nbr_idx.size();
+  }
+  // slots: colour-major; inside a colour by (tile, boundary first, Morton).
+  // Column lengths of a max-min Vecchia factor are very skewed (median ~m,
+  // max ~12m): long columns get more lanes (chunk planner), not a separate
+  // sort, so every chunk stays spatially compact.
   L.color_slot_ptr.assign(K + 1, 0);
   for (int i = 0; i < n; ++i) L.color_slot_ptr[colors[i]]++;
   for (int c = 0; c < K; ++c) L.color_slot_ptr[c + 1] += L.color_slot_ptr[c];
@@ -364,21 +397,33 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
   }
   L.slot_loc.resize(n);
   L.loc_slot.resize(n);
-  std::vector<int> group_starts;  // slot index where a group starts (all colours)
+  std::vector<int> group_starts;  // slot index where a (colour, tile, class) group starts
+  std::vector<int> group_tile, group_class;
   {
     std::vector<int> f(L.color_slot_ptr.begin(), L.color_slot_ptr.end() - 1);
-    for (int r = 0; r < n; ++r) { int i = perm[r]; int s = f[colors[i] - 1]++; L.slot_loc[s] = i; }
+    for (int r = 0; r < n; ++r) { int i = perm[r]; int s2 = f[colors[i] - 1]++; L.slot_loc[s2] = i; }
     for (int c = 0; c < K; ++c) {
-      for (int g0 = L.color_slot_ptr[c]; g0 < L.color_slot_ptr[c + 1]; g0 += kSlotGroup) {
-        int g1 = std::min(g0 + kSlotGroup, L.color_slot_ptr[c + 1]);
-        group_starts.push_back(g0);
-        std::stable_sort(L.slot_loc.begin() + g0, L.slot_loc.begin() + g1,
-                         [&](int x, int y) { return cptr[x + 1] - cptr[x] > cptr[y + 1] - cptr[y]; });
+      int a0 = L.color_slot_ptr[c], a1 = L.color_slot_ptr[c + 1];
+      // Morton order already implies tile order; sort inside a tile by class then length
+      std::stable_sort(L.slot_loc.begin() + a0, L.slot_loc.begin() + a1, [&](int x, int y) {
+        if (tile[x] != tile[y]) return tile[x] < tile[y];
+        return boundary[x] > boundary[y];  // stable: Morton order inside a class
+      });
+      for (int s2 = a0; s2 < a1;) {
+        int tt = tile[L.slot_loc[s2]], cl = boundary[L.slot_loc[s2]];
+        int e2 = s2;
+        while (e2 < a1 && tile[L.slot_loc[e2]] == tt && boundary[L.slot_loc[e2]] == cl) ++e2;
+        // split large groups spatially?  groups are <= n/(T*K) slots: keep whole
+        group_starts.push_back(s2);
+        group_tile.push_back(tt);
+        group_class.push_back(cl);
+        s2 = e2;
       }
     }
     group_starts.push_back(n);
-    for (int s = 0; s < n; ++s) L.loc_slot[L.slot_loc[s]] = s;
+    for (int s2 = 0; s2 < n; ++s2) L.loc_slot[L.slot_loc[s2]] = s2;
   }
+  for (int i = 0; i < n; ++i) L.n_boundary += boundary[i];
   L.nnz = cptr[n];
   std::vector<int> crow(L.nnz), csrc(L.nnz);
   {
@@ -402,29 +447,74 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
   // ceil(l/k) <= kRowsMax and takes up to 64/k slots.
   L.color_chunk_ptr.assign(K + 1, 0);
   L.chunk_slot0.clear(); L.chunk_len.clear(); L.chunk_nslot.clear(); L.chunk_lk.clear(); L.chunk_off.clear();
+  L.lane_tab.clear();
+  if (n >= (1 << 28) - 1) { err = "n too large for the sweep lane table (< 2^28)"; return false; }
   long long off = 0;
+  (void)crow_ptr;
   size_t gi = 0;
+  L.tile_chunks.assign((size_t)K * T * 3, -1);
   for (int c = 0; c < K; ++c) {
     while (group_starts[gi] < L.color_slot_ptr[c + 1]) {
-      int s = group_starts[gi], s1 = group_starts[gi + 1];
-      while (s < s1) {
-        int l = std::max(1, L.collen[s]);
-        int lk = 0;
-        while (lk < 6 && (l + (1 << lk) - 1) >> lk > kRowsMax) ++lk;
-        int k = 1 << lk;
-        int ns = std::min(64 >> lk, s1 - s);
-        int rows = (l + k - 1) / k;
-        L.chunk_slot0.push_back(s);
+      int s2 = group_starts[gi], s1 = group_starts[gi + 1];
+      int tt = group_tile[gi], cl = group_class[gi];
+      int* tc = &L.tile_chunks[((size_t)c * T + tt) * 3];
+      int first_chunk = (int)L.chunk_slot0.size();
+      if (cl == 1) tc[0] = first_chunk;          // boundary group comes first
+      else { if (tc[0] < 0) tc[0] = first_chunk; tc[1] = first_chunk; }
+      while (s2 < s1) {
+        // take a Morton-contiguous run of slots whose lane groups fit 64 lanes
+        int e3 = s2, lanes = 0;
+        while (e3 < s1) {
+          int l = std::max(1, L.collen[e3]);
+          int lk = 0;
+          while (lk < 6 && (l + (1 << lk) - 1) >> lk > kRowsMax) ++lk;
+          if (lanes + (1 << lk) > 64) break;
+          lanes += 1 << lk;
+          ++e3;
+        }
+        // inside the chunk: groups by descending size => aligned offsets
+        std::vector<int> idx(e3 - s2);
+        std::iota(idx.begin(), idx.end(), s2);
+        auto lk_of = [&](int sl) {
+          int l = std::max(1, L.collen[sl]), lk = 0;
+          while (lk < 6 && (l + (1 << lk) - 1) >> lk > kRowsMax) ++lk;
+          return lk;
+        };
+        std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) { return lk_of(x) > lk_of(y); });
+        int rows = 1, maxlk = 0, o = 0;
+        const size_t lt0 = L.lane_tab.size();
+        L.lane_tab.resize(lt0 + 64, 0);
+        for (int sl : idx) {
+          int lk = lk_of(sl), k = 1 << lk;
+          int l = std::max(1, L.collen[sl]);
+          rows = std::max(rows, (l + k - 1) / k);
+          maxlk = std::max(maxlk, lk);
+          for (int u = 0; u < k; ++u) L.lane_tab[lt0 + o + u] = (sl + 1) | (lk << 28);
+          o += k;
+        }
+        // fixed stride: every chunk spans kRowsMax rows, so an entry's address
+        // depends only on the chunk index (no metadata round trip)
+        L.chunk_slot0.push_back(s2);
         L.chunk_len.push_back(rows);
-        L.chunk_nslot.push_back(ns);
-        L.chunk_lk.push_back(lk);
+        L.chunk_nslot.push_back(e3 - s2);
+        L.chunk_lk.push_back(maxlk);
         L.chunk_off.push_back(off);
-        off += (long long)rows * 64;
-        s += ns;
+        off += (long long)kRowsMax * 64;
+        s2 = e3;
       }
+      int end_chunk = (int)L.chunk_slot0.size();
+      if (cl == 1) { tc[1] = end_chunk; tc[2] = end_chunk; }
+      else tc[2] = end_chunk;
       ++gi;
     }
     L.color_chunk_ptr[c + 1] = (int)L.chunk_slot0.size();
+    // tiles with no slot of this colour: empty ranges at the colour's end
+    for (int tt = 0; tt < T; ++tt) {
+      int* tc = &L.tile_chunks[((size_t)c * T + tt) * 3];
+      if (tc[0] < 0) tc[0] = tc[1] = tc[2] = L.color_chunk_ptr[c + 1];
+      if (tc[1] < 0) tc[1] = tc[2];
+      if (tc[2] < 0) tc[2] = tc[1];
+    }
   }
   L.nchunks = (int)L.chunk_slot0.size();
   L.chunk_off.push_back(off);
@@ -432,12 +522,14 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
   L.ent_rowpos.assign(off, 0);
   L.ent_src.assign(off, -1);
   for (int ch = 0; ch < L.nchunks; ++ch) {
-    const int lk = L.chunk_lk[ch], k = 1 << lk;
-    for (int t = 0; t < L.chunk_nslot[ch]; ++t) {
-      int s = L.chunk_slot0[ch] + t;
-      int i = L.slot_loc[s];
+    for (int lane = 0; lane < 64; ++lane) {
+      const int v = L.lane_tab[(size_t)ch * 64 + lane];
+      if (v == 0) continue;
+      const int sl = (v & ((1 << 28) - 1)) - 1, lk = v >> 28, k = 1 << lk;
+      if ((lane & (k - 1)) != 0) continue;  // first lane of the slot's group
+      const int i = L.slot_loc[sl];
       for (long long p = cptr[i], j = 0; p < cptr[i + 1]; ++p, ++j) {
-        long long e = L.chunk_off[ch] + (j >> lk) * 64 + t * k + (j & (k - 1));
+        long long e = L.chunk_off[ch] + (j >> lk) * 64 + lane + (j & (k - 1));
         L.ent_rowpos[e] = L.rpos[crow[p]];
         L.ent_src[e] = csrc[p];
       }

@@ -24,17 +24,21 @@ int greedy_coloring(const int* nn_rowmajor, int n, int b, std::vector<int>& colo
 // bounding box of the first min(d,3) coordinates.
 void morton_keys(const double* locs_colmajor, int n, int d, std::vector<uint64_t>& keys);
 
-// Device layout of the chromatic sweep ("sliced-ELL by colour").
-//  - slots: locations re-indexed colour-major (colour 1 first), spatially
-//    (Morton) sorted inside a colour;
-//  - r positions: Morton rank of each Vecchia row;
-//  - chunks: one wavefront over 64/k consecutive slots of one colour, k =
-//    lanes per slot (power of two) chosen so that no chunk has more than
-//    kRowsMax rows (long columns of coarse max-min points are split over lanes);
-//  - entries: entry j of the t-th slot of a chunk stored at
-//    chunk_off[ch] + (j / k) * 64 + t * k + (j % k).
-constexpr int kRowsMax = 16;
-constexpr int kSlotGroup = 512;  // spatial group of same-colour slots (see build_sweep_layout)
+// Device layout of the chromatic sweep ("sliced ELL with per-slot lane groups").
+//  - slots: locations re-indexed colour-major; inside a colour grouped by
+//    spatial tile (a Morton range) and boundary/interior class, Morton order
+//    inside a group;
+//  - r / field / Linv rows: Morton rank of the location (rpos);
+//  - chunks: one wavefront over a Morton-contiguous run of slots of one
+//    group; slot i gets k_i = 2^lk_i lanes (aligned sub-group, k_i lanes
+//    cover ceil(len_i / kRowsMax) <= k_i), so no lane holds more than
+//    kRowsMax entries and the chunk stays spatially compact (its r gathers and
+//    scatters hit a few Morton-contiguous lines);
+//  - lane_tab[ch*64 + lane] = (slot + 1) | lk << 28 (0: idle lane);
+//  - entry j of slot i lives at ch * kRowsMax * 64 + (j / k_i) * 64 + o_i + j % k_i
+//    (o_i = first lane of the slot's group; fixed chunk stride).
+constexpr int kRowsMax = 16;  // entries per lane of a sweep chunk (== kSweepRows)
+
 struct SweepLayout {
   int n = 0, b = 0, K = 0, nchunks = 0;
   long long nnz = 0, n_entries = 0;
@@ -47,15 +51,24 @@ struct SweepLayout {
   std::vector<int> collen;           // n (slot order)
   std::vector<int> chunk_slot0;      // nchunks
   std::vector<int> chunk_len;        // nchunks: rows of the chunk
-  std::vector<int> chunk_nslot;      // nchunks: slots in the chunk (<= 64/k)
-  std::vector<int> chunk_lk;         // nchunks: log2(k)
+  std::vector<int> chunk_nslot;      // nchunks: slots in the chunk
+  std::vector<int> chunk_lk;         // nchunks: log2(max k over the chunk's slots)
+  std::vector<int> lane_tab;         // nchunks x 64
   std::vector<long long> chunk_off;  // nchunks
+  // spatial tiles for the persistent sweep: tile(loc) = rpos[loc]*T/n
+  int n_tiles = 1;
+  std::vector<int> tile_chunks;      // (K*T) x 3: chunk range [a, m) boundary, [m, e) interior of (colour, tile)
+  std::vector<int> nbr_ptr;          // T+1: CSR of neighbour tiles (moral-graph edges across tiles)
+  std::vector<int> nbr_idx;
+  long long n_boundary = 0;          // slots with a moral neighbour in another tile
   std::vector<int> ent_rowpos;       // n_entries (padding: 0)
   std::vector<int> ent_src;          // n_entries (device Linv index rpos[k]*b+j; padding: -1)
 };
 
+// n_tiles: spatial tiles (Morton ranges) for the persistent sweep (>= 1).
 bool build_sweep_layout(const int* nn_rowmajor, int n, int b, const int* colors,
-                        const double* locs_colmajor, int d, SweepLayout& L, std::string& err);
+                        const double* locs_colmajor, int d, int n_tiles, SweepLayout& L,
+                        std::string& err);
 
 // Level sets of the Vecchia DAG for the sparse triangular solve:
 // level(i) = 1 + max level(NN(i)), level 0 rows have no neighbours.

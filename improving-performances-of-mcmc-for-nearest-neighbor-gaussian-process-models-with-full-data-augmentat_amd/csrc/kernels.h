@@ -23,8 +23,8 @@ constexpr int kSweepRows = 16;  // == kRowsMax of the layout planner
 
 // one wavefront's chunk of the sweep layout, loaded with one 16-byte scalar load
 struct __attribute__((aligned(16))) ChunkMeta {
-  int slot0;       // first slot
-  int packed;      // rows | nslot << 8 | lk << 16
+  int slot0;       // first slot (a valid slot of the chunk)
+  int packed;      // rows | min(nslot,255) << 8 | max_lk << 16
   long long off;   // first entry
 };
 // per-slot constants of the sweep, one 32-byte record per slot
@@ -39,6 +39,7 @@ struct __attribute__((aligned(32))) SlotData {
 
 struct SweepDev {  // device pointers of the sliced-ELL layout
   const ChunkMeta* meta;
+  const int* lane_tab;      // nchunks x 64: (slot + 1) | lk << 28, 0 = idle
   SlotData* slots;
   const double* ent_val;
   const int* ent_rowpos;
@@ -81,6 +82,12 @@ hipError_t launch_slots_to_field(hipStream_t st, int n, const int* slot_dpos, co
 hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, int chunk_begin, int nchunks_color,
                               const SweepScalars* sc, int sweep_local, const double* z, int n);
 
+// all colours of n_sweeps sweeps in one persistent launch (grid = T tiles,
+// T <= #CUs); progress[T] must be zero and *err zero before the launch.
+hipError_t launch_sweep_persistent(hipStream_t st, const SweepDev& L, const int* tile_chunks, int T, int K,
+                                   int n_sweeps, const int* nbr_ptr, const int* nbr_idx, int* progress,
+                                   int* err, const SweepScalars* sc, const double* z, int n);
+
 // obs reductions: mode 0 -> partial[0] += (y - f[loc] - mu + beta0)^2
 //                 mode 1 -> partial[0] += ((y-b)^2 - (y-a)^2) / (2 sd^2),
 //                           a = fnew[loc]+mu-beta0, b = f[loc]+mu-beta0
@@ -92,6 +99,9 @@ hipError_t launch_tri_level(hipStream_t st, const int* rows, int nrows, const do
                             const int* nn, int b, const double* u, double* x);
 hipError_t launch_axpby_shift(hipStream_t st, int n, const double* x, double scale, double shift,
                               double* y);
+
+// x[0..n) = v (a kernel node, replayed with the graph)
+hipError_t launch_fill_int(hipStream_t st, int* x, int n, int v);
 
 // busy-wait on the device for `seconds` (bounded; measurement helper)
 hipError_t launch_spin(hipStream_t st, double seconds);

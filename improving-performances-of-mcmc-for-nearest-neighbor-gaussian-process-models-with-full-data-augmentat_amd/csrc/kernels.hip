@@ -472,33 +472,37 @@ hipError_t launch_reduce4(hipStream_t st, const double* partials, int nblocks, d
 }
 
 // ------------------------------------------------------------------ A5
-// lane -> (slot, sub-lane) of a chunk: k = 2^lk lanes per slot.  The chunk
-// index is wave-uniform (readfirstlane) so its metadata is a scalar load.
+// lane -> (slot, sub-lane) of a chunk.  Slot groups are aligned power-of-two
+// lane ranges of size k (per slot).  Chunks have a fixed stride of
+// kSweepRows x 64 entries, so the entry loads depend only on the chunk index
+// and issue in the same round trip as the lane-table load.
 struct ChunkLane {
-  int lk, k, t, u, s, rows;
+  int lk, k, u, s;
   bool valid;
   long long base;
 };
 __device__ __forceinline__ ChunkLane chunk_lane(const SweepDev& L, int ch, int lane) {
   ch = __builtin_amdgcn_readfirstlane(ch);
-  const ChunkMeta m = L.meta[ch];
+  const int v = L.lane_tab[(size_t)ch * 64 + lane];
   ChunkLane c;
-  c.rows = m.packed & 0xFF;
-  const int nslot = (m.packed >> 8) & 0xFF;
-  c.lk = (m.packed >> 16) & 0xFF;
+  c.valid = v != 0;
+  c.lk = c.valid ? (v >> 28) : 0;
   c.k = 1 << c.lk;
-  c.t = lane >> c.lk;
   c.u = lane & (c.k - 1);
-  c.valid = c.t < nslot;
-  c.s = m.slot0 + (c.valid ? c.t : 0);
-  c.base = m.off + lane;
+  c.s = c.valid ? (v & 0x0FFFFFFF) - 1 : 0;
+  c.base = (long long)ch * (kSweepRows * 64) + lane;
   return c;
 }
 
-// sum over the k lanes of a slot; xor butterfly => bitwise-identical result
-// in every lane of the group (IEEE addition is commutative)
+// sum over the k lanes of a slot (k varies per lane group, groups aligned);
+// xor butterfly => bitwise-identical result in every lane of a group (IEEE
+// addition is commutative)
 __device__ __forceinline__ double group_sum(double v, int k) {
-  for (int off = 1; off < k; off <<= 1) v += __shfl_xor(v, off, 64);
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const double o = __shfl_xor(v, off, 64);
+    if (off < k) v += o;
+  }
   return v;
 }
 
@@ -510,13 +514,12 @@ __global__ __launch_bounds__(256) void sell_refresh_kernel(SweepDev L, int nchun
   const int ch = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (ch >= nchunks) return;
   const ChunkLane c = chunk_lane(L, ch, threadIdx.x & 63);
-  const int len = c.valid ? L.slots[c.s].collen : 0;
-  // all loads first (clamped rows, unconditional), then the stores: no
-  // per-row round trip (padding entries have src -1 -> read linv[0], unused)
+  // entry loads depend only on the chunk index (padding: src -1 -> linv[0], unused)
   int src[kSweepRows];
   double v[kSweepRows];
 #pragma unroll
-  for (int j = 0; j < kSweepRows; ++j) src[j] = ent_src[c.base + (long long)min(j, c.rows - 1) * 64];
+  for (int j = 0; j < kSweepRows; ++j) src[j] = ent_src[c.base + (long long)j * 64];
+  const int len = c.valid ? L.slots[c.s].collen : 0;
 #pragma unroll
   for (int j = 0; j < kSweepRows; ++j) v[j] = linv[max(src[j], 0)];
   double D = 0.0;
@@ -601,35 +604,55 @@ hipError_t launch_slots_to_field(hipStream_t st, int n, const int* slot_dpos, co
 //   r_k += B[k,i] (w_i' - w_i)
 // Blocks are remapped so that consecutive (spatially adjacent) chunks run on
 // the same XCD and share its L2 for the r gathers.
-template <bool INJECT>
-__global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, int chunk_begin, int nchunks_color,
-                                                          const SweepScalars* __restrict__ scal,
-                                                          int sweep_local, const double* __restrict__ z,
-                                                          int n) {
-  const int nb = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q = nb >> 3, rm = nb & 7;
-  const int lb = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + (bid >> 3);
-  const int lch = lb * 4 + (threadIdx.x >> 6);
-  if (lch >= nchunks_color) return;
-  const ChunkLane c = chunk_lane(L, chunk_begin + lch, threadIdx.x & 63);
+// r accessor: plain (per-colour kernels: the launch boundary orders colours)
+// or sc1 write-through relaxed agent-scope atomics (persistent kernel: r is
+// handed between workgroups inside one launch, MI355X_MICROARCH.md "Valid
+// forms", first table row: every store and every load of r is sc1).
+template <bool SC1>
+__device__ __forceinline__ double r_load(const double* r, int p) {
+  if (SC1) {
+    unsigned long long v = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(r) + p,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __longlong_as_double((long long)v);
+  }
+  return r[p];
+}
+template <bool SC1>
+__device__ __forceinline__ void r_store(double* r, int p, double v) {
+  if (SC1)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(r) + p,
+                       (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  else
+    r[p] = v;
+}
+
+// one chunk of one colour (the body shared by both sweep kernels)
+template <bool INJECT, bool SC1>
+__device__ __forceinline__ void sweep_chunk(const SweepDev& L, int ch, int lane,
+                                            const SweepScalars* __restrict__ scal, int sweep_local,
+                                            const double* __restrict__ z, int n) {
+  const ChunkLane c = chunk_lane(L, ch, lane);
   double* r = L.r;  // gathered then scattered: no __restrict__
-  const SlotData sd = L.slots[c.s];
-  const double w = L.w_slot[c.s];
-  const int len = c.valid ? sd.collen : 0;
+  // round trip 1: entries (address from the chunk index only) + lane table;
+  // round trip 2: slot record, w and the r gathers
   double v[kSweepRows], rv[kSweepRows];
   int p[kSweepRows];
 #pragma unroll
   for (int j = 0; j < kSweepRows; ++j) {
-    const long long e = c.base + (long long)min(j, c.rows - 1) * 64;
+    const long long e = c.base + (long long)j * 64;
     v[j] = L.ent_val[e];
     p[j] = L.ent_rowpos[e];
   }
+  const SlotData sd = L.slots[c.s];
+  const double w = L.w_slot[c.s];
+  const int len = c.valid ? sd.collen : 0;
   const double inv_s2 = scal->inv_s2, inv_t2 = scal->inv_t2;
   double zz;
   if (INJECT) zz = z[(size_t)sweep_local * n + sd.loc];
   else zz = normal_at(scal->seed, scal->counter_base + (uint64_t)sweep_local, (uint32_t)sd.loc);
 #pragma unroll
-  for (int j = 0; j < kSweepRows; ++j) rv[j] = r[p[j]];
+  for (int j = 0; j < kSweepRows; ++j) rv[j] = r_load<SC1>(r, p[j]);
   double acc = 0.0;
 #pragma unroll
   for (int j = 0; j < kSweepRows; ++j) acc += (j * c.k + c.u < len) ? v[j] * rv[j] : 0.0;
@@ -642,7 +665,102 @@ __global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, int chunk_
   if (c.u == 0) L.w_slot[c.s] = wn;
 #pragma unroll
   for (int j = 0; j < kSweepRows; ++j)
-    if (j * c.k + c.u < len) r[p[j]] = rv[j] + v[j] * dw;
+    if (j * c.k + c.u < len) r_store<SC1>(r, p[j], rv[j] + v[j] * dw);
+}
+
+template <bool INJECT>
+__global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, int chunk_begin, int nchunks_color,
+                                                          const SweepScalars* __restrict__ scal,
+                                                          int sweep_local, const double* __restrict__ z,
+                                                          int n) {
+  const int nb = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nb >> 3, rm = nb & 7;
+  const int lb = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + (bid >> 3);
+  const int lch = lb * 4 + (threadIdx.x >> 6);
+  if (lch >= nchunks_color) return;
+  sweep_chunk<INJECT, false>(L, chunk_begin + lch, threadIdx.x & 63, scal, sweep_local, z, n);
+}
+
+// ------------------------------------------------------------------ A1, persistent
+// All colours of n_sweeps sweeps in ONE launch.  One workgroup (4 waves) per
+// spatial tile (a Morton range of locations), one workgroup per CU (the
+// dynamic LDS request admits only one).  Step p = s*K + c + 1 of tile t:
+//   1. wave 0 polls progress[u] >= p-1 for every neighbour tile u (tiles with a
+//      moral-graph edge to t) -- relaxed sc1 loads, bounded spin;
+//   2. barrier; the tile's BOUNDARY chunks of colour c (slots with a moral
+//      neighbour in another tile) are updated, r accessed with sc1 loads/stores;
+//   3. every wave drains its stores (vmcnt(0)); barrier; one lane publishes
+//      progress[t] = p (relaxed sc1 store);
+//   4. the tile's INTERIOR chunks of colour c (rows touched only by this tile)
+//      are updated while the neighbours proceed.
+// Exactly the reference's colour order: a boundary slot of colour c reads
+// rows whose other members belong to neighbour tiles' boundary slots, which
+// have all finished colours < c of this sweep (and not started colours > c:
+// those wait for this tile).  Progress is monotone and the minimum-progress
+// tile never waits, so the protocol cannot deadlock once all workgroups are
+// resident (grid <= CUs).  A spin that exceeds ~4 s sets *err and gives up.
+template <bool INJECT>
+__global__ __launch_bounds__(256) void sweep_persistent_kernel(SweepDev L, const int* __restrict__ tile_chunks,
+                                                               int T, int K, int n_sweeps,
+                                                               const int* __restrict__ nbr_ptr,
+                                                               const int* __restrict__ nbr_idx,
+                                                               int* __restrict__ progress,
+                                                               int* __restrict__ err,
+                                                               const SweepScalars* __restrict__ scal,
+                                                               const double* __restrict__ z, int n) {
+  // XCD-aware tile choice: blocks b, b+8, ... share an XCD, so give them
+  // Morton-consecutive tiles (most hand-offs then stay inside one XCD's L2)
+  const int nb = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nb >> 3, rm = nb & 7;
+  const int t = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + (bid >> 3);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int nb0 = nbr_ptr[t], nb1 = nbr_ptr[t + 1];
+  __shared__ int s_fail;
+  if (threadIdx.x == 0) s_fail = 0;
+  __syncthreads();
+  for (int s = 0; s < n_sweeps; ++s) {
+    for (int c = 0; c < K; ++c) {
+      const int pstep = s * K + c + 1;
+      const int* tc = tile_chunks + ((size_t)c * T + t) * 3;
+      const int a = tc[0], m = tc[1], e = tc[2];
+      if (wave == 0 && pstep > 1 && nb1 > nb0) {
+        const unsigned long long t0 = wall_clock64();
+        for (;;) {
+          bool ok = true;
+          for (int i = nb0 + lane; i < nb1; i += 64)
+            ok &= __hip_atomic_load(progress + nbr_idx[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= pstep - 1;
+          if (__all(ok)) break;
+          if (wall_clock64() - t0 > 400000000ull) {  // ~4 s at 100 MHz
+            if (lane == 0) { atomicMax(err, 1 + t); s_fail = 1; }
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __syncthreads();
+      if (s_fail) return;
+      for (int ch = a + wave; ch < m; ch += 4) sweep_chunk<INJECT, true>(L, ch, lane, scal, s, z, n);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_store(progress + t, pstep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int ch = m + wave; ch < e; ch += 4) sweep_chunk<INJECT, true>(L, ch, lane, scal, s, z, n);
+    }
+  }
+}
+
+hipError_t launch_sweep_persistent(hipStream_t st, const SweepDev& L, const int* tile_chunks, int T, int K,
+                                   int n_sweeps, const int* nbr_ptr, const int* nbr_idx, int* progress,
+                                   int* err, const SweepScalars* sc, const double* z, int n) {
+  // 96 KiB of dynamic LDS: only one workgroup fits per CU (160 KiB)
+  const size_t lds = 96 * 1024;
+  if (z)
+    hipLaunchKernelGGL((sweep_persistent_kernel<true>), dim3(T), dim3(kBlock), lds, st, L, tile_chunks, T, K,
+                       n_sweeps, nbr_ptr, nbr_idx, progress, err, sc, z, n);
+  else
+    hipLaunchKernelGGL((sweep_persistent_kernel<false>), dim3(T), dim3(kBlock), lds, st, L, tile_chunks, T, K,
+                       n_sweeps, nbr_ptr, nbr_idx, progress, err, sc, z, n);
+  return hipGetLastError();
 }
 
 hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, int chunk_begin, int nchunks_color,
@@ -725,6 +843,15 @@ hipError_t launch_axpby_shift(hipStream_t st, int n, const double* x, double sca
                               double* y) {
   int g = (n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(axpby_shift_kernel, dim3(g), dim3(kBlock), 0, st, n, x, scale, shift, y);
+  return hipGetLastError();
+}
+
+__global__ void fill_int_kernel(int* __restrict__ x, int n, int v) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) x[i] = v;
+}
+
+hipError_t launch_fill_int(hipStream_t st, int* x, int n, int v) {
+  hipLaunchKernelGGL(fill_int_kernel, dim3(1), dim3(256), 0, st, x, n, v);
   return hipGetLastError();
 }
 

@@ -83,6 +83,9 @@ typedef struct {
   long long n_entries; /* sliced-ELL entries incl. padding */
   int max_collen;  /* longest column of B */
   int device;      /* HIP device ordinal */
+  int n_tiles;     /* spatial tiles of the persistent sweep */
+  long long n_boundary; /* locations with a moral neighbour in another tile */
+  int sweep_mode;  /* 1 persistent dataflow kernel, 0 one kernel per colour */
 } nngp_info;
 
 /* ---------- library ---------- */

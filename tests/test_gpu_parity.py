@@ -310,3 +310,31 @@ def test_size_independent_properties_large(P, O):
                   np.zeros(n), lm, 0.0, 0.0, 0.0, z)
     np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-10)
     assert info["nnz"] == n * (m + 1) - m * (m + 1) // 2
+
+
+@pytest.mark.parametrize("n,m", [(3000, 10), (60000, 15)])
+def test_persistent_sweep_bitwise_equals_per_colour_launches(P, O, n, m, monkeypatch):
+    """The persistent dataflow kernel (tiles + neighbour progress counters)
+    must read exactly the values the colour-by-colour launches read: results
+    are bitwise identical, and both match the oracle."""
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=n)
+    cp = COVS["matern15_isotropic"]
+    field = np.random.default_rng(5).normal(size=n)
+    out = {}
+    for mode in ["launch", "persistent"]:
+        monkeypatch.setenv("NNGP_SWEEP", mode)
+        with _ctx(P, locs, NN, col, lm, y) as ctx:
+            info = ctx.info
+            assert info["sweep_mode"] == (1 if mode == "persistent" else 0)
+            ctx.factor(0, "matern15_isotropic", cp)
+            ctx.set_field(field)
+            ctx.set_mu(None, 0.2)
+            ctx.sweep(4, 0.2, 0.1, -0.3, 99, 7)
+            out[mode] = ctx.get_field()
+            Lo = ctx.get_linv(0)
+    assert info["n_tiles"] == max(1, min(256, n // 1024))
+    np.testing.assert_array_equal(out["persistent"], out["launch"])
+    z = O.sweep_normals(99, 7, 4, n)
+    ref = O.sweep("local", field, Lo, NN, col, O.precision_diag(Lo, NN), np.ones(n, np.int32), y,
+                  np.full(n, 0.2), lm, 0.2, 0.1, -0.3, z)
+    np.testing.assert_allclose(out["persistent"], ref, rtol=1e-7, atol=1e-8)
