@@ -1,17 +1,22 @@
 #!/usr/bin/env python
 """Headline benchmark: full-field chromatic Gibbs sweeps/sec at n=1e6, m=15
-(synthetic 2-D Matern-3/2 field, fp64, one chain per GPU), with the sweep
-kernel's achieved bandwidth against the MI355X HBM roofline and the CPU
-oracle's reference-faithful sweep timed on the host beside it.
+(synthetic 2-D Matern-3/2 field, fp64), with the sweep kernel's achieved
+bandwidth against the MI355X HBM roofline and the CPU oracle's
+reference-faithful sweep timed on the host beside it.
 
 Contract: python bench.py --gpus N --steps K --warmup W  (N>1 under
 torch.distributed.run; one rank per GPU).  A step = one chromatic sweep (all K
-colours, all n latents, update_Gaussian.R:257-275 with n_chromatic = 1).  The
-timed region runs the reference's per-iteration call shape: nngp_sweep with
-n_chromatic = 10 sweeps per call (r = B w refresh + 10 sweeps).
-Multi-GPU: every rank runs an independent chain on its own synthetic field
-(the reference's chain-level parallelism, mclapply -> ranks): weak scaling,
-no data-path collective (DESIGN.md "Multi-GPU").
+colours, all n latents, update_Gaussian.R:257-275 with n_chromatic = 1) of
+each of the --chains chains of the GPU (default 3 = the reference's default
+n_chains, initialize.R:9, which it runs concurrently with mclapply).  The
+chains of a GPU share one context and sweep in the same kernels
+(nngp_sweep_chains).  value = chain-sweeps/s over all GPUs.  The timed region
+runs the reference's per-iteration call shape: n_chromatic = 10 sweeps per
+call (r = B w refresh + 10 sweeps).  A single-chain context is timed too
+("single_chain" in config).
+Multi-GPU: every rank runs its own chains on its own synthetic field (the
+reference's chain-level parallelism, mclapply -> ranks): weak scaling, no
+data-path collective (DESIGN.md "Multi-GPU").
 """
 from __future__ import annotations
 
@@ -35,7 +40,7 @@ def log(msg, rank=0):
         print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def make_workload(P, n, m, covfun, cp, seed, device):
+def make_workload(P, n, m, covfun, cp, seed, device, chains):
     rng = np.random.default_rng(seed)
     t = time.time()
     locs = rng.uniform(size=(n, 2))
@@ -51,12 +56,21 @@ def make_workload(P, n, m, covfun, cp, seed, device):
     w = ctx.tri_solve(0, rng.normal(size=n))
     y = beta0 + w + np.sqrt(tau2) * rng.normal(size=n)
     ctx.close()
-    ctx = P.ChainContext(locs, NN, col, lm, y, device=device)
-    ctx.factor(0, covfun, cp)
-    ctx.set_field(beta0 + w + 0.1 * rng.normal(size=n))
-    ctx.set_mu(None, beta0)
-    return ctx, dict(locs=locs, NN=NN, col=col, lm=lm, y=y, beta0=beta0, log_noise_variance=np.log(tau2),
-                     log_scale=0.0, t_graph=t_graph)
+    wl = dict(locs=locs, NN=NN, col=col, lm=lm, y=y, beta0=beta0, log_noise_variance=np.log(tau2),
+              log_scale=0.0, t_graph=t_graph, w=w)
+    return wl
+
+
+def open_context(P, wl, covfun, cp, device, chains, seed):
+    rng = np.random.default_rng(seed)
+    ctx = P.ChainContext(wl["locs"], wl["NN"], wl["col"], wl["lm"], wl["y"], device=device, n_chains=chains)
+    for k in range(chains):
+        ctx.select(k)
+        ctx.factor(0, covfun, cp)
+        ctx.set_field(wl["beta0"] + wl["w"] + 0.1 * rng.normal(size=len(wl["y"])))
+        ctx.set_mu(None, wl["beta0"])
+    ctx.select(0)
+    return ctx
 
 
 def cpu_baseline(P, wl, covfun, cp, budget_s):
@@ -102,6 +116,8 @@ def main():
     ap.add_argument("--covfun", default="matern15_isotropic")
     ap.add_argument("--range", type=float, default=0.05)
     ap.add_argument("--n-chromatic", type=int, default=10)
+    ap.add_argument("--chains", type=int, default=3)
+    ap.add_argument("--no-single-chain", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -122,49 +138,70 @@ def main():
     P = _pkgload.load()
     covfun = args.covfun
     cp = [1.0, args.range, 0.0]
-    log(f"setup n={args.n} m={args.m} {covfun} world={world}", rank)
-    ctx, wl = make_workload(P, args.n, args.m, covfun, cp, seed=1000 + rank, device=local_rank)
-    wl["field0"] = ctx.get_field()
-    info = ctx.info
-    log(f"graph prep {wl['t_graph']:.1f}s colours={info['n_colors']} nnz={info['nnz']} "
-        f"entries={info['n_entries']} max_collen={info['max_collen']}", rank)
+    log(f"setup n={args.n} m={args.m} {covfun} chains={args.chains} world={world}", rank)
+    wl = make_workload(P, args.n, args.m, covfun, cp, seed=1000 + rank, device=local_rank, chains=args.chains)
+    C = args.chains
     nc = args.n_chromatic
     b0, ls, lnv = wl["beta0"], wl["log_scale"], wl["log_noise_variance"]
-    seed = 77 + rank
+    seeds = [77 + 10 * rank + k for k in range(C)]
 
-    def run_sweeps(k, base):
-        done = 0
-        while done < k:
-            s = min(nc, k - done)
-            ctx.sweep(s, b0, ls, lnv, seed, base + done)
-            done += s
-        return base + done
+    def timed(ctx, steps, warmup):
+        """warmup + steps sweeps of every chain of ctx in calls of n_chromatic"""
+        k = ctx.n_chains
 
-    ctr = run_sweeps(args.warmup, 0)
-    torch.cuda.synchronize(local_rank) if torch.cuda.is_available() else None
-    if dist:
-        dist.barrier()
-    t0 = time.perf_counter()
-    ctr = run_sweeps(args.steps, ctr)
-    if torch.cuda.is_available():
-        torch.cuda.synchronize(local_rank)
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        def run(nsw, base):
+            done = 0
+            while done < nsw:
+                s = min(nc, nsw - done)
+                ctx.sweep_chains(s, [b0] * k, [ls] * k, [lnv] * k, seeds[:k], [base + done] * k)
+                done += s
+            return base + done
+
+        ctr = run(warmup, 0)
+        if torch.cuda.is_available():
+            torch.cuda.synchronize(local_rank)
+        if dist:
+            dist.barrier()
+        t0 = time.perf_counter()
+        ctr = run(steps, ctr)
+        if torch.cuda.is_available():
+            torch.cuda.synchronize(local_rank)
+        if dist:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([el], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, ctr
+
+    single = None
+    if not args.no_single_chain:
+        ctx1 = open_context(P, wl, covfun, cp, local_rank, 1, seed=5 + rank)
+        el1, _ = timed(ctx1, args.steps, args.warmup)
+        single = {"value": args.steps * world / el1, "unit": "sweeps/s",
+                  "ms_per_step": el1 * 1e3 / args.steps,
+                  "n_entries": ctx1.info["n_entries"]}
+        ctx1.close()
+    ctx = open_context(P, wl, covfun, cp, local_rank, C, seed=7 + rank)
+    info = ctx.info
+    wl["field0"] = ctx.get_field()
+    log(f"graph prep {wl['t_graph']:.1f}s colours={info['n_colors']} nnz={info['nnz']} "
+        f"entries={info['n_entries']} chunks={info['n_chunks']} lanes/chain={info['lanes_per_chain']} "
+        f"max_collen={info['max_collen']}", rank)
+    elapsed, ctr = timed(ctx, args.steps, args.warmup)
 
     # per-kernel timing (HIP events around every colour launch, on the
     # context's own stream) -> sweep kernel time per sweep
     n, nnz = args.n, info["nnz"]
-    bytes_sweep = 12 * nnz + 40 * n  # SURVEY §8(d) algorithmic bytes per sweep
+    # SURVEY §8(d) algorithmic bytes: 12 nnz + 40 n per chain-sweep, the 4-byte
+    # row index of an entry shared by the chains of a launch
+    bytes_sweep = C * (8 * nnz + 40 * n) + 4 * nnz
     roofline = None
     if not args.no_kernel_timing:
         ksw = max(4, min(20, args.steps))
         try:
-            ms_tot, kms = ctx.sweep_timed(ksw, b0, ls, lnv, seed, ctr, per_kernel=True)
+            ms_tot, kms = ctx.sweep_timed(ksw, [b0] * C, [ls] * C, [lnv] * C, seeds, [ctr] * C, per_kernel=True)
         except Exception as e:  # report, do not hide the throughput line
             log(f"per-kernel timing failed: {e}", rank)
             kms = float("nan")
@@ -175,22 +212,25 @@ def main():
                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                     "kernel": "sweep_color_kernel", "kernel_avg_us": kms * 1e3 / launches,
                     "algorithmic_bytes_per_sweep": bytes_sweep,
+                    "algorithmic_bytes_per_launch": bytes_sweep / info["n_colors"],
                     "launches_per_sweep": info["n_colors"]}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline (oracle, 1 core)...", rank)
         cpu = cpu_baseline(P, wl, covfun, cp, args.cpu_budget)
     ctx.close()
-    total_sweeps = args.steps * world
-    value = total_sweeps / elapsed
+    value = args.steps * C * world / elapsed
     out = {"metric": "full-field Gibbs sweeps/sec at n=1e6, m=15; achieved HBM GB/s vs roofline",
            "value": value, "unit": "sweeps/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
            "data": "synthetic (U[0,1]^2 locations, exact max-min order, field drawn from the Vecchia prior)",
-           "config": {"workload": f"chromatic sweep n={n} m={args.m} {covfun} range={args.range}, one chain per GPU",
-                      "n": n, "m": args.m, "n_colors": info["n_colors"], "nnz": nnz,
-                      "n_chromatic_per_call": nc, "parallelism": f"chains x{world} (independent)"},
+           "config": {"workload": (f"chromatic sweep n={n} m={args.m} {covfun} range={args.range}, "
+                                   f"{C} chains per GPU swept together (value = chain-sweeps/s)"),
+                      "n": n, "m": args.m, "n_colors": info["n_colors"], "nnz": nnz, "chains_per_gpu": C,
+                      "n_entries": info["n_entries"], "n_chromatic_per_call": nc,
+                      "single_chain": single,
+                      "parallelism": f"chains {C} per GPU x {world} GPUs (independent)"},
            "roofline": roofline, "cpu_baseline": cpu}
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -27,9 +27,9 @@ COVFUNS = {
 ABI_SYMBOLS = (
     "nngp_abi_version", "nngp_status_string", "nngp_order_maxmin", "nngp_find_ordered_nn",
     "nngp_greedy_coloring", "nngp_ctx_create", "nngp_ctx_destroy", "nngp_ctx_last_error",
-    "nngp_ctx_info", "nngp_factor", "nngp_get_linv", "nngp_set_linv", "nngp_accept_factor",
+    "nngp_set_chain", "nngp_ctx_info", "nngp_factor", "nngp_get_linv", "nngp_set_linv", "nngp_accept_factor",
     "nngp_get_precision_diag", "nngp_set_field", "nngp_get_field", "nngp_set_mu",
-    "nngp_loglik", "nngp_sweep", "nngp_ancillary_propose", "nngp_field_response_ratio",
+    "nngp_loglik", "nngp_sweep", "nngp_sweep_chains", "nngp_ancillary_propose", "nngp_field_response_ratio",
     "nngp_accept_field", "nngp_beta0_stats", "nngp_sum_squared_residuals", "nngp_spmv",
     "nngp_tri_solve", "nngp_sweep_timed", "nngp_device_normals",
 )
@@ -45,7 +45,7 @@ class Info(C.Structure):
     _fields_ = [("n", C.c_int), ("b", C.c_int), ("d", C.c_int), ("n_obs", C.c_int),
                 ("n_colors", C.c_int), ("n_levels", C.c_int), ("nnz", C.c_longlong),
                 ("n_entries", C.c_longlong), ("max_collen", C.c_int), ("device", C.c_int),
-                ("n_tiles", C.c_int), ("n_boundary", C.c_longlong), ("sweep_mode", C.c_int)]
+                ("n_chains", C.c_int), ("lanes_per_chain", C.c_int), ("n_chunks", C.c_int)]
 
 
 _dp = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
@@ -66,7 +66,8 @@ def _load():
     L.nngp_find_ordered_nn.argtypes = [_dp, C.c_int, C.c_int, C.c_int, _ip]
     L.nngp_greedy_coloring.argtypes = [_ip, C.c_int, C.c_int, _ip, C.POINTER(C.c_int)]
     L.nngp_ctx_create.argtypes = [_dp, C.c_int, C.c_int, _ip, C.c_int, _ip, _ip, _dp, C.c_int,
-                                  C.c_int, C.POINTER(_vp)]
+                                  C.c_int, C.c_int, C.POINTER(_vp)]
+    L.nngp_set_chain.argtypes = [_vp, C.c_int]
     L.nngp_ctx_destroy.argtypes = [_vp]
     L.nngp_ctx_destroy.restype = None
     L.nngp_ctx_last_error.argtypes = [_vp]
@@ -90,8 +91,10 @@ def _load():
     L.nngp_sum_squared_residuals.argtypes = [_vp, C.c_double, C.POINTER(C.c_double)]
     L.nngp_spmv.argtypes = [_vp, C.c_int, _dp, C.c_int, _dp]
     L.nngp_tri_solve.argtypes = [_vp, C.c_int, _dp, _dp]
-    L.nngp_sweep_timed.argtypes = [_vp, C.c_int, C.c_double, C.c_double, C.c_double, C.c_uint64,
-                                   C.c_uint64, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    _up = np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS")
+    L.nngp_sweep_chains.argtypes = [_vp, C.c_int, _dp, _dp, _dp, _up, _up]
+    L.nngp_sweep_timed.argtypes = [_vp, C.c_int, _dp, _dp, _dp, _up, _up,
+                                   C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.nngp_device_normals.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_int, _dp]
     return L
 

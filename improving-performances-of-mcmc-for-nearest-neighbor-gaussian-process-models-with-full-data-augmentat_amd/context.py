@@ -1,6 +1,9 @@
-"""One device context per MCMC chain (replaces the per-chain ``mclapply``
-worker of Scripts/mcmc_nngp_update_Gaussian.R:25 -- HIP is not fork-safe, so
-chains are contexts, possibly on different devices, not forked processes).
+"""Device contexts of MCMC chains (replace the per-chain ``mclapply`` workers
+of Scripts/mcmc_nngp_update_Gaussian.R:25-26 -- HIP is not fork-safe, so
+chains live in device contexts, possibly on different devices, not in forked
+processes).  One context holds up to 4 chains over the same graph; their
+sweeps run in the same kernels (``sweep_chains``).  ``ChainView`` exposes
+one chain of a context with the single-chain interface.
 """
 from __future__ import annotations
 
@@ -11,11 +14,17 @@ import numpy as np
 from ._lib import COVFUNS, Info, check, colmajor, f64, i32, lib
 
 
-class ChainContext:
-    """Device-resident state of one chain: locations, NNarray, colouring,
-    observations, the current/proposal Vecchia factors, the latent field."""
+MAX_CHAINS_PER_CONTEXT = 4
 
-    def __init__(self, locs, NNarray, coloring, locs_match, observed_field, device: int = -1):
+
+class ChainContext:
+    """Device-resident state of 1..4 chains: locations, NNarray, colouring,
+    observations (shared); the current/proposal Vecchia factors, the latent
+    field and the mean (per chain).  Per-chain methods act on the selected
+    chain (``select``; chain 0 by default)."""
+
+    def __init__(self, locs, NNarray, coloring, locs_match, observed_field, device: int = -1,
+                 n_chains: int = 1):
         locs = np.asarray(locs, np.float64)
         if locs.ndim == 1:
             locs = locs[:, None]
@@ -24,11 +33,22 @@ class ChainContext:
         b = NNarray.shape[1]
         self.n, self.d, self.b = n, d, b
         self.n_obs = len(observed_field)
+        self.n_chains = int(n_chains)
         h = C.c_void_p()
         check(lib.nngp_ctx_create(colmajor(locs, np.float64), n, d, colmajor(NNarray, np.int32), b,
                                   i32(coloring), i32(locs_match), f64(observed_field), self.n_obs,
-                                  int(device), C.byref(h)))
+                                  self.n_chains, int(device), C.byref(h)))
         self._h = h
+        self._sel = 0
+
+    def select(self, chain: int) -> "ChainContext":
+        if chain != self._sel:
+            self._chk(lib.nngp_set_chain(self._h, int(chain)))
+            self._sel = int(chain)
+        return self
+
+    def view(self, chain: int) -> "ChainView":
+        return ChainView(self, chain)
 
     # ------------------------------------------------------------ lifetime
     def close(self) -> None:
@@ -110,13 +130,27 @@ class ChainContext:
                                  float(log_noise_variance), int(seed) & (2 ** 64 - 1),
                                  int(counter_base) & (2 ** 64 - 1), zp))
 
+    def sweep_chains(self, n_sweeps: int, beta0, log_scale, log_noise_variance, seed, counter_base) -> None:
+        """n_sweeps sweeps of every chain (per-chain argument sequences)."""
+        a = self._chain_args(beta0, log_scale, log_noise_variance, seed, counter_base)
+        self._chk(lib.nngp_sweep_chains(self._h, int(n_sweeps), *a))
+
+    def _chain_args(self, beta0, log_scale, log_noise_variance, seed, counter_base):
+        k = self.n_chains
+        f = [np.ascontiguousarray(np.broadcast_to(np.asarray(v, np.float64), (k,))) for v in
+             (beta0, log_scale, log_noise_variance)]
+        u = [np.ascontiguousarray(np.broadcast_to(np.asarray([int(x) & (2 ** 64 - 1) for x in np.atleast_1d(v)],
+                                                             np.uint64), (k,))) for v in (seed, counter_base)]
+        return (*f, *u)
+
     def sweep_timed(self, n_sweeps, beta0, log_scale, log_noise_variance, seed, counter_base,
                     per_kernel: bool = False):
+        """sweep_chains bracketed by HIP events -> (ms, summed per-colour kernel ms or None)."""
         ms = C.c_double()
         kms = C.c_double()
-        self._chk(lib.nngp_sweep_timed(self._h, int(n_sweeps), float(beta0), float(log_scale),
-                                       float(log_noise_variance), int(seed), int(counter_base),
-                                       C.byref(ms), C.byref(kms) if per_kernel else None))
+        a = self._chain_args(beta0, log_scale, log_noise_variance, seed, counter_base)
+        self._chk(lib.nngp_sweep_timed(self._h, int(n_sweeps), *a, C.byref(ms),
+                                       C.byref(kms) if per_kernel else None))
         return ms.value, (kms.value if per_kernel else None)
 
     def ancillary_propose(self, beta0: float, dlog_scale: float) -> None:
@@ -154,6 +188,53 @@ class ChainContext:
         out = np.zeros(self.n)
         self._chk(lib.nngp_tri_solve(self._h, which, f64(u), out))
         return out
+
+
+class ChainView:
+    """One chain of a ChainContext with the single-chain interface (every
+    method selects the chain first)."""
+
+    def __init__(self, ctx: ChainContext, chain: int):
+        self.ctx, self.chain = ctx, int(chain)
+        self.n, self.d, self.b, self.n_obs = ctx.n, ctx.d, ctx.b, ctx.n_obs
+
+    def __getattr__(self, name):
+        attr = getattr(self.ctx, name)
+        if not callable(attr) or name in ("close", "view", "sweep_chains", "sweep_timed"):
+            return attr
+
+        def bound(*a, **kw):
+            self.ctx.select(self.chain)
+            return attr(*a, **kw)
+        return bound
+
+    @property
+    def info(self) -> dict:
+        return self.ctx.info
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.ctx.close()
+
+
+def make_chain_views(locs, NNarray, coloring, locs_match, observed_field, n_chains: int, devices=None):
+    """Chains dealt round-robin over `devices`, then packed <= 4 per context:
+    returns one ChainView per chain (chain i -> views[i])."""
+    devices = list(devices) if devices else [-1]
+    per_dev = {}
+    for i in range(n_chains):
+        per_dev.setdefault(devices[i % len(devices)], []).append(i)
+    views = [None] * n_chains
+    for dev, chains in per_dev.items():
+        for g in range(0, len(chains), MAX_CHAINS_PER_CONTEXT):
+            group = chains[g:g + MAX_CHAINS_PER_CONTEXT]
+            ctx = ChainContext(locs, NNarray, coloring, locs_match, observed_field, device=dev,
+                               n_chains=len(group))
+            for k, i in enumerate(group):
+                views[i] = ctx.view(k)
+    return views
 
 
 def device_normals(seed: int, sweep: int, n: int, device: int = 0) -> np.ndarray:

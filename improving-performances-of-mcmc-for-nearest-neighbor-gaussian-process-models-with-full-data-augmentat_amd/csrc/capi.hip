@@ -1,5 +1,5 @@
 // C ABI (include/nngp.h) of the MI355X-native NNGP chromatic-Gibbs hot path.
-// One nngp_ctx per MCMC chain: device buffers, the sweep layout planned on the
+// One nngp_ctx per group of <= 4 MCMC chains: device buffers, the sweep layout planned on the
 // host (graph_prep.cpp), one HIP stream, and cached hipGraphs of the sweep.
 #include <hip/hip_runtime.h>
 
@@ -24,56 +24,63 @@ using namespace nngp;
 // Linv, field, r) is stored in Morton order ("dpos" = lay.rpos[loc]) so the
 // neighbour gathers of the factor build, the SpMV and the sweep hit nearby
 // lines; the host boundary converts to and from the Vecchia (location) order.
+//
+// A context holds C <= 4 chains over the same locations / NNarray / colouring
+// (the reference's n_chains, each with its own covariance parameters, factor,
+// field and mean).  Per-chain entry points act on the chain selected by
+// nngp_set_chain; nngp_sweep_chains sweeps every chain in the same kernels.
+struct ChainState {
+  double* linv_d[2] = {nullptr, nullptr};
+  double* field_d = nullptr;
+  double* field_prop_d = nullptr;
+  double* mu_d = nullptr;
+  bool have_factor[2] = {false, false};
+  bool have_field = false, have_mu = false, mu_is_const = true;
+  double mu_beta0 = 0.0;
+};
+
 struct nngp_ctx {
   int device = 0;
   hipStream_t st = nullptr;
   int n = 0, d = 0, b = 0, n_obs = 0, ds = 2;
+  int C = 1, cur = 0;
   std::string err;
   SweepLayout lay;
+  std::vector<ColorArgs> cargs;  // per colour
   std::vector<int> dpos;   // loc -> device row (== lay.rpos)
   std::vector<int> level_ptr, level_rows;
+  ChainState ch[kMaxChains];
   // device buffers
   double* locs_d = nullptr;  // n x d row-major
   double* sc_d = nullptr;    // n x ds scaled coordinates
   int* nn_d = nullptr;       // n x b row-major, 0-based, -1 = NA
-  double* linv_d[2] = {nullptr, nullptr};
+  const double** linv_cur_d = nullptr;  // C pointers: current factor of each chain
+  const double** linv_cur_h = nullptr;  // pinned mirror
   int* fail_d = nullptr;
-  ChunkMeta* meta_d = nullptr;
   int* lane_tab_d = nullptr;
-  SlotData* slots_d = nullptr;
+  SlotShared* slots_d = nullptr;
+  double2* dr_d = nullptr;
   int* slot_dpos_d = nullptr;
   int* ent_rowpos_d = nullptr;
   int* ent_src_d = nullptr;
-  double* ent_val_d = nullptr;
-  double* w_slot_d = nullptr;
-  int* tile_chunks_d = nullptr;
-  int* nbr_ptr_d = nullptr;
-  int* nbr_idx_d = nullptr;
-  int* progress_d = nullptr;  // n_tiles progress counters + 1 error word
-  int n_tiles = 1;
-  bool persistent = true;     // NNGP_SWEEP=launch selects one kernel per colour
-  double* r_d = nullptr;
+  double* ent_val_d = nullptr;   // C x n_entries
+  double* w_slot_d = nullptr;    // n x C
+  double* r_d = nullptr;         // n x C
   int* level_rows_d = nullptr;
   int* obs_ptr_d = nullptr;
   int* obs_idx_d = nullptr;
   int* lm_d = nullptr;  // locs_match, 0-based
   double* y_d = nullptr;
-  double* mu_d = nullptr;
-  double* field_d = nullptr;
-  double* field_prop_d = nullptr;
   double* tmp_d = nullptr;
   double* tmp2_d = nullptr;
   double* partials_d = nullptr;
   double* res_d = nullptr;
   double* z_d = nullptr;
   size_t z_cap = 0;
-  SweepScalars* scal_d = nullptr;
-  SweepScalars* scal_h = nullptr;  // pinned
+  SweepScalars* scal_d = nullptr;  // C
+  SweepScalars* scal_h = nullptr;  // pinned, C
   double* res_h = nullptr;         // pinned, 8 doubles
-  bool have_factor[2] = {false, false};
-  bool have_field = false, have_mu = false, mu_is_const = true;
-  double mu_beta0 = 0.0;
-  std::map<int, hipGraphExec_t> graphs;
+  std::map<long long, hipGraphExec_t> graphs;  // key: n_sweeps << 8 | chain mask
   std::vector<hipGraph_t> graph_objs;
 };
 
@@ -119,19 +126,28 @@ int set_device(nngp_ctx* c) {
 // sweep-layout pointers
 SweepDev sweep_dev(nngp_ctx* c) {
   SweepDev L;
-  L.meta = c->meta_d;
   L.lane_tab = c->lane_tab_d;
   L.slots = c->slots_d;
+  L.dr = c->dr_d;
   L.ent_val = c->ent_val_d;
   L.ent_rowpos = c->ent_rowpos_d;
   L.w_slot = c->w_slot_d;
   L.r = c->r_d;
+  L.scal = c->scal_d;
+  L.n_entries = c->lay.n_entries;
+  L.C = c->C;
+  L.LW = c->lay.LW;
   return L;
 }
 
-int refresh_sweep_values(nngp_ctx* c) {
-  HIPCHK(c, launch_sell_refresh(c->st, sweep_dev(c), c->lay.nchunks, c->ent_src_d, c->linv_d[0],
-                                c->ent_val_d));
+// sweep values of B + precision_diag of chain k from its current factor
+int refresh_sweep_values(nngp_ctx* c, int k) {
+  SweepDev L = sweep_dev(c);
+  for (const ColorArgs& ca : c->cargs)
+    HIPCHK(c, launch_sell_refresh_color(c->st, L, ca, c->ent_src_d, c->ch[k].linv_d[0], k));
+  c->linv_cur_h[k] = c->ch[k].linv_d[0];
+  HIPCHK(c, hipMemcpyAsync(c->linv_cur_d, c->linv_cur_h, sizeof(double*) * c->C, hipMemcpyHostToDevice, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
   return NNGP_OK;
 }
 
@@ -220,14 +236,18 @@ void nngp_ctx_destroy(nngp_ctx* c) {
   if (c->st) hipStreamSynchronize(c->st);
   for (auto& kv : c->graphs) hipGraphExecDestroy(kv.second);
   for (auto g : c->graph_objs) hipGraphDestroy(g);
-  void* ptrs[] = {c->locs_d, c->sc_d, c->nn_d, c->linv_d[0], c->linv_d[1], c->fail_d,
-                  c->meta_d, c->lane_tab_d, c->slots_d, c->slot_dpos_d, c->ent_rowpos_d, c->tile_chunks_d, c->nbr_ptr_d,
-                  c->nbr_idx_d, c->progress_d, c->ent_src_d, c->ent_val_d, c->w_slot_d, c->r_d, c->level_rows_d, c->obs_ptr_d, c->obs_idx_d,
-                  c->lm_d, c->y_d, c->mu_d, c->field_d, c->field_prop_d, c->tmp_d, c->tmp2_d,
-                  c->partials_d, c->res_d, c->z_d, c->scal_d};
+  std::vector<void*> ptrs = {c->locs_d, c->sc_d, c->nn_d, c->linv_cur_d, c->fail_d, c->lane_tab_d, c->slots_d,
+                             c->dr_d, c->slot_dpos_d, c->ent_rowpos_d, c->ent_src_d, c->ent_val_d, c->w_slot_d,
+                             c->r_d, c->level_rows_d, c->obs_ptr_d, c->obs_idx_d, c->lm_d, c->y_d, c->tmp_d,
+                             c->tmp2_d, c->partials_d, c->res_d, c->z_d, c->scal_d};
+  for (int k = 0; k < kMaxChains; ++k) {
+    ChainState& s = c->ch[k];
+    ptrs.insert(ptrs.end(), {s.linv_d[0], s.linv_d[1], s.field_d, s.field_prop_d, s.mu_d});
+  }
   for (void* p : ptrs) if (p) hipFree(p);
   if (c->scal_h) hipHostFree(c->scal_h);
   if (c->res_h) hipHostFree(c->res_h);
+  if (c->linv_cur_h) hipHostFree(c->linv_cur_h);
   if (c->st) hipStreamDestroy(c->st);
   delete c;
 }
@@ -235,13 +255,14 @@ void nngp_ctx_destroy(nngp_ctx* c) {
 const char* nngp_ctx_last_error(const nngp_ctx* c) { return c ? c->err.c_str() : g_err.c_str(); }
 
 int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b, const int* coloring,
-                    const int* locs_match, const double* observed_field, int n_obs, int device,
-                    nngp_ctx** out) {
+                    const int* locs_match, const double* observed_field, int n_obs, int n_chains,
+                    int device, nngp_ctx** out) {
   if (!out) return fail_msg(nullptr, NNGP_ERR_ARG, "ctx_create: out == NULL");
   *out = nullptr;
   if (!locs || !NNarray || !coloring || !locs_match || !observed_field || n < 1 || d < 1 || d > 4 ||
-      b < 1 || b > 32 || n_obs < 1)
-    return fail_msg(nullptr, NNGP_ERR_ARG, "ctx_create: bad arguments (need n>=1, 1<=d<=4, 1<=b<=32, n_obs>=1)");
+      b < 1 || b > 32 || n_obs < 1 || n_chains < 1 || n_chains > kMaxChains)
+    return fail_msg(nullptr, NNGP_ERR_ARG,
+                    "ctx_create: bad arguments (need n>=1, 1<=d<=4, 1<=b<=32, n_obs>=1, 1<=n_chains<=4)");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail_msg(nullptr, NNGP_ERR_NODEV, "no HIP device");
   nngp_ctx* c = new (std::nothrow) nngp_ctx();
@@ -249,7 +270,7 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
   if (device < 0) { if (hipGetDevice(&device) != hipSuccess) device = 0; }
   if (device >= ndev) { delete c; return fail_msg(nullptr, NNGP_ERR_ARG, "device ordinal out of range"); }
   c->device = device;
-  c->n = n; c->d = d; c->b = b; c->n_obs = n_obs;
+  c->n = n; c->d = d; c->b = b; c->n_obs = n_obs; c->C = n_chains;
   c->ds = d <= 2 ? 2 : (d == 3 ? 3 : 4);
   int rc;
   std::vector<int> nn;
@@ -282,40 +303,33 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
     std::vector<int> f(obs_cnt.begin(), obs_cnt.end() - 1);
     for (int o = 0; o < n_obs; ++o) obs_idx[f[lm0[o]]++] = o;
   }
-  {
-    int ncu = 0;
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1) ncu = 1;
-    c->n_tiles = std::max(1, std::min(ncu, n / 1024));
-    const char* mode = std::getenv("NNGP_SWEEP");
-    c->persistent = !(mode && std::string(mode) == "launch");
-  }
-  if (!build_sweep_layout(nn.data(), n, b, coloring, locs, d, c->n_tiles, c->lay, err)) {
+  const int LW = n_chains == 1 ? 64 : (n_chains == 2 ? 32 : 16);
+  if (!build_sweep_layout(nn.data(), n, b, coloring, locs, d, LW, c->lay, err)) {
     delete c;
     return fail_msg(nullptr, NNGP_ERR_ARG, err);
   }
-  {
-    // every chunk of colour c belongs to exactly one tile range of colour c
-    const SweepLayout& Ly = c->lay;
-    std::vector<int> owner(Ly.nchunks, 0);
-    for (int col = 0; col < Ly.K; ++col)
-      for (int t = 0; t < Ly.n_tiles; ++t) {
-        const int* tc = &Ly.tile_chunks[((size_t)col * Ly.n_tiles + t) * 3];
-        if (!(Ly.color_chunk_ptr[col] <= tc[0] && tc[0] <= tc[1] && tc[1] <= tc[2] &&
-              tc[2] <= Ly.color_chunk_ptr[col + 1])) {
-          delete c;
-          return fail_msg(nullptr, NNGP_ERR_ARG, "internal: bad tile chunk range");
-        }
-        for (int ch = tc[0]; ch < tc[2]; ++ch) owner[ch]++;
-      }
-    for (int ch = 0; ch < Ly.nchunks; ++ch)
-      if (owner[ch] != 1) { delete c; return fail_msg(nullptr, NNGP_ERR_ARG, "internal: tile ranges do not partition the chunks"); }
+  const SweepLayout& L = c->lay;
+  c->cargs.resize(L.K);
+  for (int col = 0; col < L.K; ++col) {
+    ColorArgs& ca = c->cargs[col];
+    std::memset(&ca, 0, sizeof ca);
+    ca.chunk0 = L.color_chunk_ptr[col];
+    ca.nch = L.color_chunk_ptr[col + 1] - ca.chunk0;
+    ca.ncls = L.n_class[col];
+    for (int q = 0; q < ca.ncls; ++q) {
+      ca.rows[q] = L.class_rows[(size_t)col * kMaxClasses + q];
+      ca.end[q] = L.class_end[(size_t)col * kMaxClasses + q];
+      ca.base[q] = L.class_base[(size_t)col * kMaxClasses + q];
+    }
+    if (ca.ncls < 1 || ca.end[ca.ncls - 1] != ca.nch) {
+      delete c;
+      return fail_msg(nullptr, NNGP_ERR_ARG, "internal: bad colour class table");
+    }
   }
   dag_levels(nn.data(), n, b, c->level_ptr, c->level_rows);
-  c->dpos = c->lay.rpos;
+  c->dpos = L.rpos;
   const std::vector<int>& dp = c->dpos;
   for (auto& r : c->level_rows) r = dp[r];
-  std::vector<int> nobs_slot(n);
-  for (int s = 0; s < n; ++s) { int i = c->lay.slot_loc[s]; nobs_slot[s] = obs_cnt[i + 1] - obs_cnt[i]; }
   // device-order copies
   std::vector<double> locs_rm((size_t)n * d);
   for (int i = 0; i < n; ++i)
@@ -328,7 +342,7 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
     }
   std::vector<int> lm_dev(n_obs), slot_dpos(n);
   for (int o = 0; o < n_obs; ++o) lm_dev[o] = dp[lm0[o]];
-  for (int s = 0; s < n; ++s) slot_dpos[s] = dp[c->lay.slot_loc[s]];
+  for (int s = 0; s < n; ++s) slot_dpos[s] = dp[L.slot_loc[s]];
 
   if ((rc = set_device(c))) { delete c; return rc; }
 #define CK(x)                                                     \
@@ -340,71 +354,65 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
       return r_;                                                  \
     }                                                             \
   } while (0)
+  const int C = n_chains;
   CK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
-  const SweepLayout& L = c->lay;
   CK(dalloc(&c->locs_d, (size_t)n * d));
   CK(dalloc(&c->sc_d, (size_t)n * c->ds));
   CK(dalloc(&c->nn_d, (size_t)n * b));
-  CK(dalloc(&c->linv_d[0], (size_t)n * b));
-  CK(dalloc(&c->linv_d[1], (size_t)n * b));
+  for (int k = 0; k < C; ++k) {
+    ChainState& s = c->ch[k];
+    CK(dalloc(&s.linv_d[0], (size_t)n * b));
+    CK(dalloc(&s.linv_d[1], (size_t)n * b));
+    CK(dalloc(&s.field_d, n));
+    CK(dalloc(&s.field_prop_d, n));
+    CK(dalloc(&s.mu_d, n_obs));
+  }
+  CK(dalloc(&c->linv_cur_d, C));
+  CK(hipHostMalloc((void**)&c->linv_cur_h, sizeof(double*) * C, hipHostMallocDefault));
+  for (int k = 0; k < C; ++k) c->linv_cur_h[k] = c->ch[k].linv_d[0];
   CK(dalloc(&c->fail_d, 1));
-  CK(dalloc(&c->meta_d, L.nchunks));
   CK(dalloc(&c->lane_tab_d, L.lane_tab.size()));
   CK(dalloc(&c->slots_d, n));
+  CK(dalloc(&c->dr_d, (size_t)n * C));
   CK(dalloc(&c->slot_dpos_d, n));
-  CK(dalloc(&c->tile_chunks_d, L.tile_chunks.size()));
-  CK(dalloc(&c->nbr_ptr_d, L.nbr_ptr.size()));
-  CK(dalloc(&c->nbr_idx_d, std::max<size_t>(1, L.nbr_idx.size())));
-  CK(dalloc(&c->progress_d, (size_t)c->n_tiles + 4));
   CK(dalloc(&c->ent_rowpos_d, (size_t)L.n_entries));
   CK(dalloc(&c->ent_src_d, (size_t)L.n_entries));
-  CK(dalloc(&c->ent_val_d, (size_t)L.n_entries));
-  CK(dalloc(&c->w_slot_d, n));
-  CK(dalloc(&c->r_d, n));
+  CK(dalloc(&c->ent_val_d, (size_t)L.n_entries * C));
+  CK(dalloc(&c->w_slot_d, (size_t)n * C));
+  CK(dalloc(&c->r_d, (size_t)n * C));
   CK(dalloc(&c->level_rows_d, n));
   CK(dalloc(&c->obs_ptr_d, (size_t)n + 1));
   CK(dalloc(&c->obs_idx_d, n_obs));
   CK(dalloc(&c->lm_d, n_obs));
   CK(dalloc(&c->y_d, n_obs));
-  CK(dalloc(&c->mu_d, n_obs));
-  CK(dalloc(&c->field_d, n));
-  CK(dalloc(&c->field_prop_d, n));
   CK(dalloc(&c->tmp_d, n));
   CK(dalloc(&c->tmp2_d, n));
   CK(dalloc(&c->partials_d, 4 * kRedBlocks));
   CK(dalloc(&c->res_d, 8));
-  CK(dalloc(&c->scal_d, 1));
-  CK(hipHostMalloc((void**)&c->scal_h, sizeof(SweepScalars), hipHostMallocDefault));
+  CK(dalloc(&c->scal_d, C));
+  CK(hipHostMalloc((void**)&c->scal_h, sizeof(SweepScalars) * C, hipHostMallocDefault));
+  std::memset(c->scal_h, 0, sizeof(SweepScalars) * C);
   CK(hipHostMalloc((void**)&c->res_h, 8 * sizeof(double), hipHostMallocDefault));
   CK(upload(c->locs_d, locs_rm.data(), locs_rm.size(), c->st));
   CK(upload(c->nn_d, nn_dev.data(), nn_dev.size(), c->st));
   {
-    std::vector<ChunkMeta> meta(L.nchunks);
-    for (int ch = 0; ch < L.nchunks; ++ch) {
-      meta[ch].slot0 = L.chunk_slot0[ch];
-      meta[ch].packed = L.chunk_len[ch] | (std::min(L.chunk_nslot[ch], 255) << 8) | (L.chunk_lk[ch] << 16);
-      meta[ch].off = L.chunk_off[ch];
-    }
-    std::vector<SlotData> sd(n);
+    std::vector<SlotShared> sd(n);
     for (int s = 0; s < n; ++s) {
-      sd[s].D = 0.0;
-      sd[s].R = 0.0;
-      sd[s].nobs = nobs_slot[s];
-      sd[s].loc = L.slot_loc[s];
+      const int i = L.slot_loc[s];
+      sd[s].loc = i;
+      sd[s].nobs = obs_cnt[i + 1] - obs_cnt[i];
       sd[s].collen = L.collen[s];
       sd[s].dpos = slot_dpos[s];
     }
-    CK(hipMemcpy(c->meta_d, meta.data(), sizeof(ChunkMeta) * meta.size(), hipMemcpyHostToDevice));
     CK(hipMemcpy(c->lane_tab_d, L.lane_tab.data(), sizeof(int) * L.lane_tab.size(), hipMemcpyHostToDevice));
-    CK(hipMemcpy(c->slots_d, sd.data(), sizeof(SlotData) * sd.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(c->slots_d, sd.data(), sizeof(SlotShared) * sd.size(), hipMemcpyHostToDevice));
   }
+  CK(hipMemsetAsync(c->dr_d, 0, sizeof(double2) * (size_t)n * C, c->st));
   CK(upload(c->slot_dpos_d, slot_dpos.data(), n, c->st));
-  CK(upload(c->tile_chunks_d, L.tile_chunks.data(), L.tile_chunks.size(), c->st));
-  CK(upload(c->nbr_ptr_d, L.nbr_ptr.data(), L.nbr_ptr.size(), c->st));
-  CK(upload(c->nbr_idx_d, L.nbr_idx.data(), L.nbr_idx.size(), c->st));
   CK(upload(c->ent_rowpos_d, L.ent_rowpos.data(), (size_t)L.n_entries, c->st));
   CK(upload(c->ent_src_d, L.ent_src.data(), (size_t)L.n_entries, c->st));
-  CK(hipMemsetAsync(c->ent_val_d, 0, sizeof(double) * std::max<long long>(1, L.n_entries), c->st));
+  CK(hipMemsetAsync(c->ent_val_d, 0, sizeof(double) * std::max<long long>(1, L.n_entries * C), c->st));
+  CK(hipMemcpyAsync(c->linv_cur_d, c->linv_cur_h, sizeof(double*) * C, hipMemcpyHostToDevice, c->st));
   CK(upload(c->level_rows_d, c->level_rows.data(), n, c->st));
   CK(upload(c->obs_ptr_d, obs_cnt.data(), (size_t)n + 1, c->st));
   CK(upload(c->obs_idx_d, obs_idx.data(), n_obs, c->st));
@@ -413,6 +421,13 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
   CK(hipStreamSynchronize(c->st));
 #undef CK
   *out = c;
+  return NNGP_OK;
+}
+
+int nngp_set_chain(nngp_ctx* c, int chain) {
+  if (!c) return NNGP_ERR_ARG;
+  if (chain < 0 || chain >= c->C) return fail_msg(c, NNGP_ERR_ARG, "set_chain: chain out of range");
+  c->cur = chain;
   return NNGP_OK;
 }
 
@@ -425,9 +440,9 @@ int nngp_ctx_info(const nngp_ctx* c, nngp_info* info) {
   info->n_entries = c->lay.n_entries;
   info->max_collen = c->lay.max_collen;
   info->device = c->device;
-  info->n_tiles = c->n_tiles;
-  info->n_boundary = c->lay.n_boundary;
-  info->sweep_mode = c->persistent ? 1 : 0;
+  info->n_chains = c->C;
+  info->lanes_per_chain = c->lay.LW;
+  info->n_chunks = c->lay.nchunks;
   return NNGP_OK;
 }
 
@@ -469,40 +484,42 @@ int nngp_factor(nngp_ctx* c, int which, int covfun, const double* cp, int ncp) {
   if (fam < 0) return fail_msg(c, NNGP_ERR_ARG, err);
   int rc;
   if ((rc = set_device(c))) return rc;
-  const int ds = (covfun == NNGP_EXPONENTIAL_SPHERE || covfun == NNGP_MATERN_SPHERE) ? 3 : c->ds;
-  if (ds > c->ds) {
+  ChainState& S = c->ch[c->cur];
+  const bool sphere = covfun == NNGP_EXPONENTIAL_SPHERE || covfun == NNGP_MATERN_SPHERE;
+  if (sphere && c->ds < 3) {
     // sphere on d == 2: scaled coordinates are 3-D; grow the buffer once
     hipFree(c->sc_d);
     c->sc_d = nullptr;
     HIPCHK(c, dalloc(&c->sc_d, (size_t)c->n * 4));
     c->ds = 4;  // capacity marker
   }
-  const int use_ds = (covfun == NNGP_EXPONENTIAL_SPHERE || covfun == NNGP_MATERN_SPHERE) ? 3 : (c->d <= 2 ? 2 : (c->d == 3 ? 3 : 4));
+  const int use_ds = sphere ? 3 : (c->d <= 2 ? 2 : (c->d == 3 ? 3 : 4));
   HIPCHK(c, launch_scale_coords(c->st, covfun, cp, ncp, c->locs_d, c->n, c->d, c->sc_d, use_ds));
   const int big = INT_MAX;
   HIPCHK(c, hipMemcpyAsync(c->fail_d, &big, sizeof(int), hipMemcpyHostToDevice, c->st));
-  HIPCHK(c, launch_factor(c->st, fam, var, nug, nu, c->sc_d, use_ds, c->nn_d, c->n, c->b, c->linv_d[which], c->fail_d));
+  HIPCHK(c, launch_factor(c->st, fam, var, nug, nu, c->sc_d, use_ds, c->nn_d, c->n, c->b, S.linv_d[which], c->fail_d));
   int fail = 0;
   HIPCHK(c, hipMemcpyAsync(&fail, c->fail_d, sizeof(int), hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
   if (fail != big) {
-    c->have_factor[which] = false;
+    S.have_factor[which] = false;
     char buf[160];
     std::snprintf(buf, sizeof buf, "vecchia factor: local covariance of row %d is not positive definite", fail);
     return fail_msg(c, NNGP_ERR_CHOL, buf);
   }
-  c->have_factor[which] = true;
-  if (which == 0) return refresh_sweep_values(c);
+  S.have_factor[which] = true;
+  if (which == 0) return refresh_sweep_values(c, c->cur);
   return NNGP_OK;
 }
 
 int nngp_get_linv(nngp_ctx* c, int which, double* Linv) {
   if (!c || !Linv || (which != 0 && which != 1)) return NNGP_ERR_ARG;
-  if (!c->have_factor[which]) return fail_msg(c, NNGP_ERR_STATE, "get_linv: factor not computed");
+  ChainState& S = c->ch[c->cur];
+  if (!S.have_factor[which]) return fail_msg(c, NNGP_ERR_STATE, "get_linv: factor not computed");
   int rc;
   if ((rc = set_device(c))) return rc;
   std::vector<double> rm((size_t)c->n * c->b);
-  HIPCHK(c, hipMemcpyAsync(rm.data(), c->linv_d[which], rm.size() * sizeof(double), hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipMemcpyAsync(rm.data(), S.linv_d[which], rm.size() * sizeof(double), hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
   for (int i = 0; i < c->n; ++i)
     for (int j = 0; j < c->b; ++j) Linv[i + (size_t)j * c->n] = rm[(size_t)c->dpos[i] * c->b + j];
@@ -513,40 +530,38 @@ int nngp_set_linv(nngp_ctx* c, int which, const double* Linv) {
   if (!c || !Linv || (which != 0 && which != 1)) return NNGP_ERR_ARG;
   int rc;
   if ((rc = set_device(c))) return rc;
+  ChainState& S = c->ch[c->cur];
   std::vector<double> rm((size_t)c->n * c->b);
   for (int i = 0; i < c->n; ++i)
     for (int j = 0; j < c->b; ++j) rm[(size_t)c->dpos[i] * c->b + j] = Linv[i + (size_t)j * c->n];
-  HIPCHK(c, hipMemcpyAsync(c->linv_d[which], rm.data(), rm.size() * sizeof(double), hipMemcpyHostToDevice, c->st));
+  HIPCHK(c, hipMemcpyAsync(S.linv_d[which], rm.data(), rm.size() * sizeof(double), hipMemcpyHostToDevice, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
-  c->have_factor[which] = true;
-  if (which == 0) return refresh_sweep_values(c);
+  S.have_factor[which] = true;
+  if (which == 0) return refresh_sweep_values(c, c->cur);
   return NNGP_OK;
 }
 
 int nngp_accept_factor(nngp_ctx* c) {
   if (!c) return NNGP_ERR_ARG;
-  if (!c->have_factor[1]) return fail_msg(c, NNGP_ERR_STATE, "accept_factor: no proposal factor");
+  ChainState& S = c->ch[c->cur];
+  if (!S.have_factor[1]) return fail_msg(c, NNGP_ERR_STATE, "accept_factor: no proposal factor");
   int rc;
   if ((rc = set_device(c))) return rc;
-  std::swap(c->linv_d[0], c->linv_d[1]);
-  std::swap(c->have_factor[0], c->have_factor[1]);
-  // cached graphs captured the old buffer pointers
-  for (auto& kv : c->graphs) hipGraphExecDestroy(kv.second);
-  c->graphs.clear();
-  for (auto g : c->graph_objs) hipGraphDestroy(g);
-  c->graph_objs.clear();
-  return refresh_sweep_values(c);
+  std::swap(S.linv_d[0], S.linv_d[1]);
+  std::swap(S.have_factor[0], S.have_factor[1]);
+  // captured sweep graphs read the current factor through linv_cur_d: they stay valid
+  return refresh_sweep_values(c, c->cur);
 }
 
 int nngp_get_precision_diag(nngp_ctx* c, double* D) {
   if (!c || !D) return NNGP_ERR_ARG;
-  if (!c->have_factor[0]) return fail_msg(c, NNGP_ERR_STATE, "precision_diag: no factor");
+  if (!c->ch[c->cur].have_factor[0]) return fail_msg(c, NNGP_ERR_STATE, "precision_diag: no factor");
   int rc;
   if ((rc = set_device(c))) return rc;
-  std::vector<SlotData> sd(c->n);
-  HIPCHK(c, hipMemcpyAsync(sd.data(), c->slots_d, c->n * sizeof(SlotData), hipMemcpyDeviceToHost, c->st));
+  std::vector<double2> dr((size_t)c->n * c->C);
+  HIPCHK(c, hipMemcpyAsync(dr.data(), c->dr_d, dr.size() * sizeof(double2), hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
-  for (int s = 0; s < c->n; ++s) D[c->lay.slot_loc[s]] = sd[s].D;
+  for (int s = 0; s < c->n; ++s) D[c->lay.slot_loc[s]] = dr[(size_t)s * c->C + c->cur].x;
   return NNGP_OK;
 }
 
@@ -555,21 +570,23 @@ int nngp_set_field(nngp_ctx* c, const double* field) {
   if (!c || !field) return NNGP_ERR_ARG;
   int rc;
   if ((rc = set_device(c))) return rc;
+  ChainState& S = c->ch[c->cur];
   std::vector<double> f(c->n);
   for (int i = 0; i < c->n; ++i) f[c->dpos[i]] = field[i];
-  HIPCHK(c, hipMemcpyAsync(c->field_d, f.data(), c->n * sizeof(double), hipMemcpyHostToDevice, c->st));
+  HIPCHK(c, hipMemcpyAsync(S.field_d, f.data(), c->n * sizeof(double), hipMemcpyHostToDevice, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
-  c->have_field = true;
+  S.have_field = true;
   return NNGP_OK;
 }
 
 int nngp_get_field(nngp_ctx* c, double* field) {
   if (!c || !field) return NNGP_ERR_ARG;
-  if (!c->have_field) return fail_msg(c, NNGP_ERR_STATE, "get_field: no field");
+  ChainState& S = c->ch[c->cur];
+  if (!S.have_field) return fail_msg(c, NNGP_ERR_STATE, "get_field: no field");
   int rc;
   if ((rc = set_device(c))) return rc;
   std::vector<double> f(c->n);
-  HIPCHK(c, hipMemcpyAsync(f.data(), c->field_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipMemcpyAsync(f.data(), S.field_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
   for (int i = 0; i < c->n; ++i) field[i] = f[c->dpos[i]];
   return NNGP_OK;
@@ -579,23 +596,25 @@ int nngp_set_mu(nngp_ctx* c, const double* mu, double beta0) {
   if (!c) return NNGP_ERR_ARG;
   int rc;
   if ((rc = set_device(c))) return rc;
-  if (mu) HIPCHK(c, hipMemcpyAsync(c->mu_d, mu, c->n_obs * sizeof(double), hipMemcpyHostToDevice, c->st));
-  c->mu_is_const = (mu == nullptr);
-  c->mu_beta0 = beta0;
-  HIPCHK(c, launch_residual_sums(c->st, c->n, c->slots_d, c->obs_ptr_d, c->obs_idx_d, c->y_d,
-                                 mu ? c->mu_d : nullptr, beta0));
+  ChainState& S = c->ch[c->cur];
+  if (mu) HIPCHK(c, hipMemcpyAsync(S.mu_d, mu, c->n_obs * sizeof(double), hipMemcpyHostToDevice, c->st));
+  S.mu_is_const = (mu == nullptr);
+  S.mu_beta0 = beta0;
+  HIPCHK(c, launch_residual_sums(c->st, c->n, sweep_dev(c), c->cur, c->obs_ptr_d, c->obs_idx_d, c->y_d,
+                                 mu ? S.mu_d : nullptr, beta0));
   HIPCHK(c, hipStreamSynchronize(c->st));
-  c->have_mu = true;
+  S.have_mu = true;
   return NNGP_OK;
 }
 
 // ---------------------------------------------------------------- loglik
 int nngp_loglik(nngp_ctx* c, int which, double beta0, double log_scale, double* ll) {
   if (!c || !ll || (which != 0 && which != 1)) return NNGP_ERR_ARG;
-  if (!c->have_factor[which] || !c->have_field) return fail_msg(c, NNGP_ERR_STATE, "loglik: need factor and field");
+  ChainState& S = c->ch[c->cur];
+  if (!S.have_factor[which] || !S.have_field) return fail_msg(c, NNGP_ERR_STATE, "loglik: need factor and field");
   int rc;
   if ((rc = set_device(c))) return rc;
-  int nb = launch_row_stats(c->st, c->linv_d[which], c->nn_d, c->n, c->b, c->field_d, beta0, nullptr,
+  int nb = launch_row_stats(c->st, S.linv_d[which], c->nn_d, c->n, c->b, S.field_d, beta0, nullptr,
                             c->partials_d);
   HIPCHK(c, hipGetLastError());
   double r[4];
@@ -605,73 +624,79 @@ int nngp_loglik(nngp_ctx* c, int which, double beta0, double log_scale, double* 
 }
 
 // ---------------------------------------------------------------- sweep
-static int sweep_prepare(nngp_ctx* c, double beta0, double log_scale, double lnv, uint64_t seed,
+static int sweep_prepare(nngp_ctx* c, int k, double beta0, double log_scale, double lnv, uint64_t seed,
                          uint64_t counter_base) {
-  if (!c->have_factor[0] || !c->have_field || !c->have_mu)
-    return fail_msg(c, NNGP_ERR_STATE, "sweep: need factor, field and mu");
-  if (c->mu_is_const && c->mu_beta0 != beta0) {
-    // residual sums depend on beta0 when mu = beta0
-    HIPCHK(c, launch_residual_sums(c->st, c->n, c->slots_d, c->obs_ptr_d, c->obs_idx_d, c->y_d,
-                                   nullptr, beta0));
-    c->mu_beta0 = beta0;
+  ChainState& S = c->ch[k];
+  if (!S.have_factor[0] || !S.have_field || !S.have_mu) {
+    char buf[96];
+    std::snprintf(buf, sizeof buf, "sweep: chain %d needs factor, field and mu", k);
+    return fail_msg(c, NNGP_ERR_STATE, buf);
   }
-  c->scal_h->inv_s2 = std::exp(-log_scale);
-  c->scal_h->inv_t2 = std::exp(-lnv);
-  c->scal_h->beta0 = beta0;
-  c->scal_h->pad = 0;
-  c->scal_h->seed = seed;
-  c->scal_h->counter_base = counter_base;
-  HIPCHK(c, hipMemcpyAsync(c->scal_d, c->scal_h, sizeof(SweepScalars), hipMemcpyHostToDevice, c->st));
+  if (S.mu_is_const && S.mu_beta0 != beta0) {
+    // residual sums depend on beta0 when mu = beta0
+    HIPCHK(c, launch_residual_sums(c->st, c->n, sweep_dev(c), k, c->obs_ptr_d, c->obs_idx_d, c->y_d,
+                                   nullptr, beta0));
+    S.mu_beta0 = beta0;
+  }
+  SweepScalars& sc = c->scal_h[k];
+  sc.inv_s2 = std::exp(-log_scale);
+  sc.inv_t2 = std::exp(-lnv);
+  sc.beta0 = beta0;
+  sc.pad = 0;
+  sc.seed = seed;
+  sc.counter_base = counter_base;
   return NNGP_OK;
 }
 
-// r = B (field - beta0), written at Morton positions; w_slot = field - beta0
-static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, const double* z_dev,
+static int upload_scalars(nngp_ctx* c) {
+  HIPCHK(c, hipMemcpyAsync(c->scal_d, c->scal_h, sizeof(SweepScalars) * c->C, hipMemcpyHostToDevice, c->st));
+  return NNGP_OK;
+}
+
+// per chain in mask: w = field - beta0 (slot order), r = B w (Morton rows);
+// then every colour of every sweep; then field = w + beta0
+static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, int mask, const double* z_dev,
                               std::vector<hipEvent_t>* evs) {
   const int n = c->n;
-  HIPCHK(c, launch_field_to_slots(c->st, n, c->slot_dpos_d, c->field_d, c->scal_d, c->w_slot_d));
-  // shift read from device memory so a replayed graph sees the current beta0
-  launch_row_stats(c->st, c->linv_d[0], c->nn_d, n, c->b, c->field_d, 0.0, c->r_d, c->partials_d,
-                   &c->scal_d->beta0);
-  HIPCHK(c, hipGetLastError());
-  SweepDev L = sweep_dev(c);
-  if (c->persistent) {
-    // zero the progress counters + error word every call (graph memset node)
-    HIPCHK(c, launch_fill_int(c->st, c->progress_d, c->n_tiles + 4, 0));
-    if (evs) HIPCHK(c, hipEventRecord((*evs)[0], c->st));
-    HIPCHK(c, launch_sweep_persistent(c->st, L, c->tile_chunks_d, c->n_tiles, c->lay.K, n_sweeps, c->nbr_ptr_d,
-                                      c->nbr_idx_d, c->progress_d, c->progress_d + c->n_tiles, c->scal_d, z_dev, n));
-    if (evs) HIPCHK(c, hipEventRecord((*evs)[1], c->st));
-    HIPCHK(c, launch_slots_to_field(c->st, n, c->slot_dpos_d, c->w_slot_d, c->scal_d, c->field_d));
-    return NNGP_OK;
+  for (int k = 0; k < c->C; ++k) {
+    if (!((mask >> k) & 1)) continue;
+    HIPCHK(c, launch_field_to_slots(c->st, n, c->slot_dpos_d, c->ch[k].field_d, c->scal_d, c->w_slot_d, c->C, k));
+    // factor pointer and beta0 read from device memory so a replayed graph
+    // sees the current factor and beta0
+    launch_row_stats(c->st, nullptr, c->nn_d, n, c->b, c->ch[k].field_d, 0.0, c->r_d + k, c->partials_d,
+                     &c->scal_d[k].beta0, c->linv_cur_d + k, c->C);
+    HIPCHK(c, hipGetLastError());
   }
+  SweepDev L = sweep_dev(c);
   for (int s = 0; s < n_sweeps; ++s) {
     for (int col = 0; col < c->lay.K; ++col) {
-      int ch0 = c->lay.color_chunk_ptr[col];
-      int nch = c->lay.color_chunk_ptr[col + 1] - ch0;
       if (evs) HIPCHK(c, hipEventRecord((*evs)[2 * ((size_t)s * c->lay.K + col)], c->st));
-      HIPCHK(c, launch_sweep_color(c->st, L, ch0, nch, c->scal_d, s, z_dev, n));
+      HIPCHK(c, launch_sweep_color(c->st, L, c->cargs[col], mask, s, z_dev, n));
       if (evs) HIPCHK(c, hipEventRecord((*evs)[2 * ((size_t)s * c->lay.K + col) + 1], c->st));
     }
   }
-  HIPCHK(c, launch_slots_to_field(c->st, n, c->slot_dpos_d, c->w_slot_d, c->scal_d, c->field_d));
+  for (int k = 0; k < c->C; ++k)
+    if ((mask >> k) & 1)
+      HIPCHK(c, launch_slots_to_field(c->st, n, c->slot_dpos_d, c->w_slot_d, c->scal_d, c->ch[k].field_d, c->C, k));
   return NNGP_OK;
 }
 
-static int check_persistent(nngp_ctx* c) {
-  if (!c->persistent) return NNGP_OK;
-  std::vector<int> prog(c->n_tiles + 4);
-  HIPCHK(c, hipMemcpy(prog.data(), c->progress_d, sizeof(int) * prog.size(), hipMemcpyDeviceToHost));
-  const int e = prog[c->n_tiles];
-  if (e) {
-    int mn = prog[0], mx = prog[0];
-    for (int t = 0; t < c->n_tiles; ++t) { mn = std::min(mn, prog[t]); mx = std::max(mx, prog[t]); }
-    char buf[200];
-    std::snprintf(buf, sizeof buf,
-                  "persistent sweep: error word 0x%08x (tile %d timed out); progress min %d max %d of %d tiles",
-                  (unsigned)e, e - 1, mn, mx, c->n_tiles);
-    return fail_msg(c, NNGP_ERR_HIP, buf);
+static int graph_for(nngp_ctx* c, int n_sweeps, int mask, hipGraphExec_t* out) {
+  const long long key = ((long long)n_sweeps << 8) | mask;
+  auto it = c->graphs.find(key);
+  if (it == c->graphs.end()) {
+    hipGraph_t g;
+    HIPCHK(c, hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
+    int rc = enqueue_sweep_body(c, n_sweeps, mask, nullptr, nullptr);
+    hipError_t e = hipStreamEndCapture(c->st, &g);
+    if (rc) return rc;
+    if (e != hipSuccess) return fail_hip(c, e, "hipStreamEndCapture");
+    hipGraphExec_t ex;
+    HIPCHK(c, hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    c->graph_objs.push_back(g);
+    it = c->graphs.emplace(key, ex).first;
   }
+  *out = it->second;
   return NNGP_OK;
 }
 
@@ -681,9 +706,11 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
   if (n_sweeps == 0) return NNGP_OK;
   int rc;
   if ((rc = set_device(c))) return rc;
-  if ((rc = sweep_prepare(c, beta0, log_scale, lnv, seed, counter_base))) return rc;
+  const int k = c->cur, mask = 1 << k;
+  if ((rc = sweep_prepare(c, k, beta0, log_scale, lnv, seed, counter_base))) return rc;
+  if ((rc = upload_scalars(c))) return rc;
   if (z) {
-    size_t need = (size_t)n_sweeps * c->n;
+    const size_t need = (size_t)n_sweeps * c->C * c->n;
     if (need > c->z_cap) {
       if (c->z_d) hipFree(c->z_d);
       c->z_d = nullptr;
@@ -691,65 +718,65 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
       HIPCHK(c, dalloc(&c->z_d, need));
       c->z_cap = need;
     }
-    HIPCHK(c, hipMemcpyAsync(c->z_d, z, need * sizeof(double), hipMemcpyHostToDevice, c->st));
-    if ((rc = enqueue_sweep_body(c, n_sweeps, c->z_d, nullptr))) return rc;
+    for (int s = 0; s < n_sweeps; ++s)
+      HIPCHK(c, hipMemcpyAsync(c->z_d + ((size_t)s * c->C + k) * c->n, z + (size_t)s * c->n,
+                               c->n * sizeof(double), hipMemcpyHostToDevice, c->st));
+    if ((rc = enqueue_sweep_body(c, n_sweeps, mask, c->z_d, nullptr))) return rc;
   } else {
     // replay a captured graph of the whole call (launch-bound at small n)
-    auto it = c->graphs.find(n_sweeps);
-    if (it == c->graphs.end()) {
-      hipGraph_t g;
-      HIPCHK(c, hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
-      rc = enqueue_sweep_body(c, n_sweeps, nullptr, nullptr);
-      hipError_t e = hipStreamEndCapture(c->st, &g);
-      if (rc) return rc;
-      if (e != hipSuccess) return fail_hip(c, e, "hipStreamEndCapture");
-      hipGraphExec_t ex;
-      HIPCHK(c, hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-      c->graph_objs.push_back(g);
-      it = c->graphs.emplace(n_sweeps, ex).first;
-    }
-    HIPCHK(c, hipGraphLaunch(it->second, c->st));
+    hipGraphExec_t ex;
+    if ((rc = graph_for(c, n_sweeps, mask, &ex))) return rc;
+    HIPCHK(c, hipGraphLaunch(ex, c->st));
   }
   HIPCHK(c, hipStreamSynchronize(c->st));
-  return check_persistent(c);
+  return NNGP_OK;
 }
 
-int nngp_sweep_timed(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double lnv,
-                     uint64_t seed, uint64_t counter_base, double* ms, double* kernel_ms) {
-  if (!c || n_sweeps < 1 || !ms) return NNGP_ERR_ARG;
+int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const double* log_scale,
+                      const double* lnv, const uint64_t* seed, const uint64_t* counter_base) {
+  if (!c || n_sweeps < 0 || !beta0 || !log_scale || !lnv || !seed || !counter_base) return NNGP_ERR_ARG;
+  if (n_sweeps == 0) return NNGP_OK;
   int rc;
   if ((rc = set_device(c))) return rc;
-  if ((rc = sweep_prepare(c, beta0, log_scale, lnv, seed, counter_base))) return rc;
+  for (int k = 0; k < c->C; ++k)
+    if ((rc = sweep_prepare(c, k, beta0[k], log_scale[k], lnv[k], seed[k], counter_base[k]))) return rc;
+  if ((rc = upload_scalars(c))) return rc;
+  hipGraphExec_t ex;
+  if ((rc = graph_for(c, n_sweeps, (1 << c->C) - 1, &ex))) return rc;
+  HIPCHK(c, hipGraphLaunch(ex, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  return NNGP_OK;
+}
+
+int nngp_sweep_timed(nngp_ctx* c, int n_sweeps, const double* beta0, const double* log_scale,
+                     const double* lnv, const uint64_t* seed, const uint64_t* counter_base, double* ms,
+                     double* kernel_ms) {
+  if (!c || n_sweeps < 1 || !ms || !beta0 || !log_scale || !lnv || !seed || !counter_base) return NNGP_ERR_ARG;
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  for (int k = 0; k < c->C; ++k)
+    if ((rc = sweep_prepare(c, k, beta0[k], log_scale[k], lnv[k], seed[k], counter_base[k]))) return rc;
+  if ((rc = upload_scalars(c))) return rc;
+  const int mask = (1 << c->C) - 1;
   hipEvent_t e0, e1;
   HIPCHK(c, hipEventCreate(&e0));
   HIPCHK(c, hipEventCreate(&e1));
   std::vector<hipEvent_t> evs;
   if (kernel_ms) {
-    evs.resize(c->persistent ? 2 : 2 * (size_t)n_sweeps * c->lay.K);
+    evs.resize(2 * (size_t)n_sweeps * c->lay.K);
     for (auto& e : evs) HIPCHK(c, hipEventCreate(&e));
     // a bounded spin kernel keeps the GPU busy while the host enqueues the
     // event-bracketed launches, so no host submission gap lands inside a
     // measured interval
     HIPCHK(c, launch_spin(c->st, 0.05 + 2e-5 * (double)evs.size()));
     HIPCHK(c, hipEventRecord(e0, c->st));
-    rc = enqueue_sweep_body(c, n_sweeps, nullptr, &evs);
+    rc = enqueue_sweep_body(c, n_sweeps, mask, nullptr, &evs);
     HIPCHK(c, hipEventRecord(e1, c->st));
   } else {
-    auto it = c->graphs.find(n_sweeps);
-    if (it == c->graphs.end()) {
-      hipGraph_t g;
-      HIPCHK(c, hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
-      rc = enqueue_sweep_body(c, n_sweeps, nullptr, nullptr);
-      hipError_t e = hipStreamEndCapture(c->st, &g);
-      if (rc) return rc;
-      if (e != hipSuccess) return fail_hip(c, e, "hipStreamEndCapture");
-      hipGraphExec_t ex;
-      HIPCHK(c, hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-      c->graph_objs.push_back(g);
-      it = c->graphs.emplace(n_sweeps, ex).first;
-    }
+    hipGraphExec_t ex;
+    if ((rc = graph_for(c, n_sweeps, mask, &ex))) return rc;
     HIPCHK(c, hipEventRecord(e0, c->st));
-    HIPCHK(c, hipGraphLaunch(it->second, c->st));
+    HIPCHK(c, hipGraphLaunch(ex, c->st));
     HIPCHK(c, hipEventRecord(e1, c->st));
   }
   HIPCHK(c, hipStreamSynchronize(c->st));
@@ -783,27 +810,28 @@ static int tri_solve_dev(nngp_ctx* c, const double* linv, const double* u, doubl
 
 int nngp_ancillary_propose(nngp_ctx* c, double beta0, double dlog_scale) {
   if (!c) return NNGP_ERR_ARG;
-  if (!c->have_factor[0] || !c->have_factor[1] || !c->have_field)
+  ChainState& S = c->ch[c->cur];
+  if (!S.have_factor[0] || !S.have_factor[1] || !S.have_field)
     return fail_msg(c, NNGP_ERR_STATE, "ancillary_propose: need both factors and the field");
   int rc;
   if ((rc = set_device(c))) return rc;
   // tmp = B_cur (field - beta0)
-  launch_row_stats(c->st, c->linv_d[0], c->nn_d, c->n, c->b, c->field_d, beta0, c->tmp_d,
-                   c->partials_d);
+  launch_row_stats(c->st, S.linv_d[0], c->nn_d, c->n, c->b, S.field_d, beta0, c->tmp_d, c->partials_d);
   HIPCHK(c, hipGetLastError());
-  if ((rc = tri_solve_dev(c, c->linv_d[1], c->tmp_d, c->tmp2_d))) return rc;
-  HIPCHK(c, launch_axpby_shift(c->st, c->n, c->tmp2_d, std::exp(0.5 * dlog_scale), beta0, c->field_prop_d));
+  if ((rc = tri_solve_dev(c, S.linv_d[1], c->tmp_d, c->tmp2_d))) return rc;
+  HIPCHK(c, launch_axpby_shift(c->st, c->n, c->tmp2_d, std::exp(0.5 * dlog_scale), beta0, S.field_prop_d));
   HIPCHK(c, hipStreamSynchronize(c->st));
   return NNGP_OK;
 }
 
 int nngp_field_response_ratio(nngp_ctx* c, double beta0, double lnv, double* ratio) {
   if (!c || !ratio) return NNGP_ERR_ARG;
-  if (!c->have_field || !c->have_mu) return fail_msg(c, NNGP_ERR_STATE, "response_ratio: need field and mu");
+  ChainState& S = c->ch[c->cur];
+  if (!S.have_field || !S.have_mu) return fail_msg(c, NNGP_ERR_STATE, "response_ratio: need field and mu");
   int rc;
   if ((rc = set_device(c))) return rc;
-  int nb = launch_obs_reduce(c->st, 1, c->n_obs, c->y_d, c->mu_is_const ? nullptr : c->mu_d, beta0,
-                             c->lm_d, c->field_d, c->field_prop_d, 0.5 * std::exp(-lnv), c->partials_d);
+  int nb = launch_obs_reduce(c->st, 1, c->n_obs, c->y_d, S.mu_is_const ? nullptr : S.mu_d, beta0,
+                             c->lm_d, S.field_d, S.field_prop_d, 0.5 * std::exp(-lnv), c->partials_d);
   HIPCHK(c, hipGetLastError());
   double r[4];
   if ((rc = fetch4(c, nb, r))) return rc;
@@ -815,18 +843,19 @@ int nngp_accept_field(nngp_ctx* c) {
   if (!c) return NNGP_ERR_ARG;
   int rc;
   if ((rc = set_device(c))) return rc;
-  HIPCHK(c, hipMemcpyAsync(c->field_d, c->field_prop_d, c->n * sizeof(double), hipMemcpyDeviceToDevice, c->st));
+  ChainState& S = c->ch[c->cur];
+  HIPCHK(c, hipMemcpyAsync(S.field_d, S.field_prop_d, c->n * sizeof(double), hipMemcpyDeviceToDevice, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
   return NNGP_OK;
 }
 
 int nngp_beta0_stats(nngp_ctx* c, double* oqo, double* oqf) {
   if (!c || !oqo || !oqf) return NNGP_ERR_ARG;
-  if (!c->have_factor[0] || !c->have_field) return fail_msg(c, NNGP_ERR_STATE, "beta0_stats: need factor and field");
+  ChainState& S = c->ch[c->cur];
+  if (!S.have_factor[0] || !S.have_field) return fail_msg(c, NNGP_ERR_STATE, "beta0_stats: need factor and field");
   int rc;
   if ((rc = set_device(c))) return rc;
-  int nb = launch_row_stats(c->st, c->linv_d[0], c->nn_d, c->n, c->b, c->field_d, 0.0, nullptr,
-                            c->partials_d);
+  int nb = launch_row_stats(c->st, S.linv_d[0], c->nn_d, c->n, c->b, S.field_d, 0.0, nullptr, c->partials_d);
   HIPCHK(c, hipGetLastError());
   double r[4];
   if ((rc = fetch4(c, nb, r))) return rc;
@@ -837,11 +866,12 @@ int nngp_beta0_stats(nngp_ctx* c, double* oqo, double* oqf) {
 
 int nngp_sum_squared_residuals(nngp_ctx* c, double beta0, double* ssr) {
   if (!c || !ssr) return NNGP_ERR_ARG;
-  if (!c->have_field || !c->have_mu) return fail_msg(c, NNGP_ERR_STATE, "ssr: need field and mu");
+  ChainState& S = c->ch[c->cur];
+  if (!S.have_field || !S.have_mu) return fail_msg(c, NNGP_ERR_STATE, "ssr: need field and mu");
   int rc;
   if ((rc = set_device(c))) return rc;
-  int nb = launch_obs_reduce(c->st, 0, c->n_obs, c->y_d, c->mu_is_const ? nullptr : c->mu_d, beta0,
-                             c->lm_d, c->field_d, nullptr, 0.0, c->partials_d);
+  int nb = launch_obs_reduce(c->st, 0, c->n_obs, c->y_d, S.mu_is_const ? nullptr : S.mu_d, beta0,
+                             c->lm_d, S.field_d, nullptr, 0.0, c->partials_d);
   HIPCHK(c, hipGetLastError());
   double r[4];
   if ((rc = fetch4(c, nb, r))) return rc;
@@ -851,14 +881,15 @@ int nngp_sum_squared_residuals(nngp_ctx* c, double beta0, double* ssr) {
 
 int nngp_spmv(nngp_ctx* c, int which, const double* X, int ncols, double* Y) {
   if (!c || !X || !Y || ncols < 0 || (which != 0 && which != 1)) return NNGP_ERR_ARG;
-  if (!c->have_factor[which]) return fail_msg(c, NNGP_ERR_STATE, "spmv: no factor");
+  ChainState& S = c->ch[c->cur];
+  if (!S.have_factor[which]) return fail_msg(c, NNGP_ERR_STATE, "spmv: no factor");
   int rc;
   if ((rc = set_device(c))) return rc;
   std::vector<double> in(c->n), outv(c->n);
   for (int col = 0; col < ncols; ++col) {
     for (int i = 0; i < c->n; ++i) in[c->dpos[i]] = X[(size_t)col * c->n + i];
     HIPCHK(c, hipMemcpyAsync(c->tmp2_d, in.data(), c->n * sizeof(double), hipMemcpyHostToDevice, c->st));
-    launch_row_stats(c->st, c->linv_d[which], c->nn_d, c->n, c->b, c->tmp2_d, 0.0, c->tmp_d, c->partials_d);
+    launch_row_stats(c->st, S.linv_d[which], c->nn_d, c->n, c->b, c->tmp2_d, 0.0, c->tmp_d, c->partials_d);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(outv.data(), c->tmp_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
     HIPCHK(c, hipStreamSynchronize(c->st));
@@ -869,13 +900,14 @@ int nngp_spmv(nngp_ctx* c, int which, const double* X, int ncols, double* Y) {
 
 int nngp_tri_solve(nngp_ctx* c, int which, const double* u, double* x) {
   if (!c || !u || !x || (which != 0 && which != 1)) return NNGP_ERR_ARG;
-  if (!c->have_factor[which]) return fail_msg(c, NNGP_ERR_STATE, "tri_solve: no factor");
+  ChainState& S = c->ch[c->cur];
+  if (!S.have_factor[which]) return fail_msg(c, NNGP_ERR_STATE, "tri_solve: no factor");
   int rc;
   if ((rc = set_device(c))) return rc;
   std::vector<double> in(c->n), outv(c->n);
   for (int i = 0; i < c->n; ++i) in[c->dpos[i]] = u[i];
   HIPCHK(c, hipMemcpyAsync(c->tmp_d, in.data(), c->n * sizeof(double), hipMemcpyHostToDevice, c->st));
-  if ((rc = tri_solve_dev(c, c->linv_d[which], c->tmp_d, c->tmp2_d))) return rc;
+  if ((rc = tri_solve_dev(c, S.linv_d[which], c->tmp_d, c->tmp2_d))) return rc;
   HIPCHK(c, hipMemcpyAsync(outv.data(), c->tmp2_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
   for (int i = 0; i < c->n; ++i) x[i] = outv[c->dpos[i]];

@@ -325,9 +325,11 @@ int greedy_coloring(const int* nn, int n, int b, std::vector<int>& colors) {
 
 // ---------------------------------------------------------------- layout
 bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const double* locs, int d,
-                        int n_tiles, SweepLayout& L, std::string& err) {
+                        int LW, SweepLayout& L, std::string& err) {
   L = SweepLayout();
-  L.n = n; L.b = b;
+  L.n = n; L.b = b; L.LW = LW;
+  if (LW != 64 && LW != 32 && LW != 16) { err = "lanes_per_chain must be 64, 32 or 16"; return false; }
+  if (n >= (1 << 28) - 1) { err = "n too large for the sweep lane table (< 2^28)"; return false; }
   int K = 0;
   for (int i = 0; i < n; ++i) {
     if (colors[i] < 1) { err = "coloring must be 1-based positive"; return false; }
@@ -342,7 +344,7 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
   std::sort(perm.begin(), perm.end(), [&](int a, int c) { return key[a] < key[c] || (key[a] == key[c] && a < c); });
   L.rpos.resize(n);
   for (int r = 0; r < n; ++r) L.rpos[perm[r]] = r;
-  // CSC (rows ascending inside a column)
+  // CSC of B (rows ascending inside a column)
   std::vector<long long> cptr(n + 1, 0);
   for (long long e = 0; e < (long long)n * b; ++e) {
     int a = nn[e];
@@ -350,80 +352,6 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
     if (a >= 0) cptr[a + 1]++;
   }
   for (int i = 0; i < n; ++i) cptr[i + 1] += cptr[i];
-  // tiles: contiguous Morton ranges; boundary = a moral neighbour in another tile
-  const int T = std::max(1, std::min(n_tiles, n));
-  L.n_tiles = T;
-  std::vector<int> tile(n);
-  for (int i = 0; i < n; ++i) tile[i] = (int)((long long)L.rpos[i] * T / n);
-  std::vector<long long> crow_ptr(cptr);  // rows of column i: built below (needs crow)
-  std::vector<int> rows_of(cptr[n]);
-  {
-    std::vector<long long> f(cptr.begin(), cptr.end() - 1);
-    for (int k = 0; k < n; ++k)
-      for (int t = 0; t < b; ++t) {
-        int a2 = nn[(size_t)k * b + t];
-        if (a2 >= 0) rows_of[f[a2]++] = k;
-      }
-  }
-  std::vector<char> boundary(n, 0);
-  std::vector<std::vector<int>> nbrs(T);
-  for (int i = 0; i < n; ++i) {
-    for (long long q = cptr[i]; q < cptr[i + 1]; ++q) {
-      int k = rows_of[q];
-      for (int t = 0; t < b; ++t) {
-        int j = nn[(size_t)k * b + t];
-        if (j >= 0 && tile[j] != tile[i]) { boundary[i] = 1; nbrs[tile[i]].push_back(tile[j]); }
-      }
-    }
-  }
-  L.nbr_ptr.assign(T + 1, 0);
-  L.nbr_idx.clear();
-  for (int t = 0; t < T; ++t) {
-    auto& v = nbrs[t];
-    std::sort(v.begin(), v.end());
-    v.erase(std::unique(v.begin(), v.end()), v.end());
-    L.nbr_idx.insert(L.nbr_idx.end(), v.begin(), v.end());
-    L.nbr_ptr[t + 1] = (int)L.nbr_idx.size();
-  }
-  // slots: colour-major; inside a colour by (tile, boundary first, Morton).
-  // Column lengths of a max-min Vecchia factor are very skewed (median ~m,
-  // max ~12m): long columns get more lanes (chunk planner), not a separate
-  // sort, so every chunk stays spatially compact.
-  L.color_slot_ptr.assign(K + 1, 0);
-  for (int i = 0; i < n; ++i) L.color_slot_ptr[colors[i]]++;
-  for (int c = 0; c < K; ++c) L.color_slot_ptr[c + 1] += L.color_slot_ptr[c];
-  for (int c = 0; c < K; ++c) {
-    if (L.color_slot_ptr[c + 1] == L.color_slot_ptr[c]) { err = "coloring has an empty colour class"; return false; }
-  }
-  L.slot_loc.resize(n);
-  L.loc_slot.resize(n);
-  std::vector<int> group_starts;  // slot index where a (colour, tile, class) group starts
-  std::vector<int> group_tile, group_class;
-  {
-    std::vector<int> f(L.color_slot_ptr.begin(), L.color_slot_ptr.end() - 1);
-    for (int r = 0; r < n; ++r) { int i = perm[r]; int s2 = f[colors[i] - 1]++; L.slot_loc[s2] = i; }
-    for (int c = 0; c < K; ++c) {
-      int a0 = L.color_slot_ptr[c], a1 = L.color_slot_ptr[c + 1];
-      // Morton order already implies tile order; sort inside a tile by class then length
-      std::stable_sort(L.slot_loc.begin() + a0, L.slot_loc.begin() + a1, [&](int x, int y) {
-        if (tile[x] != tile[y]) return tile[x] < tile[y];
-        return boundary[x] > boundary[y];  // stable: Morton order inside a class
-      });
-      for (int s2 = a0; s2 < a1;) {
-        int tt = tile[L.slot_loc[s2]], cl = boundary[L.slot_loc[s2]];
-        int e2 = s2;
-        while (e2 < a1 && tile[L.slot_loc[e2]] == tt && boundary[L.slot_loc[e2]] == cl) ++e2;
-        // split large groups spatially?  groups are <= n/(T*K) slots: keep whole
-        group_starts.push_back(s2);
-        group_tile.push_back(tt);
-        group_class.push_back(cl);
-        s2 = e2;
-      }
-    }
-    group_starts.push_back(n);
-    for (int s2 = 0; s2 < n; ++s2) L.loc_slot[L.slot_loc[s2]] = s2;
-  }
-  for (int i = 0; i < n; ++i) L.n_boundary += boundary[i];
   L.nnz = cptr[n];
   std::vector<int> crow(L.nnz), csrc(L.nnz);
   {
@@ -436,100 +364,105 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
         crow[p] = k; csrc[p] = L.rpos[k] * b + t;  // device rows are Morton-ordered
       }
   }
-  L.collen.resize(n);
-  for (int s = 0; s < n; ++s) {
-    int i = L.slot_loc[s];
-    L.collen[s] = (int)(cptr[i + 1] - cptr[i]);
-    L.max_collen = std::max(L.max_collen, L.collen[s]);
+  // per-location lane shape
+  std::vector<unsigned char> lk_of(n), rows_of(n);
+  for (int i = 0; i < n; ++i) {
+    const int len = std::max<long long>(1, cptr[i + 1] - cptr[i]);
+    L.max_collen = std::max(L.max_collen, len);
+    int lk = 0;
+    while ((len + (1 << lk) - 1) >> lk > kRowsMax) ++lk;
+    if ((1 << lk) > LW) {
+      err = "a column of B has " + std::to_string(len) + " entries, more than lanes_per_chain * 16 = " +
+            std::to_string(LW * kRowsMax) + " (use fewer chains per context)";
+      return false;
+    }
+    lk_of[i] = (unsigned char)lk;
+    rows_of[i] = (unsigned char)((len + (1 << lk) - 1) >> lk);
   }
-  // chunks: walk each colour's slots (descending column length); a chunk
-  // starting at a slot of length l uses k = 2^lk lanes per slot with
-  // ceil(l/k) <= kRowsMax and takes up to 64/k slots.
+  // slots: colour-major; inside a colour by rows (descending), Morton order
+  L.color_slot_ptr.assign(K + 1, 0);
+  for (int i = 0; i < n; ++i) L.color_slot_ptr[colors[i]]++;
+  for (int c = 0; c < K; ++c) L.color_slot_ptr[c + 1] += L.color_slot_ptr[c];
+  for (int c = 0; c < K; ++c)
+    if (L.color_slot_ptr[c + 1] == L.color_slot_ptr[c]) { err = "coloring has an empty colour class"; return false; }
+  L.slot_loc.resize(n);
+  L.loc_slot.resize(n);
+  {
+    std::vector<int> f(L.color_slot_ptr.begin(), L.color_slot_ptr.end() - 1);
+    for (int r = 0; r < n; ++r) { int i = perm[r]; L.slot_loc[f[colors[i] - 1]++] = i; }
+    for (int c = 0; c < K; ++c)
+      std::stable_sort(L.slot_loc.begin() + L.color_slot_ptr[c], L.slot_loc.begin() + L.color_slot_ptr[c + 1],
+                       [&](int x, int y) { return rows_of[x] > rows_of[y]; });
+    for (int s2 = 0; s2 < n; ++s2) L.loc_slot[L.slot_loc[s2]] = s2;
+  }
+  L.collen.resize(n);
+  for (int s2 = 0; s2 < n; ++s2) {
+    int i = L.slot_loc[s2];
+    L.collen[s2] = (int)(cptr[i + 1] - cptr[i]);
+  }
+  // chunks
   L.color_chunk_ptr.assign(K + 1, 0);
-  L.chunk_slot0.clear(); L.chunk_len.clear(); L.chunk_nslot.clear(); L.chunk_lk.clear(); L.chunk_off.clear();
+  L.n_class.assign(K, 0);
+  L.class_rows.assign((size_t)K * kMaxClasses, 0);
+  L.class_end.assign((size_t)K * kMaxClasses, 0);
+  L.class_base.assign((size_t)K * kMaxClasses, 0);
   L.lane_tab.clear();
-  if (n >= (1 << 28) - 1) { err = "n too large for the sweep lane table (< 2^28)"; return false; }
+  std::vector<long long> chunk_base;
+  std::vector<int> chunk_rows;
   long long off = 0;
-  (void)crow_ptr;
-  size_t gi = 0;
-  L.tile_chunks.assign((size_t)K * T * 3, -1);
   for (int c = 0; c < K; ++c) {
-    while (group_starts[gi] < L.color_slot_ptr[c + 1]) {
-      int s2 = group_starts[gi], s1 = group_starts[gi + 1];
-      int tt = group_tile[gi], cl = group_class[gi];
-      int* tc = &L.tile_chunks[((size_t)c * T + tt) * 3];
-      int first_chunk = (int)L.chunk_slot0.size();
-      if (cl == 1) tc[0] = first_chunk;          // boundary group comes first
-      else { if (tc[0] < 0) tc[0] = first_chunk; tc[1] = first_chunk; }
-      while (s2 < s1) {
-        // take a Morton-contiguous run of slots whose lane groups fit 64 lanes
+    const int a0 = L.color_slot_ptr[c], a1 = L.color_slot_ptr[c + 1];
+    const int ch_c0 = (int)chunk_base.size();
+    for (int s2 = a0; s2 < a1;) {
+      const int R = rows_of[L.slot_loc[s2]];
+      int e2 = s2;
+      while (e2 < a1 && rows_of[L.slot_loc[e2]] == R) ++e2;
+      const int q = L.n_class[c]++;
+      L.class_rows[(size_t)c * kMaxClasses + q] = R;
+      L.class_base[(size_t)c * kMaxClasses + q] = off;
+      // Morton-contiguous runs whose lane groups fit LW lanes
+      while (s2 < e2) {
         int e3 = s2, lanes = 0;
-        while (e3 < s1) {
-          int l = std::max(1, L.collen[e3]);
-          int lk = 0;
-          while (lk < 6 && (l + (1 << lk) - 1) >> lk > kRowsMax) ++lk;
-          if (lanes + (1 << lk) > 64) break;
-          lanes += 1 << lk;
+        while (e3 < e2) {
+          const int k = 1 << lk_of[L.slot_loc[e3]];
+          if (lanes + k > LW) break;
+          lanes += k;
           ++e3;
         }
-        // inside the chunk: groups by descending size => aligned offsets
         std::vector<int> idx(e3 - s2);
         std::iota(idx.begin(), idx.end(), s2);
-        auto lk_of = [&](int sl) {
-          int l = std::max(1, L.collen[sl]), lk = 0;
-          while (lk < 6 && (l + (1 << lk) - 1) >> lk > kRowsMax) ++lk;
-          return lk;
-        };
-        std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) { return lk_of(x) > lk_of(y); });
-        int rows = 1, maxlk = 0, o = 0;
+        std::stable_sort(idx.begin(), idx.end(),
+                         [&](int x, int y) { return lk_of[L.slot_loc[x]] > lk_of[L.slot_loc[y]]; });
         const size_t lt0 = L.lane_tab.size();
-        L.lane_tab.resize(lt0 + 64, 0);
+        L.lane_tab.resize(lt0 + LW, 0);
+        int o = 0;
         for (int sl : idx) {
-          int lk = lk_of(sl), k = 1 << lk;
-          int l = std::max(1, L.collen[sl]);
-          rows = std::max(rows, (l + k - 1) / k);
-          maxlk = std::max(maxlk, lk);
-          for (int u = 0; u < k; ++u) L.lane_tab[lt0 + o + u] = (sl + 1) | (lk << 28);
-          o += k;
+          const int lk = lk_of[L.slot_loc[sl]];
+          for (int u = 0; u < (1 << lk); ++u) L.lane_tab[lt0 + o + u] = (sl + 1) | (lk << 28);
+          o += 1 << lk;
         }
-        // fixed stride: every chunk spans kRowsMax rows, so an entry's address
-        // depends only on the chunk index (no metadata round trip)
-        L.chunk_slot0.push_back(s2);
-        L.chunk_len.push_back(rows);
-        L.chunk_nslot.push_back(e3 - s2);
-        L.chunk_lk.push_back(maxlk);
-        L.chunk_off.push_back(off);
-        off += (long long)kRowsMax * 64;
+        chunk_base.push_back(off);
+        chunk_rows.push_back(R);
+        off += (long long)LW * R;
         s2 = e3;
       }
-      int end_chunk = (int)L.chunk_slot0.size();
-      if (cl == 1) { tc[1] = end_chunk; tc[2] = end_chunk; }
-      else tc[2] = end_chunk;
-      ++gi;
+      L.class_end[(size_t)c * kMaxClasses + q] = (int)chunk_base.size() - ch_c0;
     }
-    L.color_chunk_ptr[c + 1] = (int)L.chunk_slot0.size();
-    // tiles with no slot of this colour: empty ranges at the colour's end
-    for (int tt = 0; tt < T; ++tt) {
-      int* tc = &L.tile_chunks[((size_t)c * T + tt) * 3];
-      if (tc[0] < 0) tc[0] = tc[1] = tc[2] = L.color_chunk_ptr[c + 1];
-      if (tc[1] < 0) tc[1] = tc[2];
-      if (tc[2] < 0) tc[2] = tc[1];
-    }
+    L.color_chunk_ptr[c + 1] = (int)chunk_base.size();
   }
-  L.nchunks = (int)L.chunk_slot0.size();
-  L.chunk_off.push_back(off);
+  L.nchunks = (int)chunk_base.size();
   L.n_entries = off;
   L.ent_rowpos.assign(off, 0);
   L.ent_src.assign(off, -1);
   for (int ch = 0; ch < L.nchunks; ++ch) {
-    for (int lane = 0; lane < 64; ++lane) {
-      const int v = L.lane_tab[(size_t)ch * 64 + lane];
+    for (int lane = 0; lane < LW; ++lane) {
+      const int v = L.lane_tab[(size_t)ch * LW + lane];
       if (v == 0) continue;
       const int sl = (v & ((1 << 28) - 1)) - 1, lk = v >> 28, k = 1 << lk;
       if ((lane & (k - 1)) != 0) continue;  // first lane of the slot's group
       const int i = L.slot_loc[sl];
       for (long long p = cptr[i], j = 0; p < cptr[i + 1]; ++p, ++j) {
-        long long e = L.chunk_off[ch] + (j >> lk) * 64 + lane + (j & (k - 1));
+        const long long e = chunk_base[ch] + (j >> lk) * LW + lane + (j & (k - 1));
         L.ent_rowpos[e] = L.rpos[crow[p]];
         L.ent_src[e] = csrc[p];
       }

@@ -24,23 +24,27 @@ int greedy_coloring(const int* nn_rowmajor, int n, int b, std::vector<int>& colo
 // bounding box of the first min(d,3) coordinates.
 void morton_keys(const double* locs_colmajor, int n, int d, std::vector<uint64_t>& keys);
 
-// Device layout of the chromatic sweep ("sliced ELL with per-slot lane groups").
-//  - slots: locations re-indexed colour-major; inside a colour grouped by
-//    spatial tile (a Morton range) and boundary/interior class, Morton order
-//    inside a group;
+// Device layout of the chromatic sweep ("sliced ELL with row-count classes").
+//  - slots: locations re-indexed colour-major; inside a colour by row-count
+//    class R (descending), Morton order inside a class;
 //  - r / field / Linv rows: Morton rank of the location (rpos);
-//  - chunks: one wavefront over a Morton-contiguous run of slots of one
-//    group; slot i gets k_i = 2^lk_i lanes (aligned sub-group, k_i lanes
-//    cover ceil(len_i / kRowsMax) <= k_i), so no lane holds more than
-//    kRowsMax entries and the chunk stays spatially compact (its r gathers and
-//    scatters hit a few Morton-contiguous lines);
-//  - lane_tab[ch*64 + lane] = (slot + 1) | lk << 28 (0: idle lane);
-//  - entry j of slot i lives at ch * kRowsMax * 64 + (j / k_i) * 64 + o_i + j % k_i
-//    (o_i = first lane of the slot's group; fixed chunk stride).
-constexpr int kRowsMax = 16;  // entries per lane of a sweep chunk (== kSweepRows)
+//  - slot i (column i of B, len_i entries) gets k_i = 2^lk_i lanes and
+//    R_i = ceil(len_i / k_i) rows, k_i the smallest power of two with
+//    R_i <= kRowsMax (so len <= 16 => k = 1, R = len: no padding);
+//  - chunk: one wavefront's share of ONE chain: LW lanes (LW = 64 / chains
+//    per wave) over a Morton-contiguous run of slots of one (colour, class);
+//    all chunks of a class have R rows, so chunk q of the class starts at
+//    entry base_class + q * LW * R: a closed form of per-colour kernel
+//    arguments (no metadata load in front of the entry loads);
+//  - lane_tab[ch*LW + l] = (slot + 1) | lk << 28 (0: idle lane); lane groups
+//    sorted by descending k inside a chunk => aligned power-of-two groups;
+//  - entry q of slot i lives at chunk_base + (q >> lk) * LW + o_i + (q & (k-1))
+//    (o_i = first lane of the slot's group).
+constexpr int kRowsMax = 16;  // rows per lane of a sweep chunk (== kSweepRows)
+constexpr int kMaxClasses = kRowsMax;
 
 struct SweepLayout {
-  int n = 0, b = 0, K = 0, nchunks = 0;
+  int n = 0, b = 0, K = 0, nchunks = 0, LW = 64;
   long long nnz = 0, n_entries = 0;
   int max_collen = 0;
   std::vector<int> color_slot_ptr;   // K+1
@@ -49,25 +53,21 @@ struct SweepLayout {
   std::vector<int> loc_slot;         // n
   std::vector<int> rpos;             // n: loc -> device row (Morton rank): r, field, Linv rows
   std::vector<int> collen;           // n (slot order)
-  std::vector<int> chunk_slot0;      // nchunks
-  std::vector<int> chunk_len;        // nchunks: rows of the chunk
-  std::vector<int> chunk_nslot;      // nchunks: slots in the chunk
-  std::vector<int> chunk_lk;         // nchunks: log2(max k over the chunk's slots)
-  std::vector<int> lane_tab;         // nchunks x 64
-  std::vector<long long> chunk_off;  // nchunks
-  // spatial tiles for the persistent sweep: tile(loc) = rpos[loc]*T/n
-  int n_tiles = 1;
-  std::vector<int> tile_chunks;      // (K*T) x 3: chunk range [a, m) boundary, [m, e) interior of (colour, tile)
-  std::vector<int> nbr_ptr;          // T+1: CSR of neighbour tiles (moral-graph edges across tiles)
-  std::vector<int> nbr_idx;
-  long long n_boundary = 0;          // slots with a moral neighbour in another tile
+  std::vector<int> lane_tab;         // nchunks x LW
+  // per colour: n_class[c] classes; class q of colour c (index c*kMaxClasses+q):
+  // rows, exclusive chunk end relative to the colour's first chunk, first entry
+  std::vector<int> n_class;          // K
+  std::vector<int> class_rows;       // K * kMaxClasses
+  std::vector<int> class_end;        // K * kMaxClasses
+  std::vector<long long> class_base; // K * kMaxClasses
   std::vector<int> ent_rowpos;       // n_entries (padding: 0)
   std::vector<int> ent_src;          // n_entries (device Linv index rpos[k]*b+j; padding: -1)
 };
 
-// n_tiles: spatial tiles (Morton ranges) for the persistent sweep (>= 1).
+// lanes_per_chain: 64, 32 or 16 (1, 2 or 3-4 chains per wavefront).  Fails if
+// a column of B is longer than lanes_per_chain * kRowsMax.
 bool build_sweep_layout(const int* nn_rowmajor, int n, int b, const int* colors,
-                        const double* locs_colmajor, int d, int n_tiles, SweepLayout& L,
+                        const double* locs_colmajor, int d, int lanes_per_chain, SweepLayout& L,
                         std::string& err);
 
 // Level sets of the Vecchia DAG for the sparse triangular solve:

@@ -9,7 +9,7 @@ constexpr int kWave = 64;
 constexpr int kBlock = 256;
 constexpr int kRedBlocks = 1024;  // max partial blocks of a reduction
 
-// scalars read by the sweep kernels from device memory (graph-replay safe)
+// per-chain scalars read by the sweep kernels from device memory (graph-replay safe)
 struct SweepScalars {
   double inv_s2;     // exp(-log_scale)
   double inv_t2;     // exp(-log_noise_variance)
@@ -20,31 +20,41 @@ struct SweepScalars {
 };
 
 constexpr int kSweepRows = 16;  // == kRowsMax of the layout planner
+constexpr int kMaxChains = 4;
 
-// one wavefront's chunk of the sweep layout, loaded with one 16-byte scalar load
-struct __attribute__((aligned(16))) ChunkMeta {
-  int slot0;       // first slot (a valid slot of the chunk)
-  int packed;      // rows | min(nslot,255) << 8 | max_lk << 16
-  long long off;   // first entry
-};
-// per-slot constants of the sweep, one 32-byte record per slot
-struct __attribute__((aligned(32))) SlotData {
-  double D;        // precision_diag
-  double R;        // residuals_sum
-  int nobs;        // obs_per_loc
+// per-slot constants shared by the chains of a context (16 bytes)
+struct __attribute__((aligned(16))) SlotShared {
   int loc;         // location index (0-based, Vecchia order)
+  int nobs;        // obs_per_loc
   int collen;      // length of column loc of B
   int dpos;        // device row of the location (Morton rank)
 };
 
-struct SweepDev {  // device pointers of the sliced-ELL layout
-  const ChunkMeta* meta;
-  const int* lane_tab;      // nchunks x 64: (slot + 1) | lk << 28, 0 = idle
-  SlotData* slots;
-  const double* ent_val;
-  const int* ent_rowpos;
-  double* w_slot;
-  double* r;
+// per-colour kernel arguments: row-count classes of the colour's chunks
+struct ColorArgs {
+  int chunk0;                      // first chunk of the colour (global index)
+  int nch;                         // chunks of the colour
+  int ncls;                        // classes (<= kSweepRows)
+  int rows[kSweepRows];            // rows of class q
+  int end[kSweepRows];             // exclusive chunk end of class q (relative)
+  long long base[kSweepRows];      // first entry of class q
+};
+
+// device pointers of the sliced-ELL layout; per-chain arrays interleave the
+// chains (index slot*C + chain, row*C + chain) so the chains of one entry share
+// cache lines; ent_val is chain-planar (chain * n_entries + entry).
+struct SweepDev {
+  const int* lane_tab;        // nchunks x LW: (slot + 1) | lk << 28, 0 = idle
+  const SlotShared* slots;    // n
+  double2* dr;                // n x C: {precision_diag, residuals_sum}
+  const double* ent_val;      // C x n_entries
+  const int* ent_rowpos;      // n_entries
+  double* w_slot;             // n x C
+  double* r;                  // n x C, Morton rows
+  const SweepScalars* scal;   // C
+  long long n_entries;
+  int C;                      // chains in the context
+  int LW;                     // lanes per chain (64 / pow2ceil(C))
 };
 
 // coordinate transform into the isotropic unit-range space (per covfun)
@@ -64,29 +74,31 @@ hipError_t launch_factor(hipStream_t st, int family, double var, double nugget, 
 int launch_row_stats(hipStream_t st, const double* linv, const int* nn, int n, int b,
                      const double* x, double shift, double* out,
                      double* partials /* kRedBlocks x 4 */,
-                     const double* shift_dev = nullptr /* overrides shift when set */);
+                     const double* shift_dev = nullptr /* overrides shift when set */,
+                     const double* const* linv_dev = nullptr /* overrides linv when set */,
+                     int out_stride = 1);
 // reduce `nblocks` x 4 partials into res[4] (deterministic order)
 hipError_t launch_reduce4(hipStream_t st, const double* partials, int nblocks, double* res);
 
-hipError_t launch_sell_refresh(hipStream_t st, const SweepDev& L, int nchunks, const int* ent_src,
-                               const double* linv, double* ent_val);
+// chain `chain`, one colour: ent_val[chain] from Linv (device order) and
+// dr[s*C+chain].x = precision_diag
+hipError_t launch_sell_refresh_color(hipStream_t st, const SweepDev& L, const ColorArgs& ca,
+                                     const int* ent_src, const double* linv, int chain);
 
-hipError_t launch_residual_sums(hipStream_t st, int n, SlotData* slots, const int* obs_ptr,
+// dr[s*C+chain].y = residuals_sum of the slot's observations
+hipError_t launch_residual_sums(hipStream_t st, int n, const SweepDev& L, int chain, const int* obs_ptr,
                                 const int* obs_idx, const double* y, const double* mu, double beta0);
 
+// w[s*C+chain] = field[dpos[s]] - beta0 (and back)
 hipError_t launch_field_to_slots(hipStream_t st, int n, const int* slot_dpos, const double* field,
-                                 const SweepScalars* sc, double* w_slot);
+                                 const SweepScalars* sc, double* w_slot, int C, int chain);
 hipError_t launch_slots_to_field(hipStream_t st, int n, const int* slot_dpos, const double* w_slot,
-                                 const SweepScalars* sc, double* field);
+                                 const SweepScalars* sc, double* field, int C, int chain);
 
-hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, int chunk_begin, int nchunks_color,
-                              const SweepScalars* sc, int sweep_local, const double* z, int n);
-
-// all colours of n_sweeps sweeps in one persistent launch (grid = T tiles,
-// T <= #CUs); progress[T] must be zero and *err zero before the launch.
-hipError_t launch_sweep_persistent(hipStream_t st, const SweepDev& L, const int* tile_chunks, int T, int K,
-                                   int n_sweeps, const int* nbr_ptr, const int* nbr_idx, int* progress,
-                                   int* err, const SweepScalars* sc, const double* z, int n);
+// one colour of the chromatic sweep for the chains in chain_mask;
+// z (optional): injected normals z[((sweep*C) + chain) * n + loc]
+hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, const ColorArgs& ca, int chain_mask,
+                              int sweep_local, const double* z, int n);
 
 // obs reductions: mode 0 -> partial[0] += (y - f[loc] - mu + beta0)^2
 //                 mode 1 -> partial[0] += ((y-b)^2 - (y-a)^2) / (2 sd^2),
@@ -99,9 +111,6 @@ hipError_t launch_tri_level(hipStream_t st, const int* rows, int nrows, const do
                             const int* nn, int b, const double* u, double* x);
 hipError_t launch_axpby_shift(hipStream_t st, int n, const double* x, double scale, double shift,
                               double* y);
-
-// x[0..n) = v (a kernel node, replayed with the graph)
-hipError_t launch_fill_int(hipStream_t st, int* x, int n, int v);
 
 // busy-wait on the device for `seconds` (bounded; measurement helper)
 hipError_t launch_spin(hipStream_t st, double seconds);

@@ -409,8 +409,11 @@ __global__ __launch_bounds__(256) void row_stats_kernel(const double* __restrict
                                                         const double* __restrict__ x, double shift,
                                                         double* __restrict__ out,
                                                         double* __restrict__ partials,
-                                                        const double* __restrict__ shift_dev) {
+                                                        const double* __restrict__ shift_dev,
+                                                        const double* const* __restrict__ linv_dev,
+                                                        int out_stride) {
   if (shift_dev) shift = *shift_dev;
+  if (linv_dev) linv = *linv_dev;
   double acc[4] = {0, 0, 0, 0};
   const int g = threadIdx.x & (G - 1);
   const int rows_per_grid = gridDim.x * (blockDim.x / G);
@@ -434,7 +437,7 @@ __global__ __launch_bounds__(256) void row_stats_kernel(const double* __restrict
       acc[1] += u * u;
       acc[2] += a * a;
       acc[3] += a * u;
-      if (out) out[k] = u;
+      if (out) out[(size_t)k * out_stride] = u;
     }
   }
   block_sum4(acc, partials + 4 * blockIdx.x);
@@ -442,17 +445,17 @@ __global__ __launch_bounds__(256) void row_stats_kernel(const double* __restrict
 
 int launch_row_stats(hipStream_t st, const double* linv, const int* nn, int n, int b,
                      const double* x, double shift, double* out, double* partials,
-                     const double* shift_dev) {
+                     const double* shift_dev, const double* const* linv_dev, int out_stride) {
   const int G = b <= 4 ? 4 : b <= 8 ? 8 : b <= 16 ? 16 : 32;
   long long rows_per_block = kBlock / G;
   int g = (int)((n + rows_per_block - 1) / rows_per_block);
   if (g > kRedBlocks) g = kRedBlocks;
   if (g < 1) g = 1;
   switch (G) {
-    case 4: hipLaunchKernelGGL(row_stats_kernel<4>, dim3(g), dim3(kBlock), 0, st, linv, nn, n, b, x, shift, out, partials, shift_dev); break;
-    case 8: hipLaunchKernelGGL(row_stats_kernel<8>, dim3(g), dim3(kBlock), 0, st, linv, nn, n, b, x, shift, out, partials, shift_dev); break;
-    case 16: hipLaunchKernelGGL(row_stats_kernel<16>, dim3(g), dim3(kBlock), 0, st, linv, nn, n, b, x, shift, out, partials, shift_dev); break;
-    default: hipLaunchKernelGGL(row_stats_kernel<32>, dim3(g), dim3(kBlock), 0, st, linv, nn, n, b, x, shift, out, partials, shift_dev); break;
+    case 4: hipLaunchKernelGGL(row_stats_kernel<4>, dim3(g), dim3(kBlock), 0, st, linv, nn, n, b, x, shift, out, partials, shift_dev, linv_dev, out_stride); break;
+    case 8: hipLaunchKernelGGL(row_stats_kernel<8>, dim3(g), dim3(kBlock), 0, st, linv, nn, n, b, x, shift, out, partials, shift_dev, linv_dev, out_stride); break;
+    case 16: hipLaunchKernelGGL(row_stats_kernel<16>, dim3(g), dim3(kBlock), 0, st, linv, nn, n, b, x, shift, out, partials, shift_dev, linv_dev, out_stride); break;
+    default: hipLaunchKernelGGL(row_stats_kernel<32>, dim3(g), dim3(kBlock), 0, st, linv, nn, n, b, x, shift, out, partials, shift_dev, linv_dev, out_stride); break;
   }
   return g;
 }
@@ -472,25 +475,23 @@ hipError_t launch_reduce4(hipStream_t st, const double* partials, int nblocks, d
 }
 
 // ------------------------------------------------------------------ A5
-// lane -> (slot, sub-lane) of a chunk.  Slot groups are aligned power-of-two
-// lane ranges of size k (per slot).  Chunks have a fixed stride of
-// kSweepRows x 64 entries, so the entry loads depend only on the chunk index
-// and issue in the same round trip as the lane-table load.
+// lane -> (chain, slot, sub-lane) of a chunk.  A wavefront holds 64/LW chains
+// of the same chunk (chain = lane / LW); inside a chain's LW lanes, slot groups
+// are aligned power-of-two lane ranges of size k.
 struct ChunkLane {
-  int lk, k, u, s;
+  int lk, k, u, s, l, chain;
   bool valid;
-  long long base;
 };
 __device__ __forceinline__ ChunkLane chunk_lane(const SweepDev& L, int ch, int lane) {
-  ch = __builtin_amdgcn_readfirstlane(ch);
-  const int v = L.lane_tab[(size_t)ch * 64 + lane];
   ChunkLane c;
+  c.chain = lane / L.LW;
+  c.l = lane & (L.LW - 1);
+  const int v = L.lane_tab[(size_t)ch * L.LW + c.l];
   c.valid = v != 0;
   c.lk = c.valid ? (v >> 28) : 0;
   c.k = 1 << c.lk;
-  c.u = lane & (c.k - 1);
+  c.u = c.l & (c.k - 1);
   c.s = c.valid ? (v & 0x0FFFFFFF) - 1 : 0;
-  c.base = (long long)ch * (kSweepRows * 64) + lane;
   return c;
 }
 
@@ -506,272 +507,199 @@ __device__ __forceinline__ double group_sum(double v, int k) {
   return v;
 }
 
-// refresh sweep-layout values of B from Linv and precision_diag per slot
-__global__ __launch_bounds__(256) void sell_refresh_kernel(SweepDev L, int nchunks,
-                                                           const int* __restrict__ ent_src,
-                                                           const double* __restrict__ linv,
-                                                           double* __restrict__ ent_val) {
-  const int ch = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (ch >= nchunks) return;
-  const ChunkLane c = chunk_lane(L, ch, threadIdx.x & 63);
-  // entry loads depend only on the chunk index (padding: src -1 -> linv[0], unused)
-  int src[kSweepRows];
-  double v[kSweepRows];
+// chunk -> (rows, first entry) from the colour's class table (kernel
+// arguments: compile-time indices only, so everything stays in SGPRs)
+__device__ __forceinline__ void chunk_class(const ColorArgs& ca, int lch, int LW, int& rows, long long& base) {
+  rows = ca.rows[0];
+  int start = 0;
+  long long b0 = ca.base[0];
 #pragma unroll
-  for (int j = 0; j < kSweepRows; ++j) src[j] = ent_src[c.base + (long long)j * 64];
-  const int len = c.valid ? L.slots[c.s].collen : 0;
-#pragma unroll
-  for (int j = 0; j < kSweepRows; ++j) v[j] = linv[max(src[j], 0)];
-  double D = 0.0;
-#pragma unroll
-  for (int j = 0; j < kSweepRows; ++j) D += (j * c.k + c.u < len) ? v[j] * v[j] : 0.0;
-#pragma unroll
-  for (int j = 0; j < kSweepRows; ++j)
-    if (j * c.k + c.u < len) ent_val[c.base + (long long)j * 64] = v[j];
-  D = group_sum(D, c.k);
-  if (c.valid && c.u == 0) L.slots[c.s].D = D;
+  for (int q = 1; q < kSweepRows; ++q) {
+    if (q < ca.ncls && lch >= ca.end[q - 1]) {
+      rows = ca.rows[q];
+      start = ca.end[q - 1];
+      b0 = ca.base[q];
+    }
+  }
+  base = b0 + (long long)(lch - start) * LW * rows;
 }
 
-hipError_t launch_sell_refresh(hipStream_t st, const SweepDev& L, int nchunks, const int* ent_src,
-                               const double* linv, double* ent_val) {
-  int g = (nchunks + 3) / 4;
-  hipLaunchKernelGGL(sell_refresh_kernel, dim3(g), dim3(kBlock), 0, st, L, nchunks, ent_src, linv,
-                     ent_val);
+// refresh chain `chain`'s sweep-layout values of B from Linv + precision_diag;
+// one wavefront per chunk (LW lanes used), launched per colour class table
+__global__ __launch_bounds__(256) void sell_refresh_kernel(SweepDev L, ColorArgs ca,
+                                                           const int* __restrict__ ent_src,
+                                                           const double* __restrict__ linv,
+                                                           int chain) {
+  const int lch = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (lch >= ca.nch || lane >= L.LW) return;
+  int R;
+  long long base;
+  chunk_class(ca, lch, L.LW, R, base);
+  ChunkLane c = chunk_lane(L, ca.chunk0 + lch, lane);
+  const int len = c.valid ? L.slots[c.s].collen : 0;
+  double* val = const_cast<double*>(L.ent_val) + (size_t)chain * L.n_entries;
+  double D = 0.0;
+  for (int j = 0; j < R; ++j) {
+    const long long e = base + (long long)j * L.LW + c.l;
+    const int src = ent_src[e];
+    const double v = src >= 0 ? linv[src] : 0.0;
+    if (j * c.k + c.u < len) D += v * v;
+    val[e] = v;
+  }
+  D = group_sum(D, c.k);
+  if (c.valid && c.u == 0) L.dr[(size_t)c.s * L.C + chain].x = D;
+}
+
+hipError_t launch_sell_refresh_color(hipStream_t st, const SweepDev& L, const ColorArgs& ca,
+                                     const int* ent_src, const double* linv, int chain) {
+  const int g = (ca.nch + 3) / 4;
+  if (g > 0) hipLaunchKernelGGL(sell_refresh_kernel, dim3(g), dim3(kBlock), 0, st, L, ca, ent_src, linv, chain);
   return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ A7
-__global__ void residual_sums_kernel(int n, SlotData* __restrict__ slots,
+__global__ void residual_sums_kernel(int n, SweepDev L, int chain,
                                      const int* __restrict__ obs_ptr, const int* __restrict__ obs_idx,
                                      const double* __restrict__ y, const double* __restrict__ mu,
                                      double beta0) {
   int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;
-  int loc = slots[s].loc;
+  int loc = L.slots[s].loc;
   double R = 0.0;
   for (int p = obs_ptr[loc]; p < obs_ptr[loc + 1]; ++p) {
     int o = obs_idx[p];
     R += y[o] - (mu ? mu[o] : beta0);
   }
-  slots[s].R = R;
+  L.dr[(size_t)s * L.C + chain].y = R;
 }
 
-hipError_t launch_residual_sums(hipStream_t st, int n, SlotData* slots, const int* obs_ptr,
+hipError_t launch_residual_sums(hipStream_t st, int n, const SweepDev& L, int chain, const int* obs_ptr,
                                 const int* obs_idx, const double* y, const double* mu, double beta0) {
   int g = (n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(residual_sums_kernel, dim3(g), dim3(kBlock), 0, st, n, slots, obs_ptr, obs_idx,
+  hipLaunchKernelGGL(residual_sums_kernel, dim3(g), dim3(kBlock), 0, st, n, L, chain, obs_ptr, obs_idx,
                      y, mu, beta0);
   return hipGetLastError();
 }
 
 __global__ void field_to_slots_kernel(int n, const int* __restrict__ slot_dpos,
                                       const double* __restrict__ field,
-                                      const SweepScalars* __restrict__ sc, double* __restrict__ w) {
+                                      const SweepScalars* __restrict__ sc, double* __restrict__ w,
+                                      int C) {
   int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < n) w[s] = field[slot_dpos[s]] - sc->beta0;
+  if (s < n) w[(size_t)s * C] = field[slot_dpos[s]] - sc->beta0;
 }
 __global__ void slots_to_field_kernel(int n, const int* __restrict__ slot_dpos,
                                       const double* __restrict__ w,
-                                      const SweepScalars* __restrict__ sc, double* __restrict__ field) {
+                                      const SweepScalars* __restrict__ sc, double* __restrict__ field,
+                                      int C) {
   int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < n) field[slot_dpos[s]] = w[s] + sc->beta0;
+  if (s < n) field[slot_dpos[s]] = w[(size_t)s * C] + sc->beta0;
 }
 
 hipError_t launch_field_to_slots(hipStream_t st, int n, const int* slot_dpos, const double* field,
-                                 const SweepScalars* sc, double* w_slot) {
+                                 const SweepScalars* sc, double* w_slot, int C, int chain) {
   int g = (n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(field_to_slots_kernel, dim3(g), dim3(kBlock), 0, st, n, slot_dpos, field, sc, w_slot);
+  hipLaunchKernelGGL(field_to_slots_kernel, dim3(g), dim3(kBlock), 0, st, n, slot_dpos, field, sc + chain,
+                     w_slot + chain, C);
   return hipGetLastError();
 }
 hipError_t launch_slots_to_field(hipStream_t st, int n, const int* slot_dpos, const double* w_slot,
-                                 const SweepScalars* sc, double* field) {
+                                 const SweepScalars* sc, double* field, int C, int chain) {
   int g = (n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(slots_to_field_kernel, dim3(g), dim3(kBlock), 0, st, n, slot_dpos, w_slot, sc, field);
+  hipLaunchKernelGGL(slots_to_field_kernel, dim3(g), dim3(kBlock), 0, st, n, slot_dpos, w_slot + chain,
+                     sc + chain, field, C);
   return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ A1
-// One colour of the chromatic sweep, local form.  One wavefront per chunk;
-// k lanes per location (k = 1 for typical columns, up to 16 for the long
-// columns of coarse max-min points), so every lane owns <= kSweepRows entries
-// and issues all its loads at once (clamped duplicate loads keep the loads
-// unconditional; the duplicates hit in cache).  Three dependent memory round
-// trips per wave: chunk metadata (scalar) -> entries + slot record + w ->
-// r gathers; then compute and the conflict-free scatter:
+// One colour of the chromatic sweep, local form, for up to 4 chains at once.
+// One wavefront per chunk; the 64/LW chain groups of a wavefront process the
+// same slots for different chains (same entry positions, chain-interleaved r,
+// w and {D, R}, so the chains of one entry share cache lines).  Inside a chain
+// group, k lanes per location (k = 1 for typical columns, up to 16 for the
+// long columns of coarse max-min points), R rows per lane from the colour's
+// class table (kernel arguments), so the entry and lane-table loads depend on
+// nothing but the wavefront index: two dependent memory round trips
+// (entries + lane table -> slot record, w, r gathers), then compute and the
+// conflict-free scatter:
 //   acc  = sum_{k in col(i)} B[k,i] r_k - D_i w_i      (= (B^T B w_{!c})_i)
 //   P    = D_i/s2 + n_i/t2
 //   w_i' = (R_i/t2 - acc/s2)/P + z_i/sqrt(P)
 //   r_k += B[k,i] (w_i' - w_i)
 // Blocks are remapped so that consecutive (spatially adjacent) chunks run on
 // the same XCD and share its L2 for the r gathers.
-// r accessor: plain (per-colour kernels: the launch boundary orders colours)
-// or sc1 write-through relaxed agent-scope atomics (persistent kernel: r is
-// handed between workgroups inside one launch, MI355X_MICROARCH.md "Valid
-// forms", first table row: every store and every load of r is sc1).
-template <bool SC1>
-__device__ __forceinline__ double r_load(const double* r, int p) {
-  if (SC1) {
-    unsigned long long v = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(r) + p,
-                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return __longlong_as_double((long long)v);
-  }
-  return r[p];
-}
-template <bool SC1>
-__device__ __forceinline__ void r_store(double* r, int p, double v) {
-  if (SC1)
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(r) + p,
-                       (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  else
-    r[p] = v;
-}
-
-// one chunk of one colour (the body shared by both sweep kernels)
-template <bool INJECT, bool SC1>
-__device__ __forceinline__ void sweep_chunk(const SweepDev& L, int ch, int lane,
-                                            const SweepScalars* __restrict__ scal, int sweep_local,
-                                            const double* __restrict__ z, int n) {
-  const ChunkLane c = chunk_lane(L, ch, lane);
-  double* r = L.r;  // gathered then scattered: no __restrict__
-  // round trip 1: entries (address from the chunk index only) + lane table;
-  // round trip 2: slot record, w and the r gathers
-  double v[kSweepRows], rv[kSweepRows];
-  int p[kSweepRows];
-#pragma unroll
-  for (int j = 0; j < kSweepRows; ++j) {
-    const long long e = c.base + (long long)j * 64;
-    v[j] = L.ent_val[e];
-    p[j] = L.ent_rowpos[e];
-  }
-  const SlotData sd = L.slots[c.s];
-  const double w = L.w_slot[c.s];
-  const int len = c.valid ? sd.collen : 0;
-  const double inv_s2 = scal->inv_s2, inv_t2 = scal->inv_t2;
-  double zz;
-  if (INJECT) zz = z[(size_t)sweep_local * n + sd.loc];
-  else zz = normal_at(scal->seed, scal->counter_base + (uint64_t)sweep_local, (uint32_t)sd.loc);
-#pragma unroll
-  for (int j = 0; j < kSweepRows; ++j) rv[j] = r_load<SC1>(r, p[j]);
-  double acc = 0.0;
-#pragma unroll
-  for (int j = 0; j < kSweepRows; ++j) acc += (j * c.k + c.u < len) ? v[j] * rv[j] : 0.0;
-  acc = group_sum(acc, c.k);
-  if (!c.valid) return;
-  acc -= sd.D * w;
-  const double P = sd.D * inv_s2 + (double)sd.nobs * inv_t2;
-  const double wn = (inv_t2 * sd.R - inv_s2 * acc) / P + zz / sqrt(P);
-  const double dw = wn - w;
-  if (c.u == 0) L.w_slot[c.s] = wn;
-#pragma unroll
-  for (int j = 0; j < kSweepRows; ++j)
-    if (j * c.k + c.u < len) r_store<SC1>(r, p[j], rv[j] + v[j] * dw);
-}
-
 template <bool INJECT>
-__global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, int chunk_begin, int nchunks_color,
-                                                          const SweepScalars* __restrict__ scal,
+__global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, ColorArgs ca, int chain_mask,
                                                           int sweep_local, const double* __restrict__ z,
                                                           int n) {
   const int nb = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q = nb >> 3, rm = nb & 7;
   const int lb = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + (bid >> 3);
   const int lch = lb * 4 + (threadIdx.x >> 6);
-  if (lch >= nchunks_color) return;
-  sweep_chunk<INJECT, false>(L, chunk_begin + lch, threadIdx.x & 63, scal, sweep_local, z, n);
-}
-
-// ------------------------------------------------------------------ A1, persistent
-// All colours of n_sweeps sweeps in ONE launch.  One workgroup (4 waves) per
-// spatial tile (a Morton range of locations), one workgroup per CU (the
-// dynamic LDS request admits only one).  Step p = s*K + c + 1 of tile t:
-//   1. wave 0 polls progress[u] >= p-1 for every neighbour tile u (tiles with a
-//      moral-graph edge to t) -- relaxed sc1 loads, bounded spin;
-//   2. barrier; the tile's BOUNDARY chunks of colour c (slots with a moral
-//      neighbour in another tile) are updated, r accessed with sc1 loads/stores;
-//   3. every wave drains its stores (vmcnt(0)); barrier; one lane publishes
-//      progress[t] = p (relaxed sc1 store);
-//   4. the tile's INTERIOR chunks of colour c (rows touched only by this tile)
-//      are updated while the neighbours proceed.
-// Exactly the reference's colour order: a boundary slot of colour c reads
-// rows whose other members belong to neighbour tiles' boundary slots, which
-// have all finished colours < c of this sweep (and not started colours > c:
-// those wait for this tile).  Progress is monotone and the minimum-progress
-// tile never waits, so the protocol cannot deadlock once all workgroups are
-// resident (grid <= CUs).  A spin that exceeds ~4 s sets *err and gives up.
-template <bool INJECT>
-__global__ __launch_bounds__(256) void sweep_persistent_kernel(SweepDev L, const int* __restrict__ tile_chunks,
-                                                               int T, int K, int n_sweeps,
-                                                               const int* __restrict__ nbr_ptr,
-                                                               const int* __restrict__ nbr_idx,
-                                                               int* __restrict__ progress,
-                                                               int* __restrict__ err,
-                                                               const SweepScalars* __restrict__ scal,
-                                                               const double* __restrict__ z, int n) {
-  // XCD-aware tile choice: blocks b, b+8, ... share an XCD, so give them
-  // Morton-consecutive tiles (most hand-offs then stay inside one XCD's L2)
-  const int nb = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q = nb >> 3, rm = nb & 7;
-  const int t = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + (bid >> 3);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (lch >= ca.nch) return;
   const int lane = threadIdx.x & 63;
-  const int nb0 = nbr_ptr[t], nb1 = nbr_ptr[t + 1];
-  __shared__ int s_fail;
-  if (threadIdx.x == 0) s_fail = 0;
-  __syncthreads();
-  for (int s = 0; s < n_sweeps; ++s) {
-    for (int c = 0; c < K; ++c) {
-      const int pstep = s * K + c + 1;
-      const int* tc = tile_chunks + ((size_t)c * T + t) * 3;
-      const int a = tc[0], m = tc[1], e = tc[2];
-      if (wave == 0 && pstep > 1 && nb1 > nb0) {
-        const unsigned long long t0 = wall_clock64();
-        for (;;) {
-          bool ok = true;
-          for (int i = nb0 + lane; i < nb1; i += 64)
-            ok &= __hip_atomic_load(progress + nbr_idx[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= pstep - 1;
-          if (__all(ok)) break;
-          if (wall_clock64() - t0 > 400000000ull) {  // ~4 s at 100 MHz
-            if (lane == 0) { atomicMax(err, 1 + t); s_fail = 1; }
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-      __syncthreads();
-      if (s_fail) return;
-      for (int ch = a + wave; ch < m; ch += 4) sweep_chunk<INJECT, true>(L, ch, lane, scal, s, z, n);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0) __hip_atomic_store(progress + t, pstep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int ch = m + wave; ch < e; ch += 4) sweep_chunk<INJECT, true>(L, ch, lane, scal, s, z, n);
+  const int chain = lane / L.LW;
+  if (chain >= L.C || !((chain_mask >> chain) & 1)) return;
+  int R;
+  long long base;
+  chunk_class(ca, lch, L.LW, R, base);
+  const ChunkLane c = chunk_lane(L, ca.chunk0 + lch, lane);
+  const int C = L.C;
+  double* r = L.r;  // gathered then scattered: no __restrict__
+  const double* val = L.ent_val + (size_t)chain * L.n_entries;
+  // round trip 1: entries (address from the wavefront index only) + lane table
+  double v[kSweepRows], rv[kSweepRows];
+  int p[kSweepRows];
+#pragma unroll
+  for (int j = 0; j < kSweepRows; ++j) {
+    if (j < R) {
+      const long long e = base + (long long)j * L.LW + c.l;
+      v[j] = val[e];
+      p[j] = L.ent_rowpos[e];
+    } else {
+      v[j] = 0.0;
+      p[j] = 0;
     }
   }
+  // round trip 2: slot record, w, {D, R}, scalars, r gathers
+  const SlotShared sh = L.slots[c.s];
+  const size_t sc_idx = (size_t)c.s * C + chain;
+  const double w = L.w_slot[sc_idx];
+  const double2 dr = L.dr[sc_idx];
+  const SweepScalars* scal = L.scal + chain;
+  const double inv_s2 = scal->inv_s2, inv_t2 = scal->inv_t2;
+  double zz;
+  if (INJECT) zz = z[((size_t)sweep_local * C + chain) * n + sh.loc];
+  else zz = normal_at(scal->seed, scal->counter_base + (uint64_t)sweep_local, (uint32_t)sh.loc);
+#pragma unroll
+  for (int j = 0; j < kSweepRows; ++j) rv[j] = (j < R) ? r[(size_t)p[j] * C + chain] : 0.0;
+  const int len = c.valid ? sh.collen : 0;
+  double acc = 0.0;
+#pragma unroll
+  for (int j = 0; j < kSweepRows; ++j) acc += (j * c.k + c.u < len) ? v[j] * rv[j] : 0.0;
+  acc = group_sum(acc, c.k);
+  if (!c.valid) return;
+  acc -= dr.x * w;
+  const double P = dr.x * inv_s2 + (double)sh.nobs * inv_t2;
+  const double wn = (inv_t2 * dr.y - inv_s2 * acc) / P + zz / sqrt(P);
+  const double dw = wn - w;
+  if (c.u == 0) L.w_slot[sc_idx] = wn;
+#pragma unroll
+  for (int j = 0; j < kSweepRows; ++j)
+    if (j * c.k + c.u < len) r[(size_t)p[j] * C + chain] = rv[j] + v[j] * dw;
 }
 
-hipError_t launch_sweep_persistent(hipStream_t st, const SweepDev& L, const int* tile_chunks, int T, int K,
-                                   int n_sweeps, const int* nbr_ptr, const int* nbr_idx, int* progress,
-                                   int* err, const SweepScalars* sc, const double* z, int n) {
-  // 96 KiB of dynamic LDS: only one workgroup fits per CU (160 KiB)
-  const size_t lds = 96 * 1024;
+hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, const ColorArgs& ca, int chain_mask,
+                              int sweep_local, const double* z, int n) {
+  const int g = (ca.nch + 3) / 4;
+  if (g == 0) return hipSuccess;
   if (z)
-    hipLaunchKernelGGL((sweep_persistent_kernel<true>), dim3(T), dim3(kBlock), lds, st, L, tile_chunks, T, K,
-                       n_sweeps, nbr_ptr, nbr_idx, progress, err, sc, z, n);
+    hipLaunchKernelGGL((sweep_color_kernel<true>), dim3(g), dim3(kBlock), 0, st, L, ca, chain_mask,
+                       sweep_local, z, n);
   else
-    hipLaunchKernelGGL((sweep_persistent_kernel<false>), dim3(T), dim3(kBlock), lds, st, L, tile_chunks, T, K,
-                       n_sweeps, nbr_ptr, nbr_idx, progress, err, sc, z, n);
-  return hipGetLastError();
-}
-
-hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, int chunk_begin, int nchunks_color,
-                              const SweepScalars* sc, int sweep_local, const double* z, int n) {
-  int g = (nchunks_color + 3) / 4;
-  if (z)
-    hipLaunchKernelGGL((sweep_color_kernel<true>), dim3(g), dim3(kBlock), 0, st, L, chunk_begin,
-                       nchunks_color, sc, sweep_local, z, n);
-  else
-    hipLaunchKernelGGL((sweep_color_kernel<false>), dim3(g), dim3(kBlock), 0, st, L, chunk_begin,
-                       nchunks_color, sc, sweep_local, z, n);
+    hipLaunchKernelGGL((sweep_color_kernel<false>), dim3(g), dim3(kBlock), 0, st, L, ca, chain_mask,
+                       sweep_local, z, n);
   return hipGetLastError();
 }
 
@@ -843,15 +771,6 @@ hipError_t launch_axpby_shift(hipStream_t st, int n, const double* x, double sca
                               double* y) {
   int g = (n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(axpby_shift_kernel, dim3(g), dim3(kBlock), 0, st, n, x, scale, shift, y);
-  return hipGetLastError();
-}
-
-__global__ void fill_int_kernel(int* __restrict__ x, int n, int v) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) x[i] = v;
-}
-
-hipError_t launch_fill_int(hipStream_t st, int* x, int n, int v) {
-  hipLaunchKernelGGL(fill_int_kernel, dim3(1), dim3(256), 0, st, x, n, v);
   return hipGetLastError();
 }
 

@@ -12,7 +12,7 @@ import time
 
 import numpy as np
 
-from .context import ChainContext
+from .context import make_chain_views
 from .graph import find_ordered_nn, naive_greedy_coloring, order_maxmin, sparse_chol_indices
 from .model import covparms, shape_params_of
 
@@ -161,7 +161,7 @@ def mcmc_nngp_initialize(observed_locs, observed_field, X_obs=None, X_locs=None,
 
     if devices is None:
         devices = [-1]
-    contexts = []
+    contexts = make_chain_views(locs, NNarray, va["coloring"], locs_match, observed_field, n_chains, devices)
     states = {}
     for i in range(n_chains):
         st = {"params": {}, "transition_kernels": {}}
@@ -188,13 +188,11 @@ def mcmc_nngp_initialize(observed_locs, observed_field, X_obs=None, X_locs=None,
         st["params"]["beta"] = (coef[1:] + perturb[1:]) if Xd is not None else None
         st["params"]["log_scale"] = float(np.log(rng.beta(10, 10) * var_resid))
         st["params"]["log_noise_variance"] = float(np.log(rng.beta(10, 10) * var_resid))
-        ctx = ChainContext(locs, NNarray, va["coloring"], locs_match, observed_field,
-                           device=devices[i % len(devices)])
+        ctx = contexts[i]
         ctx.factor(0, stationary_covfun, covparms(sp_names, st["params"]["shape"], 0.4, 0.7))
         w = ctx.tri_solve(0, rng.normal(size=n))
         st["params"]["field"] = st["params"]["beta_0"] + np.sqrt(np.exp(st["params"]["log_scale"])) * w
         states[f"chain_{i + 1}"] = st
-        contexts.append(ctx)
 
     records = {f"chain_{i + 1}": {"iterations": np.array([[0.0, time.time() - t_begin]]), "params": {}}
                for i in range(n_chains)}

@@ -21,8 +21,13 @@ sum_squared_residuals :281             ctx.sum_squared_residuals
 sparse_chol %*% X :79,82,147,241       ctx.spmv
 =====================================  =====================================
 
-Chains are contexts (one per chain, possibly on distinct devices) instead of
-forked ``mclapply`` workers: HIP must never be initialised before a fork.
+Chains live in device contexts (up to 4 chains per context, contexts possibly
+on distinct devices) instead of forked ``mclapply`` workers: HIP must never
+be initialised before a fork.  Each chain's iteration is a generator that
+yields at its chromatic sweep; the driver advances all chains in lockstep and
+sweeps the chains of one context in the same kernels (``sweep_chains``).
+Chains are independent (own RNG streams, own device state), so the lockstep
+order gives exactly the results of running the chains one after another.
 Seeds: numpy PCG64 seeded with ``iter_start + i`` (the reference's
 ``set.seed(iter_start + i)``, :34-36); the chromatic sweep's normals come from
 the device Philox stream keyed by the same value, so a resumed run is
@@ -32,7 +37,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .context import ChainContext
+from .context import ChainContext, make_chain_views
 from .model import covparms
 
 
@@ -55,8 +60,11 @@ def _interweave_prep(ctx, X, va):
     return {"Xl": Xl, "SX": SX, "covmat": cov, "covmat_chol": np.linalg.cholesky(cov).T}
 
 
-def _run_chain(i, state, ctx, X, observed_field, space_time_model, va, n_iterations_update,
-               field_thinning, ancillary, n_chromatic, iter_start, seed):
+def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_iterations_update,
+                   field_thinning, ancillary, n_chromatic, iter_start, seed):
+    """Chain i's n_iterations_update Gibbs iterations; yields its sweep
+    requests (n_sweeps, beta_0, log_scale, log_noise_variance, key, counter)
+    and returns {"state", "records", "acceptance"}."""
     rng = np.random.default_rng(int(iter_start) + i + 1)
     key = _philox_key(iter_start, i + 1, seed)
     covfun = space_time_model["covfun"]["stationary_covfun"]
@@ -177,8 +185,8 @@ def _run_chain(i, state, ctx, X, observed_field, space_time_model, va, n_iterati
         ctx.set_mu(mu_of(), params["beta_0"])
 
         # ---- chromatic sampling of the field (:257-275)
-        ctx.sweep(n_chromatic, params["beta_0"], params["log_scale"], params["log_noise_variance"],
-                  key, (int(iter_start) + it - 1) * n_chromatic)
+        yield (n_chromatic, params["beta_0"], params["log_scale"], params["log_noise_variance"],
+               key, (int(iter_start) + it - 1) * n_chromatic)
 
         # ---- noise variance (:281-293)
         ssr = ctx.sum_squared_residuals(params["beta_0"])
@@ -205,6 +213,55 @@ def _run_chain(i, state, ctx, X, observed_field, space_time_model, va, n_iterati
                            "covariance_acceptance_ancillary": acc_anc}}
 
 
+def _run_chain(i, state, ctx, X, observed_field, space_time_model, va, n_iterations_update,
+               field_thinning, ancillary, n_chromatic, iter_start, seed):
+    """One chain alone (each sweep through ctx.sweep)."""
+    prog = _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_iterations_update,
+                          field_thinning, ancillary, n_chromatic, iter_start, seed)
+    try:
+        req = next(prog)
+        while True:
+            ctx.sweep(*req)
+            req = next(prog)
+    except StopIteration as stop:
+        return stop.value
+
+
+def _drive(programs, contexts):
+    """Advance chain programs in lockstep; the sweeps of all chains of one
+    ChainContext go through one sweep_chains call."""
+    results = [None] * len(programs)
+    reqs = {}
+    for i, g in enumerate(programs):
+        try:
+            reqs[i] = next(g)
+        except StopIteration as stop:
+            results[i] = stop.value
+    while reqs:
+        groups = {}
+        for i in reqs:
+            owner = getattr(contexts[i], "ctx", None)
+            groups.setdefault(id(owner) if owner is not None else ("solo", i), []).append(i)
+        for ids in groups.values():
+            owner = getattr(contexts[ids[0]], "ctx", None)
+            same_n = len({reqs[i][0] for i in ids}) == 1
+            if owner is not None and len(ids) == owner.n_chains and same_n and owner.n_chains > 1:
+                order = sorted(ids, key=lambda i: contexts[i].chain)
+                cols = list(zip(*[reqs[i] for i in order]))
+                owner.sweep_chains(cols[0][0], cols[1], cols[2], cols[3], cols[4], cols[5])
+            else:
+                for i in ids:
+                    contexts[i].sweep(*reqs[i])
+        nxt = {}
+        for i in reqs:
+            try:
+                nxt[i] = programs[i].send(None)
+            except StopIteration as stop:
+                results[i] = stop.value
+        reqs = nxt
+    return results
+
+
 def mcmc_nngp_update_Gaussian(locs, X, observed_field, space_time_model, vecchia_approx, states,
                               n_iterations_update, n_cores=None, field_thinning=1.0, ancillary=True,
                               n_chromatic=10, iterations=None, contexts=None, seed=1, devices=None):
@@ -213,13 +270,11 @@ def mcmc_nngp_update_Gaussian(locs, X, observed_field, space_time_model, vecchia
     names = list(states.keys()) if isinstance(states, dict) else [f"chain_{i + 1}" for i in range(len(states))]
     st_list = list(states.values()) if isinstance(states, dict) else list(states)
     if contexts is None:
-        devices = devices or [-1]
-        contexts = [ChainContext(locs, vecchia_approx["NNarray"], vecchia_approx["coloring"],
-                                 vecchia_approx["locs_match"], observed_field, device=devices[i % len(devices)])
-                    for i in range(len(st_list))]
-    out = {}
-    for i, (nm, st) in enumerate(zip(names, st_list)):
-        out[nm] = _run_chain(i, st, contexts[i], X, np.asarray(observed_field, np.float64), space_time_model,
-                             vecchia_approx, int(n_iterations_update), float(field_thinning), bool(ancillary),
-                             int(n_chromatic), iter_start, seed)
-    return out
+        contexts = make_chain_views(locs, vecchia_approx["NNarray"], vecchia_approx["coloring"],
+                                    vecchia_approx["locs_match"], observed_field, len(st_list), devices)
+    y = np.asarray(observed_field, np.float64)
+    programs = [_chain_program(i, st, contexts[i], X, y, space_time_model, vecchia_approx,
+                               int(n_iterations_update), float(field_thinning), bool(ancillary),
+                               int(n_chromatic), iter_start, seed)
+                for i, st in enumerate(st_list)]
+    return dict(zip(names, _drive(programs, contexts)))

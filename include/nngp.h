@@ -10,8 +10,11 @@
  * caller-allocated.  Device state is owned by the context and freed only by
  * nngp_ctx_destroy.  Calls on one context are serialised by the caller;
  * distinct contexts may live on distinct devices.  HIP is initialised lazily
- * by nngp_ctx_create: never fork() after it (replaces parallel::mclapply,
- * Scripts/mcmc_nngp_update_Gaussian.R:25, by one context per chain).
+ * by nngp_ctx_create: never fork() after it.  A context holds 1..4 MCMC chains
+ * over the same locations / NNarray / colouring (replaces the per-chain
+ * workers of parallel::mclapply, Scripts/mcmc_nngp_update_Gaussian.R:25-26):
+ * per-chain entry points act on the chain chosen by nngp_set_chain, and
+ * nngp_sweep_chains sweeps all chains of the context in the same kernels.
  *
  * Reference interface each entry point replaces (path:line under the
  * reference tree):
@@ -26,6 +29,8 @@
  *                              Scripts/mcmc_nngp_update_Gaussian.R:8-12,184-186
  *   nngp_set_mu .............. mu + residuals_sum, update_Gaussian.R:85-90,249-250,260
  *   nngp_sweep ............... chromatic sampling, update_Gaussian.R:257-275
+ *   nngp_sweep_chains ........ the same for every chain (mclapply over chains,
+ *                              update_Gaussian.R:25-26, around :257-275)
  *   nngp_ancillary_propose ... new_field, update_Gaussian.R:127 (SpMV + sparse
  *                              triangular solve)
  *   nngp_field_response_ratio  dnorm ratio, update_Gaussian.R:129-131
@@ -44,7 +49,7 @@
 extern "C" {
 #endif
 
-#define NNGP_ABI_VERSION 1
+#define NNGP_ABI_VERSION 2
 
 typedef enum {
   NNGP_OK = 0,
@@ -83,9 +88,9 @@ typedef struct {
   long long n_entries; /* sliced-ELL entries incl. padding */
   int max_collen;  /* longest column of B */
   int device;      /* HIP device ordinal */
-  int n_tiles;     /* spatial tiles of the persistent sweep */
-  long long n_boundary; /* locations with a moral neighbour in another tile */
-  int sweep_mode;  /* 1 persistent dataflow kernel, 0 one kernel per colour */
+  int n_chains;    /* chains held by the context */
+  int lanes_per_chain; /* sweep lanes of one chain in a wavefront (64/32/16) */
+  int n_chunks;    /* sweep chunks (wavefront tasks per chain and sweep) */
 } nngp_info;
 
 /* ---------- library ---------- */
@@ -104,11 +109,14 @@ int nngp_greedy_coloring(const int* NNarray, int n, int b, int* coloring, int* n
 /* ---------- device context ---------- */
 /* locs n x d col-major (ordered); NNarray n x b col-major 1-based (NA=INT_MIN);
  * coloring 1-based (length n); locs_match 1-based (length n_obs);
- * observed_field length n_obs.  device: HIP ordinal (-1: current). */
+ * observed_field length n_obs; n_chains 1..4 (chain 0 selected).
+ * device: HIP ordinal (-1: current). */
 int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
                     const int* coloring, const int* locs_match,
-                    const double* observed_field, int n_obs, int device,
+                    const double* observed_field, int n_obs, int n_chains, int device,
                     nngp_ctx** out);
+/* select the chain (0-based) the per-chain entry points below act on */
+int nngp_set_chain(nngp_ctx* ctx, int chain);
 void nngp_ctx_destroy(nngp_ctx* ctx);
 const char* nngp_ctx_last_error(const nngp_ctx* ctx);
 int nngp_ctx_info(const nngp_ctx* ctx, nngp_info* info);
@@ -141,6 +149,13 @@ int nngp_sweep(nngp_ctx* ctx, int n_sweeps, double beta0, double log_scale,
                double log_noise_variance, uint64_t seed, uint64_t counter_base,
                const double* z);
 
+/* n_sweeps sweeps of EVERY chain of the context in the same kernels; arrays
+ * of length n_chains.  Chain k's result is bitwise identical to nngp_sweep on
+ * chain k alone with the same arguments. */
+int nngp_sweep_chains(nngp_ctx* ctx, int n_sweeps, const double* beta0, const double* log_scale,
+                      const double* log_noise_variance, const uint64_t* seed,
+                      const uint64_t* counter_base);
+
 /* Ancillary proposal: proposal field = beta0 + exp(0.5*dlog_scale) *
  * B_prop^{-1} (B_cur (field - beta0)) (update_Gaussian.R:127). */
 int nngp_ancillary_propose(nngp_ctx* ctx, double beta0, double dlog_scale);
@@ -159,12 +174,12 @@ int nngp_spmv(nngp_ctx* ctx, int which, const double* X, int ncols, double* Y);
 int nngp_tri_solve(nngp_ctx* ctx, int which, const double* u, double* x);
 
 /* ---------- measurement ---------- */
-/* Runs n_sweeps sweeps on the context's stream bracketed by HIP events;
+/* nngp_sweep_chains bracketed by HIP events on the context's stream;
  * *ms = elapsed; per-colour-kernel durations are summed into *kernel_ms when
  * kernel_ms != NULL (each colour launch bracketed by its own events). */
-int nngp_sweep_timed(nngp_ctx* ctx, int n_sweeps, double beta0, double log_scale,
-                     double log_noise_variance, uint64_t seed, uint64_t counter_base,
-                     double* ms, double* kernel_ms);
+int nngp_sweep_timed(nngp_ctx* ctx, int n_sweeps, const double* beta0, const double* log_scale,
+                     const double* log_noise_variance, const uint64_t* seed,
+                     const uint64_t* counter_base, double* ms, double* kernel_ms);
 /* Philox normals generated by the device code path (test hook). */
 int nngp_device_normals(int device, uint64_t seed, uint64_t sweep, int n, double* z);
 

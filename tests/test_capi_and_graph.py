@@ -20,7 +20,7 @@ def test_header_symbols_exported(P):
     lib = C.CDLL(str(_lib.LIB_PATH))
     for s in sorted(declared):
         assert hasattr(lib, s), s
-    assert P.lib.nngp_abi_version() == 1
+    assert P.lib.nngp_abi_version() == 2
 
 
 def test_library_has_gfx950_code_object():
@@ -116,3 +116,18 @@ def test_gelman_rubin_on_identical_chains(P):
     assert np.all(g["R_hat"] < 1.05)
     E, _ = P.ESS(recs, 0.5)
     assert np.all(E[:-1] > 100)
+
+
+@pytest.mark.parametrize("n,m,lw,seed", [(3000, 10, 64, 1), (5000, 15, 32, 2), (8000, 15, 16, 3),
+                                         (2000, 30, 16, 4), (50, 3, 64, 5), (1, 0, 64, 6)])
+def test_sweep_layout_invariants(tmp_path, n, m, lw, seed):
+    """C++ check of the planner: every nonzero of B exactly once, at the
+    address the sweep kernel computes from the colour class table."""
+    import subprocess
+
+    csrc = next(ROOT.glob("*_amd")) / "csrc"
+    exe = tmp_path / "layout_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", str(csrc), str(ROOT / "tests/cpp/layout_check.cpp"),
+                    str(csrc / "graph_prep.cpp"), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe), str(n), str(m), str(lw), str(seed)], capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr

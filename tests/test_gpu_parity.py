@@ -312,29 +312,63 @@ def test_size_independent_properties_large(P, O):
     assert info["nnz"] == n * (m + 1) - m * (m + 1) // 2
 
 
-@pytest.mark.parametrize("n,m", [(3000, 10), (60000, 15)])
-def test_persistent_sweep_bitwise_equals_per_colour_launches(P, O, n, m, monkeypatch):
-    """The persistent dataflow kernel (tiles + neighbour progress counters)
-    must read exactly the values the colour-by-colour launches read: results
-    are bitwise identical, and both match the oracle."""
-    locs, NN, col, lm, y = make_problem(P, n, m, seed=n)
-    cp = COVS["matern15_isotropic"]
-    field = np.random.default_rng(5).normal(size=n)
-    out = {}
-    for mode in ["launch", "persistent"]:
-        monkeypatch.setenv("NNGP_SWEEP", mode)
-        with _ctx(P, locs, NN, col, lm, y) as ctx:
-            info = ctx.info
-            assert info["sweep_mode"] == (1 if mode == "persistent" else 0)
-            ctx.factor(0, "matern15_isotropic", cp)
-            ctx.set_field(field)
-            ctx.set_mu(None, 0.2)
-            ctx.sweep(4, 0.2, 0.1, -0.3, 99, 7)
-            out[mode] = ctx.get_field()
-            Lo = ctx.get_linv(0)
-    assert info["n_tiles"] == max(1, min(256, n // 1024))
-    np.testing.assert_array_equal(out["persistent"], out["launch"])
-    z = O.sweep_normals(99, 7, 4, n)
-    ref = O.sweep("local", field, Lo, NN, col, O.precision_diag(Lo, NN), np.ones(n, np.int32), y,
-                  np.full(n, 0.2), lm, 0.2, 0.1, -0.3, z)
-    np.testing.assert_allclose(out["persistent"], ref, rtol=1e-7, atol=1e-8)
+@pytest.mark.parametrize("n,m,C", [(3000, 10, 2), (3000, 10, 3), (60000, 15, 4), (60000, 15, 3)])
+def test_batched_chains_bitwise_equal_single_chain_contexts(P, O, n, m, C):
+    """nngp_sweep_chains on a C-chain context (chains share the wavefronts)
+    gives, for every chain, exactly the bits of a 1-chain context swept alone
+    with the same arguments; and chain 0 matches the oracle."""
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=n + C)
+    rng = np.random.default_rng(C)
+    cps = [[1.0 + 0.2 * k, 0.05 + 0.01 * k, 0.1 * k] for k in range(C)]
+    fields = [rng.normal(size=n) for _ in range(C)]
+    b0 = [0.2 * k for k in range(C)]
+    ls = [0.1 - 0.05 * k for k in range(C)]
+    lnv = [-0.3 + 0.1 * k for k in range(C)]
+    seeds = [99 + k for k in range(C)]
+    bases = [7 + 3 * k for k in range(C)]
+    with P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=C) as ctx:
+        info = ctx.info
+        assert info["n_chains"] == C and info["lanes_per_chain"] == {2: 32, 3: 16, 4: 16}[C]
+        for k in range(C):
+            ctx.select(k)
+            ctx.factor(0, "matern15_isotropic", cps[k])
+            ctx.set_field(fields[k])
+            ctx.set_mu(None, b0[k])
+        ctx.sweep_chains(4, b0, ls, lnv, seeds, bases)
+        got = [ctx.select(k).get_field() for k in range(C)]
+        Lo0 = ctx.select(0).get_linv(0)
+    for k in range(C):
+        with _ctx(P, locs, NN, col, lm, y) as one:
+            one.factor(0, "matern15_isotropic", cps[k])
+            one.set_field(fields[k])
+            one.set_mu(None, b0[k])
+            one.sweep(4, b0[k], ls[k], lnv[k], seeds[k], bases[k])
+            np.testing.assert_array_equal(got[k], one.get_field())
+    z = O.sweep_normals(seeds[0], bases[0], 4, n)
+    ref = O.sweep("local", fields[0], Lo0, NN, col, O.precision_diag(Lo0, NN), np.ones(n, np.int32), y,
+                  np.full(n, b0[0]), lm, b0[0], ls[0], lnv[0], z)
+    np.testing.assert_allclose(got[0], ref, rtol=1e-7, atol=1e-8)
+
+
+def test_single_chain_sweep_inside_batched_context(P, O):
+    """nngp_sweep on one chain of a 3-chain context leaves the other chains
+    untouched and equals the oracle (injected normals)."""
+    n, m = 4000, 8
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=3)
+    rng = np.random.default_rng(8)
+    fields = [rng.normal(size=n) for _ in range(3)]
+    with P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=3) as ctx:
+        for k in range(3):
+            ctx.select(k)
+            ctx.factor(0, "exponential_isotropic", [1.0, 0.1, 0.05])
+            ctx.set_field(fields[k])
+            ctx.set_mu(None, 0.0)
+        z = rng.normal(size=(2, n))
+        ctx.select(1).sweep(2, 0.0, 0.0, 0.0, 0, 0, z=z)
+        got = [ctx.select(k).get_field() for k in range(3)]
+        Lo = ctx.select(1).get_linv(0)
+    np.testing.assert_array_equal(got[0], fields[0])
+    np.testing.assert_array_equal(got[2], fields[2])
+    ref = O.sweep("local", fields[1], Lo, NN, col, O.precision_diag(Lo, NN), np.ones(n, np.int32), y,
+                  np.zeros(n), lm, 0.0, 0.0, 0.0, z)
+    np.testing.assert_allclose(got[1], ref, rtol=1e-9, atol=1e-10)
