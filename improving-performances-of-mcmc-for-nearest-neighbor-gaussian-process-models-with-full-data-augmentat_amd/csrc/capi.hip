@@ -46,7 +46,6 @@ struct nngp_ctx {
   int C = 1, cur = 0;
   std::string err;
   SweepLayout lay;
-  std::vector<ColorArgs> cargs;  // per colour
   std::vector<int> dpos;   // loc -> device row (== lay.rpos)
   std::vector<int> level_ptr, level_rows;
   ChainState ch[kMaxChains];
@@ -57,11 +56,11 @@ struct nngp_ctx {
   const double** linv_cur_d = nullptr;  // C pointers: current factor of each chain
   const double** linv_cur_h = nullptr;  // pinned mirror
   int* fail_d = nullptr;
-  int* lane_tab_d = nullptr;
+  int* chunk_slot0_d = nullptr;
   SlotShared* slots_d = nullptr;
   double2* dr_d = nullptr;
   int* slot_dpos_d = nullptr;
-  int* ent_rowpos_d = nullptr;
+  int* ent_pk_d = nullptr;
   int* ent_src_d = nullptr;
   double* ent_val_d = nullptr;   // C x n_entries
   double* w_slot_d = nullptr;    // n x C
@@ -126,11 +125,11 @@ int set_device(nngp_ctx* c) {
 // sweep-layout pointers
 SweepDev sweep_dev(nngp_ctx* c) {
   SweepDev L;
-  L.lane_tab = c->lane_tab_d;
+  L.chunk_slot0 = c->chunk_slot0_d;
   L.slots = c->slots_d;
   L.dr = c->dr_d;
   L.ent_val = c->ent_val_d;
-  L.ent_rowpos = c->ent_rowpos_d;
+  L.ent_pk = c->ent_pk_d;
   L.w_slot = c->w_slot_d;
   L.r = c->r_d;
   L.scal = c->scal_d;
@@ -142,9 +141,7 @@ SweepDev sweep_dev(nngp_ctx* c) {
 
 // sweep values of B + precision_diag of chain k from its current factor
 int refresh_sweep_values(nngp_ctx* c, int k) {
-  SweepDev L = sweep_dev(c);
-  for (const ColorArgs& ca : c->cargs)
-    HIPCHK(c, launch_sell_refresh_color(c->st, L, ca, c->ent_src_d, c->ch[k].linv_d[0], k));
+  HIPCHK(c, launch_sell_refresh(c->st, sweep_dev(c), c->lay.nchunks, c->ent_src_d, c->ch[k].linv_d[0], k));
   c->linv_cur_h[k] = c->ch[k].linv_d[0];
   HIPCHK(c, hipMemcpyAsync(c->linv_cur_d, c->linv_cur_h, sizeof(double*) * c->C, hipMemcpyHostToDevice, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
@@ -236,8 +233,8 @@ void nngp_ctx_destroy(nngp_ctx* c) {
   if (c->st) hipStreamSynchronize(c->st);
   for (auto& kv : c->graphs) hipGraphExecDestroy(kv.second);
   for (auto g : c->graph_objs) hipGraphDestroy(g);
-  std::vector<void*> ptrs = {c->locs_d, c->sc_d, c->nn_d, c->linv_cur_d, c->fail_d, c->lane_tab_d, c->slots_d,
-                             c->dr_d, c->slot_dpos_d, c->ent_rowpos_d, c->ent_src_d, c->ent_val_d, c->w_slot_d,
+  std::vector<void*> ptrs = {c->locs_d, c->sc_d, c->nn_d, c->linv_cur_d, c->fail_d, c->chunk_slot0_d, c->slots_d,
+                             c->dr_d, c->slot_dpos_d, c->ent_pk_d, c->ent_src_d, c->ent_val_d, c->w_slot_d,
                              c->r_d, c->level_rows_d, c->obs_ptr_d, c->obs_idx_d, c->lm_d, c->y_d, c->tmp_d,
                              c->tmp2_d, c->partials_d, c->res_d, c->z_d, c->scal_d};
   for (int k = 0; k < kMaxChains; ++k) {
@@ -309,23 +306,7 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
     return fail_msg(nullptr, NNGP_ERR_ARG, err);
   }
   const SweepLayout& L = c->lay;
-  c->cargs.resize(L.K);
-  for (int col = 0; col < L.K; ++col) {
-    ColorArgs& ca = c->cargs[col];
-    std::memset(&ca, 0, sizeof ca);
-    ca.chunk0 = L.color_chunk_ptr[col];
-    ca.nch = L.color_chunk_ptr[col + 1] - ca.chunk0;
-    ca.ncls = L.n_class[col];
-    for (int q = 0; q < ca.ncls; ++q) {
-      ca.rows[q] = L.class_rows[(size_t)col * kMaxClasses + q];
-      ca.end[q] = L.class_end[(size_t)col * kMaxClasses + q];
-      ca.base[q] = L.class_base[(size_t)col * kMaxClasses + q];
-    }
-    if (ca.ncls < 1 || ca.end[ca.ncls - 1] != ca.nch) {
-      delete c;
-      return fail_msg(nullptr, NNGP_ERR_ARG, "internal: bad colour class table");
-    }
-  }
+  static_assert(kPkRowBits == kRowBits && kPkPadRow == kPadRow, "packed entry format");
   dag_levels(nn.data(), n, b, c->level_ptr, c->level_rows);
   c->dpos = L.rpos;
   const std::vector<int>& dp = c->dpos;
@@ -371,11 +352,11 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
   CK(hipHostMalloc((void**)&c->linv_cur_h, sizeof(double*) * C, hipHostMallocDefault));
   for (int k = 0; k < C; ++k) c->linv_cur_h[k] = c->ch[k].linv_d[0];
   CK(dalloc(&c->fail_d, 1));
-  CK(dalloc(&c->lane_tab_d, L.lane_tab.size()));
+  CK(dalloc(&c->chunk_slot0_d, L.chunk_slot0.size()));
   CK(dalloc(&c->slots_d, n));
   CK(dalloc(&c->dr_d, (size_t)n * C));
   CK(dalloc(&c->slot_dpos_d, n));
-  CK(dalloc(&c->ent_rowpos_d, (size_t)L.n_entries));
+  CK(dalloc(&c->ent_pk_d, (size_t)L.n_entries));
   CK(dalloc(&c->ent_src_d, (size_t)L.n_entries));
   CK(dalloc(&c->ent_val_d, (size_t)L.n_entries * C));
   CK(dalloc(&c->w_slot_d, (size_t)n * C));
@@ -402,14 +383,14 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
       sd[s].loc = i;
       sd[s].nobs = obs_cnt[i + 1] - obs_cnt[i];
       sd[s].collen = L.collen[s];
-      sd[s].dpos = slot_dpos[s];
+      sd[s].f0 = L.slot_f0[s];
     }
-    CK(hipMemcpy(c->lane_tab_d, L.lane_tab.data(), sizeof(int) * L.lane_tab.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(c->chunk_slot0_d, L.chunk_slot0.data(), sizeof(int) * L.chunk_slot0.size(), hipMemcpyHostToDevice));
     CK(hipMemcpy(c->slots_d, sd.data(), sizeof(SlotShared) * sd.size(), hipMemcpyHostToDevice));
   }
   CK(hipMemsetAsync(c->dr_d, 0, sizeof(double2) * (size_t)n * C, c->st));
   CK(upload(c->slot_dpos_d, slot_dpos.data(), n, c->st));
-  CK(upload(c->ent_rowpos_d, L.ent_rowpos.data(), (size_t)L.n_entries, c->st));
+  CK(upload(c->ent_pk_d, L.ent_pk.data(), (size_t)L.n_entries, c->st));
   CK(upload(c->ent_src_d, L.ent_src.data(), (size_t)L.n_entries, c->st));
   CK(hipMemsetAsync(c->ent_val_d, 0, sizeof(double) * std::max<long long>(1, L.n_entries * C), c->st));
   CK(hipMemcpyAsync(c->linv_cur_d, c->linv_cur_h, sizeof(double*) * C, hipMemcpyHostToDevice, c->st));
@@ -671,7 +652,9 @@ static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, int mask, const double*
   for (int s = 0; s < n_sweeps; ++s) {
     for (int col = 0; col < c->lay.K; ++col) {
       if (evs) HIPCHK(c, hipEventRecord((*evs)[2 * ((size_t)s * c->lay.K + col)], c->st));
-      HIPCHK(c, launch_sweep_color(c->st, L, c->cargs[col], mask, s, z_dev, n));
+      HIPCHK(c, launch_sweep_color(c->st, L, c->lay.color_chunk_ptr[col],
+                                   c->lay.color_chunk_ptr[col + 1] - c->lay.color_chunk_ptr[col], mask, s,
+                                   z_dev, n));
       if (evs) HIPCHK(c, hipEventRecord((*evs)[2 * ((size_t)s * c->lay.K + col) + 1], c->st));
     }
   }

@@ -329,7 +329,7 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
   L = SweepLayout();
   L.n = n; L.b = b; L.LW = LW;
   if (LW != 64 && LW != 32 && LW != 16) { err = "lanes_per_chain must be 64, 32 or 16"; return false; }
-  if (n >= (1 << 28) - 1) { err = "n too large for the sweep lane table (< 2^28)"; return false; }
+  if (n >= kPadRow) { err = "n too large for the packed sweep row index (< 2^25 - 1)"; return false; }
   int K = 0;
   for (int i = 0; i < n; ++i) {
     if (colors[i] < 1) { err = "coloring must be 1-based positive"; return false; }
@@ -364,22 +364,17 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
         crow[p] = k; csrc[p] = L.rpos[k] * b + t;  // device rows are Morton-ordered
       }
   }
-  // per-location lane shape
-  std::vector<unsigned char> lk_of(n), rows_of(n);
+  const int cap = LW * kRowsMax, max_slots = 2 * LW - 1;
   for (int i = 0; i < n; ++i) {
-    const int len = std::max<long long>(1, cptr[i + 1] - cptr[i]);
+    const int len = (int)(cptr[i + 1] - cptr[i]);
     L.max_collen = std::max(L.max_collen, len);
-    int lk = 0;
-    while ((len + (1 << lk) - 1) >> lk > kRowsMax) ++lk;
-    if ((1 << lk) > LW) {
-      err = "a column of B has " + std::to_string(len) + " entries, more than lanes_per_chain * 16 = " +
-            std::to_string(LW * kRowsMax) + " (use fewer chains per context)";
+    if (len > cap) {
+      err = "a column of B has " + std::to_string(len) + " entries, more than a sweep chunk (" +
+            std::to_string(cap) + "; use fewer chains per context)";
       return false;
     }
-    lk_of[i] = (unsigned char)lk;
-    rows_of[i] = (unsigned char)((len + (1 << lk) - 1) >> lk);
   }
-  // slots: colour-major; inside a colour by rows (descending), Morton order
+  // slots: colour-major, Morton order inside a colour
   L.color_slot_ptr.assign(K + 1, 0);
   for (int i = 0; i < n; ++i) L.color_slot_ptr[colors[i]]++;
   for (int c = 0; c < K; ++c) L.color_slot_ptr[c + 1] += L.color_slot_ptr[c];
@@ -390,80 +385,45 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
   {
     std::vector<int> f(L.color_slot_ptr.begin(), L.color_slot_ptr.end() - 1);
     for (int r = 0; r < n; ++r) { int i = perm[r]; L.slot_loc[f[colors[i] - 1]++] = i; }
-    for (int c = 0; c < K; ++c)
-      std::stable_sort(L.slot_loc.begin() + L.color_slot_ptr[c], L.slot_loc.begin() + L.color_slot_ptr[c + 1],
-                       [&](int x, int y) { return rows_of[x] > rows_of[y]; });
     for (int s2 = 0; s2 < n; ++s2) L.loc_slot[L.slot_loc[s2]] = s2;
   }
   L.collen.resize(n);
+  L.slot_f0.resize(n);
   for (int s2 = 0; s2 < n; ++s2) {
     int i = L.slot_loc[s2];
     L.collen[s2] = (int)(cptr[i + 1] - cptr[i]);
   }
-  // chunks
+  // chunks: greedy runs of whole slots (<= cap cells, <= max_slots slots)
   L.color_chunk_ptr.assign(K + 1, 0);
-  L.n_class.assign(K, 0);
-  L.class_rows.assign((size_t)K * kMaxClasses, 0);
-  L.class_end.assign((size_t)K * kMaxClasses, 0);
-  L.class_base.assign((size_t)K * kMaxClasses, 0);
-  L.lane_tab.clear();
-  std::vector<long long> chunk_base;
-  std::vector<int> chunk_rows;
-  long long off = 0;
+  L.chunk_slot0.clear();
   for (int c = 0; c < K; ++c) {
-    const int a0 = L.color_slot_ptr[c], a1 = L.color_slot_ptr[c + 1];
-    const int ch_c0 = (int)chunk_base.size();
-    for (int s2 = a0; s2 < a1;) {
-      const int R = rows_of[L.slot_loc[s2]];
-      int e2 = s2;
-      while (e2 < a1 && rows_of[L.slot_loc[e2]] == R) ++e2;
-      const int q = L.n_class[c]++;
-      L.class_rows[(size_t)c * kMaxClasses + q] = R;
-      L.class_base[(size_t)c * kMaxClasses + q] = off;
-      // Morton-contiguous runs whose lane groups fit LW lanes
-      while (s2 < e2) {
-        int e3 = s2, lanes = 0;
-        while (e3 < e2) {
-          const int k = 1 << lk_of[L.slot_loc[e3]];
-          if (lanes + k > LW) break;
-          lanes += k;
-          ++e3;
-        }
-        std::vector<int> idx(e3 - s2);
-        std::iota(idx.begin(), idx.end(), s2);
-        std::stable_sort(idx.begin(), idx.end(),
-                         [&](int x, int y) { return lk_of[L.slot_loc[x]] > lk_of[L.slot_loc[y]]; });
-        const size_t lt0 = L.lane_tab.size();
-        L.lane_tab.resize(lt0 + LW, 0);
-        int o = 0;
-        for (int sl : idx) {
-          const int lk = lk_of[L.slot_loc[sl]];
-          for (int u = 0; u < (1 << lk); ++u) L.lane_tab[lt0 + o + u] = (sl + 1) | (lk << 28);
-          o += 1 << lk;
-        }
-        chunk_base.push_back(off);
-        chunk_rows.push_back(R);
-        off += (long long)LW * R;
-        s2 = e3;
+    int fill = 0, cnt = 0;
+    for (int s2 = L.color_slot_ptr[c]; s2 < L.color_slot_ptr[c + 1]; ++s2) {
+      const int len = L.collen[s2];
+      if (cnt == 0 || fill + len > cap || cnt + 1 > max_slots) {
+        L.chunk_slot0.push_back(s2);
+        fill = 0;
+        cnt = 0;
       }
-      L.class_end[(size_t)c * kMaxClasses + q] = (int)chunk_base.size() - ch_c0;
+      L.slot_f0[s2] = fill;
+      fill += len;
+      ++cnt;
     }
-    L.color_chunk_ptr[c + 1] = (int)chunk_base.size();
+    L.color_chunk_ptr[c + 1] = (int)L.chunk_slot0.size();
   }
-  L.nchunks = (int)chunk_base.size();
-  L.n_entries = off;
-  L.ent_rowpos.assign(off, 0);
-  L.ent_src.assign(off, -1);
+  L.nchunks = (int)L.chunk_slot0.size();
+  L.chunk_slot0.push_back(n);
+  L.n_entries = (long long)L.nchunks * cap;
+  L.ent_pk.assign(L.n_entries, (int)((unsigned)kPadRow | ((unsigned)max_slots << kRowBits)));
+  L.ent_src.assign(L.n_entries, -1);
   for (int ch = 0; ch < L.nchunks; ++ch) {
-    for (int lane = 0; lane < LW; ++lane) {
-      const int v = L.lane_tab[(size_t)ch * LW + lane];
-      if (v == 0) continue;
-      const int sl = (v & ((1 << 28) - 1)) - 1, lk = v >> 28, k = 1 << lk;
-      if ((lane & (k - 1)) != 0) continue;  // first lane of the slot's group
-      const int i = L.slot_loc[sl];
-      for (long long p = cptr[i], j = 0; p < cptr[i + 1]; ++p, ++j) {
-        const long long e = chunk_base[ch] + (j >> lk) * LW + lane + (j & (k - 1));
-        L.ent_rowpos[e] = L.rpos[crow[p]];
+    const long long base = (long long)ch * cap;
+    for (int s2 = L.chunk_slot0[ch]; s2 < L.chunk_slot0[ch + 1]; ++s2) {
+      const int i = L.slot_loc[s2], q = s2 - L.chunk_slot0[ch];
+      long long f = L.slot_f0[s2];
+      for (long long p = cptr[i]; p < cptr[i + 1]; ++p, ++f) {
+        const long long e = base + (f % kRowsMax) * LW + f / kRowsMax;
+        L.ent_pk[e] = (int)((unsigned)L.rpos[crow[p]] | ((unsigned)q << kRowBits));
         L.ent_src[e] = csrc[p];
       }
     }

@@ -24,24 +24,23 @@ int greedy_coloring(const int* nn_rowmajor, int n, int b, std::vector<int>& colo
 // bounding box of the first min(d,3) coordinates.
 void morton_keys(const double* locs_colmajor, int n, int d, std::vector<uint64_t>& keys);
 
-// Device layout of the chromatic sweep ("sliced ELL with row-count classes").
-//  - slots: locations re-indexed colour-major; inside a colour by row-count
-//    class R (descending), Morton order inside a class;
+// Device layout of the chromatic sweep ("merge-path slot streams").
+//  - slots: locations re-indexed colour-major, Morton order inside a colour;
 //  - r / field / Linv rows: Morton rank of the location (rpos);
-//  - slot i (column i of B, len_i entries) gets k_i = 2^lk_i lanes and
-//    R_i = ceil(len_i / k_i) rows, k_i the smallest power of two with
-//    R_i <= kRowsMax (so len <= 16 => k = 1, R = len: no padding);
-//  - chunk: one wavefront's share of ONE chain: LW lanes (LW = 64 / chains
-//    per wave) over a Morton-contiguous run of slots of one (colour, class);
-//    all chunks of a class have R rows, so chunk q of the class starts at
-//    entry base_class + q * LW * R: a closed form of per-colour kernel
-//    arguments (no metadata load in front of the entry loads);
-//  - lane_tab[ch*LW + l] = (slot + 1) | lk << 28 (0: idle lane); lane groups
-//    sorted by descending k inside a chunk => aligned power-of-two groups;
-//  - entry q of slot i lives at chunk_base + (q >> lk) * LW + o_i + (q & (k-1))
-//    (o_i = first lane of the slot's group).
-constexpr int kRowsMax = 16;  // rows per lane of a sweep chunk (== kSweepRows)
-constexpr int kMaxClasses = kRowsMax;
+//  - chunk: one chain group of a wavefront (LW lanes = 64 / chains per
+//    wave) x kRowsMax rows = LW*16 entry cells.  A chunk holds a contiguous
+//    run of whole slots of one colour (at most 2*LW - 1 slots): their columns
+//    of B concatenated in the lane-major stream f = lane*16 + row, so a
+//    column may continue from one lane into the next; the unused tail of the
+//    stream is padding.  Every chunk has the same size, so cell (lane, row)
+//    of chunk ch is entry ch*LW*16 + row*LW + lane (coalesced row loads, no
+//    metadata in front of them);
+//  - ent_pk[e] = rowpos | q << 25 (q = slot index inside the chunk; padding:
+//    rowpos = kPadRow, q = 2*LW - 1);
+//  - slot_f0[s] = first stream cell of slot s inside its chunk.
+constexpr int kRowsMax = 16;          // rows per lane (== kSweepRows)
+constexpr int kRowBits = 25;          // rowpos bits of ent_pk (n < 2^25)
+constexpr int kPadRow = (1 << kRowBits) - 1;
 
 struct SweepLayout {
   int n = 0, b = 0, K = 0, nchunks = 0, LW = 64;
@@ -49,23 +48,19 @@ struct SweepLayout {
   int max_collen = 0;
   std::vector<int> color_slot_ptr;   // K+1
   std::vector<int> color_chunk_ptr;  // K+1
+  std::vector<int> chunk_slot0;      // nchunks+1: first slot of each chunk
   std::vector<int> slot_loc;         // n
   std::vector<int> loc_slot;         // n
   std::vector<int> rpos;             // n: loc -> device row (Morton rank): r, field, Linv rows
   std::vector<int> collen;           // n (slot order)
-  std::vector<int> lane_tab;         // nchunks x LW
-  // per colour: n_class[c] classes; class q of colour c (index c*kMaxClasses+q):
-  // rows, exclusive chunk end relative to the colour's first chunk, first entry
-  std::vector<int> n_class;          // K
-  std::vector<int> class_rows;       // K * kMaxClasses
-  std::vector<int> class_end;        // K * kMaxClasses
-  std::vector<long long> class_base; // K * kMaxClasses
-  std::vector<int> ent_rowpos;       // n_entries (padding: 0)
+  std::vector<int> slot_f0;          // n (slot order)
+  std::vector<int> ent_pk;           // n_entries
   std::vector<int> ent_src;          // n_entries (device Linv index rpos[k]*b+j; padding: -1)
 };
 
 // lanes_per_chain: 64, 32 or 16 (1, 2 or 3-4 chains per wavefront).  Fails if
-// a column of B is longer than lanes_per_chain * kRowsMax.
+// a column of B is longer than a chunk (lanes_per_chain * 16 entries) or n
+// does not fit the packed row index.
 bool build_sweep_layout(const int* nn_rowmajor, int n, int b, const int* colors,
                         const double* locs_colmajor, int d, int lanes_per_chain, SweepLayout& L,
                         std::string& err);

@@ -27,28 +27,21 @@ struct __attribute__((aligned(16))) SlotShared {
   int loc;         // location index (0-based, Vecchia order)
   int nobs;        // obs_per_loc
   int collen;      // length of column loc of B
-  int dpos;        // device row of the location (Morton rank)
+  int f0;          // first stream cell of the slot inside its chunk
 };
 
-// per-colour kernel arguments: row-count classes of the colour's chunks
-struct ColorArgs {
-  int chunk0;                      // first chunk of the colour (global index)
-  int nch;                         // chunks of the colour
-  int ncls;                        // classes (<= kSweepRows)
-  int rows[kSweepRows];            // rows of class q
-  int end[kSweepRows];             // exclusive chunk end of class q (relative)
-  long long base[kSweepRows];      // first entry of class q
-};
+constexpr int kPkRowBits = 25;                    // ent_pk = rowpos | q << 25
+constexpr int kPkPadRow = (1 << kPkRowBits) - 1;  // padding rowpos
 
-// device pointers of the sliced-ELL layout; per-chain arrays interleave the
-// chains (index slot*C + chain, row*C + chain) so the chains of one entry share
-// cache lines; ent_val is chain-planar (chain * n_entries + entry).
+// device pointers of the merge-path sweep layout (graph_prep.h); per-chain
+// arrays interleave the chains (slot*C + chain, row*C + chain) so the chains of
+// one entry share cache lines; ent_val is chain-planar (chain*n_entries + e).
 struct SweepDev {
-  const int* lane_tab;        // nchunks x LW: (slot + 1) | lk << 28, 0 = idle
+  const int* chunk_slot0;     // nchunks+1
   const SlotShared* slots;    // n
   double2* dr;                // n x C: {precision_diag, residuals_sum}
   const double* ent_val;      // C x n_entries
-  const int* ent_rowpos;      // n_entries
+  const int* ent_pk;          // n_entries
   double* w_slot;             // n x C
   double* r;                  // n x C, Morton rows
   const SweepScalars* scal;   // C
@@ -80,10 +73,10 @@ int launch_row_stats(hipStream_t st, const double* linv, const int* nn, int n, i
 // reduce `nblocks` x 4 partials into res[4] (deterministic order)
 hipError_t launch_reduce4(hipStream_t st, const double* partials, int nblocks, double* res);
 
-// chain `chain`, one colour: ent_val[chain] from Linv (device order) and
-// dr[s*C+chain].x = precision_diag
-hipError_t launch_sell_refresh_color(hipStream_t st, const SweepDev& L, const ColorArgs& ca,
-                                     const int* ent_src, const double* linv, int chain);
+// chain `chain`: ent_val[chain] from Linv (device order) and
+// dr[s*C+chain].x = precision_diag, for chunks [0, nchunks)
+hipError_t launch_sell_refresh(hipStream_t st, const SweepDev& L, int nchunks, const int* ent_src,
+                               const double* linv, int chain);
 
 // dr[s*C+chain].y = residuals_sum of the slot's observations
 hipError_t launch_residual_sums(hipStream_t st, int n, const SweepDev& L, int chain, const int* obs_ptr,
@@ -97,7 +90,7 @@ hipError_t launch_slots_to_field(hipStream_t st, int n, const int* slot_dpos, co
 
 // one colour of the chromatic sweep for the chains in chain_mask;
 // z (optional): injected normals z[((sweep*C) + chain) * n + loc]
-hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, const ColorArgs& ca, int chain_mask,
+hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, int chunk0, int nch, int chain_mask,
                               int sweep_local, const double* z, int n);
 
 // obs reductions: mode 0 -> partial[0] += (y - f[loc] - mu + beta0)^2

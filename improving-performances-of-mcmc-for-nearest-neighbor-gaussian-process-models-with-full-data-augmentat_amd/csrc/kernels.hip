@@ -475,86 +475,55 @@ hipError_t launch_reduce4(hipStream_t st, const double* partials, int nblocks, d
 }
 
 // ------------------------------------------------------------------ A5
-// lane -> (chain, slot, sub-lane) of a chunk.  A wavefront holds 64/LW chains
-// of the same chunk (chain = lane / LW); inside a chain's LW lanes, slot groups
-// are aligned power-of-two lane ranges of size k.
-struct ChunkLane {
-  int lk, k, u, s, l, chain;
-  bool valid;
-};
-__device__ __forceinline__ ChunkLane chunk_lane(const SweepDev& L, int ch, int lane) {
-  ChunkLane c;
-  c.chain = lane / L.LW;
-  c.l = lane & (L.LW - 1);
-  const int v = L.lane_tab[(size_t)ch * L.LW + c.l];
-  c.valid = v != 0;
-  c.lk = c.valid ? (v >> 28) : 0;
-  c.k = 1 << c.lk;
-  c.u = c.l & (c.k - 1);
-  c.s = c.valid ? (v & 0x0FFFFFFF) - 1 : 0;
-  return c;
-}
+// Merge-path sweep layout (graph_prep.h): chunk ch of one chain is LW lanes x
+// kSweepRows rows; cell (lane l, row j) = stream position f = l*16 + j holds
+// entry ch*LW*16 + j*LW + l.  Slot q of the chunk covers stream cells
+// [f0_q, f0_q + len_q).
 
-// sum over the k lanes of a slot (k varies per lane group, groups aligned);
-// xor butterfly => bitwise-identical result in every lane of a group (IEEE
-// addition is commutative)
-__device__ __forceinline__ double group_sum(double v, int k) {
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const double o = __shfl_xor(v, off, 64);
-    if (off < k) v += o;
-  }
-  return v;
-}
-
-// chunk -> (rows, first entry) from the colour's class table (kernel
-// arguments: compile-time indices only, so everything stays in SGPRs)
-__device__ __forceinline__ void chunk_class(const ColorArgs& ca, int lch, int LW, int& rows, long long& base) {
-  rows = ca.rows[0];
-  int start = 0;
-  long long b0 = ca.base[0];
-#pragma unroll
-  for (int q = 1; q < kSweepRows; ++q) {
-    if (q < ca.ncls && lch >= ca.end[q - 1]) {
-      rows = ca.rows[q];
-      start = ca.end[q - 1];
-      b0 = ca.base[q];
-    }
-  }
-  base = b0 + (long long)(lch - start) * LW * rows;
-}
-
-// refresh chain `chain`'s sweep-layout values of B from Linv + precision_diag;
-// one wavefront per chunk (LW lanes used), launched per colour class table
-__global__ __launch_bounds__(256) void sell_refresh_kernel(SweepDev L, ColorArgs ca,
+// refresh chain `chain`'s B values in the sweep layout (one lane per cell)
+// and precision_diag (one lane per slot, entries summed in row order)
+template <int LW>
+__global__ __launch_bounds__(256) void sell_refresh_kernel(SweepDev L, int nchunks,
                                                            const int* __restrict__ ent_src,
-                                                           const double* __restrict__ linv,
-                                                           int chain) {
-  const int lch = blockIdx.x * 4 + (threadIdx.x >> 6);
+                                                           const double* __restrict__ linv, int chain) {
+  // a wave covers 64/LW chunks: lanes [g*LW, (g+1)*LW) take chunk wave*(64/LW) + g
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (lch >= ca.nch || lane >= L.LW) return;
-  int R;
-  long long base;
-  chunk_class(ca, lch, L.LW, R, base);
-  ChunkLane c = chunk_lane(L, ca.chunk0 + lch, lane);
-  const int len = c.valid ? L.slots[c.s].collen : 0;
+  const int chk = wave * (64 / LW) + lane / LW;
+  const int l = lane % LW;
+  if (chk >= nchunks) return;
+  const long long base = (long long)chk * LW * kSweepRows;
   double* val = const_cast<double*>(L.ent_val) + (size_t)chain * L.n_entries;
-  double D = 0.0;
-  for (int j = 0; j < R; ++j) {
-    const long long e = base + (long long)j * L.LW + c.l;
+#pragma unroll
+  for (int j = 0; j < kSweepRows; ++j) {
+    const long long e = base + (long long)j * LW + l;
     const int src = ent_src[e];
-    const double v = src >= 0 ? linv[src] : 0.0;
-    if (j * c.k + c.u < len) D += v * v;
-    val[e] = v;
+    val[e] = src >= 0 ? linv[src] : 0.0;
   }
-  D = group_sum(D, c.k);
-  if (c.valid && c.u == 0) L.dr[(size_t)c.s * L.C + chain].x = D;
+  const int s0 = L.chunk_slot0[chk], nsl = L.chunk_slot0[chk + 1] - s0;
+  for (int t = l; t < nsl; t += LW) {
+    const SlotShared sh = L.slots[s0 + t];
+    double D = 0.0;
+    for (int f = sh.f0; f < sh.f0 + sh.collen; ++f) {
+      const double v = linv[ent_src[base + (long long)(f % kSweepRows) * LW + f / kSweepRows]];
+      D += v * v;
+    }
+    L.dr[(size_t)(s0 + t) * L.C + chain].x = D;
+  }
 }
 
-hipError_t launch_sell_refresh_color(hipStream_t st, const SweepDev& L, const ColorArgs& ca,
-                                     const int* ent_src, const double* linv, int chain) {
-  const int g = (ca.nch + 3) / 4;
-  if (g > 0) hipLaunchKernelGGL(sell_refresh_kernel, dim3(g), dim3(kBlock), 0, st, L, ca, ent_src, linv, chain);
+hipError_t launch_sell_refresh(hipStream_t st, const SweepDev& L, int nchunks, const int* ent_src,
+                               const double* linv, int chain) {
+  const int per_wave = 64 / L.LW;
+  const int waves = (nchunks + per_wave - 1) / per_wave;
+  const int g = (waves + 3) / 4;
+  if (g == 0) return hipSuccess;
+  switch (L.LW) {
+    case 64: hipLaunchKernelGGL(sell_refresh_kernel<64>, dim3(g), dim3(kBlock), 0, st, L, nchunks, ent_src, linv, chain); break;
+    case 32: hipLaunchKernelGGL(sell_refresh_kernel<32>, dim3(g), dim3(kBlock), 0, st, L, nchunks, ent_src, linv, chain); break;
+    case 16: hipLaunchKernelGGL(sell_refresh_kernel<16>, dim3(g), dim3(kBlock), 0, st, L, nchunks, ent_src, linv, chain); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
@@ -613,93 +582,171 @@ hipError_t launch_slots_to_field(hipStream_t st, int n, const int* slot_dpos, co
 }
 
 // ------------------------------------------------------------------ A1
-// One colour of the chromatic sweep, local form, for up to 4 chains at once.
-// One wavefront per chunk; the 64/LW chain groups of a wavefront process the
-// same slots for different chains (same entry positions, chain-interleaved r,
-// w and {D, R}, so the chains of one entry share cache lines).  Inside a chain
-// group, k lanes per location (k = 1 for typical columns, up to 16 for the
-// long columns of coarse max-min points), R rows per lane from the colour's
-// class table (kernel arguments), so the entry and lane-table loads depend on
-// nothing but the wavefront index: two dependent memory round trips
-// (entries + lane table -> slot record, w, r gathers), then compute and the
-// conflict-free scatter:
+// One colour of the chromatic sweep, local form, for up to 4 chains at once:
 //   acc  = sum_{k in col(i)} B[k,i] r_k - D_i w_i      (= (B^T B w_{!c})_i)
 //   P    = D_i/s2 + n_i/t2
 //   w_i' = (R_i/t2 - acc/s2)/P + z_i/sqrt(P)
 //   r_k += B[k,i] (w_i' - w_i)
+// One wavefront per chunk; its 64/LW chain groups run the same chunk for
+// different chains (same entry cells, chain-interleaved r / w / {D,R}).
+//  1. every lane loads its 16 cells (coalesced, address = chunk index only) and
+//     gathers r at their rows;
+//  2. segmented sums along the lane's cells: a slot that lies inside the lane
+//     goes to acc[q]; the part of a slot that continues from the previous lane
+//     goes to head[lane], the part that continues into the next lane to
+//     tail[lane] (LDS, per chain group);
+//  3. one owner lane per slot (q = lane, lane + LW): acc = tail[l0] +
+//     head[l0+1] + ... + head[l1] in lane order (deterministic), the Gibbs
+//     draw, dw[q] -> LDS;
+//  4. every cell scatters r_k += B[k,i] dw[q].
+// Slots of one colour share no row of B, so the scatter is conflict-free.
 // Blocks are remapped so that consecutive (spatially adjacent) chunks run on
 // the same XCD and share its L2 for the r gathers.
-template <bool INJECT>
-__global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, ColorArgs ca, int chain_mask,
-                                                          int sweep_local, const double* __restrict__ z,
-                                                          int n) {
-  const int nb = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q = nb >> 3, rm = nb & 7;
-  const int lb = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + (bid >> 3);
-  const int lch = lb * 4 + (threadIdx.x >> 6);
-  if (lch >= ca.nch) return;
-  const int lane = threadIdx.x & 63;
-  const int chain = lane / L.LW;
-  if (chain >= L.C || !((chain_mask >> chain) & 1)) return;
-  int R;
-  long long base;
-  chunk_class(ca, lch, L.LW, R, base);
-  const ChunkLane c = chunk_lane(L, ca.chunk0 + lch, lane);
-  const int C = L.C;
-  double* r = L.r;  // gathered then scattered: no __restrict__
-  const double* val = L.ent_val + (size_t)chain * L.n_entries;
-  // round trip 1: entries (address from the wavefront index only) + lane table
-  double v[kSweepRows], rv[kSweepRows];
-  int p[kSweepRows];
-#pragma unroll
-  for (int j = 0; j < kSweepRows; ++j) {
-    if (j < R) {
-      const long long e = base + (long long)j * L.LW + c.l;
-      v[j] = val[e];
-      p[j] = L.ent_rowpos[e];
-    } else {
-      v[j] = 0.0;
-      p[j] = 0;
-    }
-  }
-  // round trip 2: slot record, w, {D, R}, scalars, r gathers
-  const SlotShared sh = L.slots[c.s];
-  const size_t sc_idx = (size_t)c.s * C + chain;
-  const double w = L.w_slot[sc_idx];
-  const double2 dr = L.dr[sc_idx];
-  const SweepScalars* scal = L.scal + chain;
-  const double inv_s2 = scal->inv_s2, inv_t2 = scal->inv_t2;
-  double zz;
-  if (INJECT) zz = z[((size_t)sweep_local * C + chain) * n + sh.loc];
-  else zz = normal_at(scal->seed, scal->counter_base + (uint64_t)sweep_local, (uint32_t)sh.loc);
-#pragma unroll
-  for (int j = 0; j < kSweepRows; ++j) rv[j] = (j < R) ? r[(size_t)p[j] * C + chain] : 0.0;
-  const int len = c.valid ? sh.collen : 0;
-  double acc = 0.0;
-#pragma unroll
-  for (int j = 0; j < kSweepRows; ++j) acc += (j * c.k + c.u < len) ? v[j] * rv[j] : 0.0;
-  acc = group_sum(acc, c.k);
-  if (!c.valid) return;
-  acc -= dr.x * w;
-  const double P = dr.x * inv_s2 + (double)sh.nobs * inv_t2;
-  const double wn = (inv_t2 * dr.y - inv_s2 * acc) / P + zz / sqrt(P);
-  const double dw = wn - w;
-  if (c.u == 0) L.w_slot[sc_idx] = wn;
-#pragma unroll
-  for (int j = 0; j < kSweepRows; ++j)
-    if (j * c.k + c.u < len) r[(size_t)p[j] * C + chain] = rv[j] + v[j] * dw;
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, const ColorArgs& ca, int chain_mask,
+template <bool INJECT, int LW>
+__global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, int chunk0, int nch, int chain_mask,
+                                                          int sweep_local, const double* __restrict__ z,
+                                                          int n) {
+  constexpr int CG = 64 / LW;  // chain groups per wavefront
+  __shared__ double lds[4][CG][6 * LW];
+  const int nb = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, qq = nb >> 3, rm = nb & 7;
+  const int lb = (xcd < rm ? xcd * (qq + 1) : rm * (qq + 1) + (xcd - rm) * qq) + (bid >> 3);
+  const int wv = threadIdx.x >> 6;
+  const int lch = lb * 4 + wv;
+  if (lch >= nch) return;
+  const int lane = threadIdx.x & 63;
+  const int cg = lane / LW, l = lane % LW;
+  const int C = L.C;
+  if (cg >= C || !((chain_mask >> cg) & 1)) return;
+  const int chain = cg;
+  double* acc_s = lds[wv][cg];        // [2*LW]: per-slot sums, then dw
+  double* head_s = acc_s + 2 * LW;    // [LW]
+  double* tail_s = head_s + LW;       // [LW]
+  const int ch = chunk0 + lch;
+  const long long base = (long long)ch * LW * kSweepRows;
+  const double* val = L.ent_val + (size_t)chain * L.n_entries;
+  double* r = L.r;  // gathered then scattered: no __restrict__
+  // round trip 1: the lane's cells (address from the chunk index only) + chunk slot range
+  double v[kSweepRows], rv[kSweepRows];
+  int pk[kSweepRows];
+#pragma unroll
+  for (int j = 0; j < kSweepRows; ++j) {
+    const long long e = base + (long long)j * LW + l;
+    v[j] = val[e];
+    pk[j] = L.ent_pk[e];
+  }
+  const int s0 = L.chunk_slot0[ch];
+  const int nsl = L.chunk_slot0[ch + 1] - s0;
+  // round trip 2: r gathers + the owned slots' records (independent of each other)
+#pragma unroll
+  for (int j = 0; j < kSweepRows; ++j) {
+    const int p = pk[j] & kPkPadRow;
+    rv[j] = (p != kPkPadRow) ? r[(size_t)p * C + chain] : 0.0;
+  }
+  SlotShared sh[2];
+  double2 dr[2];
+  double w[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int t = l + u * LW;
+    const int s = s0 + min(t, nsl - 1);
+    sh[u] = L.slots[s];
+    dr[u] = L.dr[(size_t)s * C + chain];
+    w[u] = L.w_slot[(size_t)s * C + chain];
+  }
+  const SweepScalars* scal = L.scal + chain;
+  const double inv_s2 = scal->inv_s2, inv_t2 = scal->inv_t2;
+  // segmented sums along the lane's cells
+  int q[kSweepRows];
+#pragma unroll
+  for (int j = 0; j < kSweepRows; ++j) q[j] = (int)((unsigned)pk[j] >> kPkRowBits);
+  const int dummy = 2 * LW - 1;
+  const int q_prev_last = __shfl(q[kSweepRows - 1], lane - 1, 64);
+  const int q_next_first = __shfl(q[0], lane + 1, 64);
+  const bool started_before = l > 0 && q[0] != dummy && q[0] == q_prev_last;
+  const bool continues_after = l < LW - 1 && q[kSweepRows - 1] != dummy && q[kSweepRows - 1] == q_next_first;
+  double seg = 0.0;
+  bool first = true;
+#pragma unroll
+  for (int j = 0; j < kSweepRows; ++j) {
+    seg += v[j] * rv[j];
+    const bool end_here = (j == kSweepRows - 1) || (q[j] != q[j + 1 < kSweepRows ? j + 1 : j]);
+    if (end_here) {
+      if (first && started_before) head_s[l] = seg;
+      else if (j == kSweepRows - 1 && continues_after) tail_s[l] = seg;
+      else acc_s[q[j]] = seg;
+      seg = 0.0;
+      first = false;
+    }
+  }
+  wave_lds_sync();
+  // owner lanes: the Gibbs draw of slots q = l and q = l + LW
+  double dwv[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int t = l + u * LW;
+    dwv[u] = 0.0;
+    if (t < nsl) {
+      const int f0 = sh[u].f0, len = sh[u].collen;
+      const int l0 = f0 / kSweepRows, l1 = (f0 + len - 1) / kSweepRows;
+      double acc;
+      if (l0 == l1) {
+        acc = acc_s[t];
+      } else {
+        acc = tail_s[l0];
+        for (int ll = l0 + 1; ll <= l1; ++ll) acc += head_s[ll];
+      }
+      double zz;
+      if (INJECT) zz = z[((size_t)sweep_local * C + chain) * n + sh[u].loc];
+      else zz = normal_at(scal->seed, scal->counter_base + (uint64_t)sweep_local, (uint32_t)sh[u].loc);
+      acc -= dr[u].x * w[u];
+      const double P = dr[u].x * inv_s2 + (double)sh[u].nobs * inv_t2;
+      const double wn = (inv_t2 * dr[u].y - inv_s2 * acc) / P + zz / sqrt(P);
+      dwv[u] = wn - w[u];
+      L.w_slot[(size_t)(s0 + t) * C + chain] = wn;
+    }
+  }
+  // acc[t] is read and then overwritten by its owner lane only
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+    if (l + u * LW < nsl) acc_s[l + u * LW] = dwv[u];
+  wave_lds_sync();
+#pragma unroll
+  for (int j = 0; j < kSweepRows; ++j) {
+    const int p = pk[j] & kPkPadRow;
+    if (p != kPkPadRow) r[(size_t)p * C + chain] = rv[j] + v[j] * acc_s[q[j]];
+  }
+}
+
+hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, int chunk0, int nch, int chain_mask,
                               int sweep_local, const double* z, int n) {
-  const int g = (ca.nch + 3) / 4;
+  const int g = (nch + 3) / 4;
   if (g == 0) return hipSuccess;
-  if (z)
-    hipLaunchKernelGGL((sweep_color_kernel<true>), dim3(g), dim3(kBlock), 0, st, L, ca, chain_mask,
-                       sweep_local, z, n);
-  else
-    hipLaunchKernelGGL((sweep_color_kernel<false>), dim3(g), dim3(kBlock), 0, st, L, ca, chain_mask,
-                       sweep_local, z, n);
+#define NNGP_SWEEP_LAUNCH(I, W)                                                                     \
+  hipLaunchKernelGGL((sweep_color_kernel<I, W>), dim3(g), dim3(kBlock), 0, st, L, chunk0, nch,     \
+                     chain_mask, sweep_local, z, n)
+  if (z) {
+    switch (L.LW) {
+      case 64: NNGP_SWEEP_LAUNCH(true, 64); break;
+      case 32: NNGP_SWEEP_LAUNCH(true, 32); break;
+      case 16: NNGP_SWEEP_LAUNCH(true, 16); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else {
+    switch (L.LW) {
+      case 64: NNGP_SWEEP_LAUNCH(false, 64); break;
+      case 32: NNGP_SWEEP_LAUNCH(false, 32); break;
+      case 16: NNGP_SWEEP_LAUNCH(false, 16); break;
+      default: return hipErrorInvalidValue;
+    }
+  }
+#undef NNGP_SWEEP_LAUNCH
   return hipGetLastError();
 }
 

@@ -1,7 +1,7 @@
 // Invariants of the sweep layout planner (graph_prep.cpp), checked on CPU:
-// every nonzero B[k,i] appears exactly once, in its slot's lane group, at the
-// closed-form address the sweep kernel computes from the colour class table;
-// padding is inert; chunk classes tile each colour.  Usage:
+// every nonzero B[k,i] appears exactly once, in its slot's stream range, at
+// the closed-form address the sweep kernel computes (fixed chunk stride,
+// lane-major stream); padding is inert and only at the stream tail.  Usage:
 //   layout_check <n> <m> <lanes_per_chain> <seed>   (prints "ok <stats>")
 #include <cstdio>
 #include <cstdlib>
@@ -54,53 +54,45 @@ int main(int argc, char** argv) {
       ++nnz;
     }
   REQUIRE(nnz == L.nnz);
-  std::vector<char> seen_slot(n, 0);
+  const int cap = LW * kRowsMax, dummy = 2 * LW - 1;
+  REQUIRE(L.n_entries == (long long)L.nchunks * cap);
+  REQUIRE(L.chunk_slot0[L.nchunks] == n);
   std::vector<char> used((size_t)L.n_entries, 0);
   long long found = 0;
   for (int c = 0; c < K; ++c) {
-    const int ch0 = L.color_chunk_ptr[c], nch = L.color_chunk_ptr[c + 1] - ch0;
-    const int ncls = L.n_class[c];
-    REQUIRE(ncls >= 1 && ncls <= kMaxClasses);
-    REQUIRE(L.class_end[(size_t)c * kMaxClasses + ncls - 1] == nch);
-    for (int lch = 0; lch < nch; ++lch) {
-      // the kernel's closed form (chunk_class in kernels.hip)
-      int q = 0;
-      while (q + 1 < ncls && lch >= L.class_end[(size_t)c * kMaxClasses + q]) ++q;
-      const int R = L.class_rows[(size_t)c * kMaxClasses + q];
-      const int start = q ? L.class_end[(size_t)c * kMaxClasses + q - 1] : 0;
-      const long long base = L.class_base[(size_t)c * kMaxClasses + q] + (long long)(lch - start) * LW * R;
-      REQUIRE(R >= 1 && R <= kRowsMax);
-      REQUIRE(base + (long long)LW * R <= L.n_entries);
-      const int ch = ch0 + lch;
-      for (int l = 0; l < LW; ++l) {
-        const int v = L.lane_tab[(size_t)ch * LW + l];
-        if (!v) continue;
-        const int s = (v & 0x0FFFFFFF) - 1, lk = v >> 28, k = 1 << lk;
-        REQUIRE(s >= L.color_slot_ptr[c] && s < L.color_slot_ptr[c + 1]);
-        REQUIRE((l & (k - 1)) == (l % k));  // aligned group
-        const int i = L.slot_loc[s];
+    REQUIRE(L.chunk_slot0[L.color_chunk_ptr[c]] == L.color_slot_ptr[c]);
+    for (int ch = L.color_chunk_ptr[c]; ch < L.color_chunk_ptr[c + 1]; ++ch) {
+      const int s0 = L.chunk_slot0[ch], s1 = L.chunk_slot0[ch + 1];
+      REQUIRE(s1 > s0 && s1 - s0 <= 2 * LW - 1);
+      REQUIRE(s1 <= L.color_slot_ptr[c + 1]);
+      const long long base = (long long)ch * cap;  // the kernel's closed form
+      int f = 0;
+      for (int s = s0; s < s1; ++s) {
+        const int i = L.slot_loc[s], q = s - s0;
         REQUIRE(col[i] == c + 1);
+        REQUIRE(L.slot_f0[s] == f);
         const int len = L.collen[s];
         REQUIRE(len == (int)want[i].size());
-        REQUIRE((len + k - 1) / k <= R);
-        const int u = l & (k - 1);
-        if (u == 0) { REQUIRE(!seen_slot[s]); seen_slot[s] = 1; }
-        for (int j = 0; j < R; ++j) {
-          const long long e = base + (long long)j * LW + l;
+        for (int t = 0; t < len; ++t, ++f) {
+          const long long e = base + (long long)(f % kRowsMax) * LW + f / kRowsMax;
           REQUIRE(!used[e]);
           used[e] = 1;
-          if (j * k + u < len) {
-            REQUIRE(want[i].count({L.ent_rowpos[e], L.ent_src[e]}) == 1);
-            ++found;
-          } else {
-            REQUIRE(L.ent_src[e] == -1);
-          }
+          const int pk = L.ent_pk[e];
+          REQUIRE((int)((unsigned)pk >> kRowBits) == q);
+          REQUIRE(want[i].count({pk & kPadRow, L.ent_src[e]}) == 1);
+          ++found;
         }
+      }
+      REQUIRE(f <= cap);
+      for (int g = f; g < cap; ++g) {  // padding tail
+        const long long e = base + (long long)(g % kRowsMax) * LW + g / kRowsMax;
+        REQUIRE(!used[e]);
+        REQUIRE((L.ent_pk[e] & kPadRow) == kPadRow && (int)((unsigned)L.ent_pk[e] >> kRowBits) == dummy);
+        REQUIRE(L.ent_src[e] == -1);
       }
     }
   }
   REQUIRE(found == nnz);
-  for (int s = 0; s < n; ++s) REQUIRE(seen_slot[s]);
   for (int i = 0; i < n; ++i) REQUIRE(L.slot_loc[L.loc_slot[i]] == i);
   std::printf("ok K=%d nnz=%lld entries=%lld chunks=%d max_collen=%d\n", K, nnz, L.n_entries, L.nchunks,
               L.max_collen);
