@@ -70,26 +70,28 @@ def test_update_iterations_match_oracle_vignette_X_locs(P, O, toy):
 
 def test_lockstep_batched_chains_equal_sequential_chains(P, toy):
     """mcmc_nngp_update_Gaussian drives the 3 chains of one context in
-    lockstep with batched sweeps; every record equals the chain run alone
-    (own 1-chain context, sweeps one by one)."""
+    lockstep with batched sweeps; every record equals the chains run one
+    after another (each sweep alone) on an identical 3-chain context."""
+    import copy
+
+    from nngp_amd.context import make_chain_views
     from nngp_amd.update_gaussian import _run_chain, mcmc_nngp_update_Gaussian
 
     L = P.mcmc_nngp_initialize(toy["locs"], toy["observed_field"], X_locs=toy["X"],
                                stationary_covfun="exponential_isotropic", m=5, n_chains=3, seed=2)
     va = L["vecchia_approx"]
     assert len({id(v.ctx) for v in L["_contexts"]}) == 1  # one 3-chain context
-    import copy
     states0 = copy.deepcopy(L["states"])
     out = mcmc_nngp_update_Gaussian(L["locs"], L["X"], L["observed_field"], L["space_time_model"], va,
                                     L["states"], 20, field_thinning=0.1, n_chromatic=3,
                                     contexts=L["_contexts"], seed=1)
+    views = make_chain_views(L["locs"], va["NNarray"], va["coloring"], va["locs_match"], L["observed_field"], 3)
+    y = np.asarray(L["observed_field"], np.float64)
     for i, (nm, st) in enumerate(states0.items()):
-        with P.ChainContext(L["locs"], va["NNarray"], va["coloring"], va["locs_match"], L["observed_field"],
-                            device=0) as one:
-            ref = _run_chain(i, st, one, L["X"], np.asarray(L["observed_field"], np.float64),
-                             L["space_time_model"], va, 20, 0.1, True, 3, 0, 1)
+        ref = _run_chain(i, st, views[i], L["X"], y, L["space_time_model"], va, 20, 0.1, True, 3, 0, 1)
         for key in ("beta_0", "log_scale", "log_noise_variance", "shape", "beta", "field"):
             np.testing.assert_array_equal(out[nm]["records"][key], ref["records"][key], err_msg=f"{nm} {key}")
+    views[0].ctx.close()
     L["_contexts"][0].close()
 
 
