@@ -56,11 +56,17 @@ struct nngp_ctx {
   const double** linv_cur_d = nullptr;  // C pointers: current factor of each chain
   const double** linv_cur_h = nullptr;  // pinned mirror
   int* fail_d = nullptr;
-  int* chunk_slot0_d = nullptr;
   SlotShared* slots_d = nullptr;
   double2* dr_d = nullptr;
   int* slot_dpos_d = nullptr;
+  int* chunk_first_d = nullptr;  // nchunks+1
+  int* loc_rank_d = nullptr;     // n: compact index of each location (Vecchia order)
+  int* pairs_d = nullptr;        // normal pairs grouped by the colour of their even member
+  std::vector<int> pair_ptr;     // K+1
+  std::vector<int> loc_rank;     // host copy
+  double* zbuf_d = nullptr;      // 2 x n x C: normals of the current / next sweep
   int* ent_pk_d = nullptr;
+  uint16_t* ent_pos_d = nullptr;
   int* ent_src_d = nullptr;
   double* ent_val_d = nullptr;   // C x n_entries
   double* w_slot_d = nullptr;    // n x C
@@ -79,6 +85,7 @@ struct nngp_ctx {
   SweepScalars* scal_d = nullptr;  // C
   SweepScalars* scal_h = nullptr;  // pinned, C
   double* res_h = nullptr;         // pinned, 8 doubles
+  unsigned long long* dbg_d = nullptr;  // NNGP_PROBE=9: per-chunk timestamps
   std::map<long long, hipGraphExec_t> graphs;  // key: n_sweeps << 8 | chain mask
   std::vector<hipGraph_t> graph_objs;
 };
@@ -125,17 +132,20 @@ int set_device(nngp_ctx* c) {
 // sweep-layout pointers
 SweepDev sweep_dev(nngp_ctx* c) {
   SweepDev L;
-  L.chunk_slot0 = c->chunk_slot0_d;
   L.slots = c->slots_d;
   L.dr = c->dr_d;
   L.ent_val = c->ent_val_d;
   L.ent_pk = c->ent_pk_d;
+  L.ent_pos = c->ent_pos_d;
   L.w_slot = c->w_slot_d;
   L.r = c->r_d;
   L.scal = c->scal_d;
   L.n_entries = c->lay.n_entries;
   L.C = c->C;
   L.LW = c->lay.LW;
+  L.chunk_first = c->chunk_first_d;
+  L.loc_rank = c->loc_rank_d;
+  L.dbg = c->dbg_d;
   return L;
 }
 
@@ -233,10 +243,11 @@ void nngp_ctx_destroy(nngp_ctx* c) {
   if (c->st) hipStreamSynchronize(c->st);
   for (auto& kv : c->graphs) hipGraphExecDestroy(kv.second);
   for (auto g : c->graph_objs) hipGraphDestroy(g);
-  std::vector<void*> ptrs = {c->locs_d, c->sc_d, c->nn_d, c->linv_cur_d, c->fail_d, c->chunk_slot0_d, c->slots_d,
+  std::vector<void*> ptrs = {c->locs_d, c->sc_d, c->nn_d, c->linv_cur_d, c->fail_d, c->slots_d,
                              c->dr_d, c->slot_dpos_d, c->ent_pk_d, c->ent_src_d, c->ent_val_d, c->w_slot_d,
                              c->r_d, c->level_rows_d, c->obs_ptr_d, c->obs_idx_d, c->lm_d, c->y_d, c->tmp_d,
-                             c->tmp2_d, c->partials_d, c->res_d, c->z_d, c->scal_d};
+                             c->tmp2_d, c->partials_d, c->res_d, c->z_d, c->scal_d, c->dbg_d,
+                             c->chunk_first_d, c->loc_rank_d, c->pairs_d, c->zbuf_d, c->ent_pos_d};
   for (int k = 0; k < kMaxChains; ++k) {
     ChainState& s = c->ch[k];
     ptrs.insert(ptrs.end(), {s.linv_d[0], s.linv_d[1], s.field_d, s.field_prop_d, s.mu_d});
@@ -321,9 +332,10 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
       int a = nn[(size_t)i * b + j];
       nn_dev[(size_t)dp[i] * b + j] = a < 0 ? -1 : dp[a];
     }
-  std::vector<int> lm_dev(n_obs), slot_dpos(n);
+  const size_t NS = (size_t)L.n_slots;
+  std::vector<int> lm_dev(n_obs), slot_dpos(NS);
   for (int o = 0; o < n_obs; ++o) lm_dev[o] = dp[lm0[o]];
-  for (int s = 0; s < n; ++s) slot_dpos[s] = dp[L.slot_loc[s]];
+  for (size_t s = 0; s < NS; ++s) slot_dpos[s] = L.slot_loc[s] < 0 ? -1 : dp[L.slot_loc[s]];
 
   if ((rc = set_device(c))) { delete c; return rc; }
 #define CK(x)                                                     \
@@ -352,14 +364,18 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
   CK(hipHostMalloc((void**)&c->linv_cur_h, sizeof(double*) * C, hipHostMallocDefault));
   for (int k = 0; k < C; ++k) c->linv_cur_h[k] = c->ch[k].linv_d[0];
   CK(dalloc(&c->fail_d, 1));
-  CK(dalloc(&c->chunk_slot0_d, L.chunk_slot0.size()));
-  CK(dalloc(&c->slots_d, n));
-  CK(dalloc(&c->dr_d, (size_t)n * C));
-  CK(dalloc(&c->slot_dpos_d, n));
+  CK(dalloc(&c->slots_d, NS));
+  CK(dalloc(&c->dr_d, NS * C));
+  CK(dalloc(&c->slot_dpos_d, NS));
+  CK(dalloc(&c->chunk_first_d, L.chunk_first.size()));
+  CK(dalloc(&c->loc_rank_d, n));
+  CK(dalloc(&c->pairs_d, (n + 1) / 2));
+  CK(dalloc(&c->zbuf_d, (size_t)2 * n * C));
   CK(dalloc(&c->ent_pk_d, (size_t)L.n_entries));
+  CK(dalloc(&c->ent_pos_d, (size_t)L.n_entries));
   CK(dalloc(&c->ent_src_d, (size_t)L.n_entries));
   CK(dalloc(&c->ent_val_d, (size_t)L.n_entries * C));
-  CK(dalloc(&c->w_slot_d, (size_t)n * C));
+  CK(dalloc(&c->w_slot_d, NS * C));
   CK(dalloc(&c->r_d, (size_t)n * C));
   CK(dalloc(&c->level_rows_d, n));
   CK(dalloc(&c->obs_ptr_d, (size_t)n + 1));
@@ -377,20 +393,39 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
   CK(upload(c->locs_d, locs_rm.data(), locs_rm.size(), c->st));
   CK(upload(c->nn_d, nn_dev.data(), nn_dev.size(), c->st));
   {
-    std::vector<SlotShared> sd(n);
-    for (int s = 0; s < n; ++s) {
+    std::vector<SlotShared> sd(NS);
+    for (size_t s = 0; s < NS; ++s) {
       const int i = L.slot_loc[s];
       sd[s].loc = i;
-      sd[s].nobs = obs_cnt[i + 1] - obs_cnt[i];
+      sd[s].nobs = i < 0 ? 0 : obs_cnt[i + 1] - obs_cnt[i];
       sd[s].collen = L.collen[s];
       sd[s].f0 = L.slot_f0[s];
     }
-    CK(hipMemcpy(c->chunk_slot0_d, L.chunk_slot0.data(), sizeof(int) * L.chunk_slot0.size(), hipMemcpyHostToDevice));
     CK(hipMemcpy(c->slots_d, sd.data(), sizeof(SlotShared) * sd.size(), hipMemcpyHostToDevice));
   }
-  CK(hipMemsetAsync(c->dr_d, 0, sizeof(double2) * (size_t)n * C, c->st));
-  CK(upload(c->slot_dpos_d, slot_dpos.data(), n, c->st));
+  CK(hipMemsetAsync(c->dr_d, 0, sizeof(double2) * NS * C, c->st));
+  CK(hipMemsetAsync(c->w_slot_d, 0, sizeof(double) * NS * C, c->st));
+  CK(upload(c->slot_dpos_d, slot_dpos.data(), NS, c->st));
+  {
+    // normals: compact rank of each location; pair p = (2p, 2p+1) is generated
+    // by the colour of 2p, pairs ordered by the compact rank of 2p
+    c->loc_rank.assign(n, 0);
+    for (int x = 0; x < n; ++x) c->loc_rank[L.compact_loc[x]] = x;
+    std::vector<int> pairs;
+    pairs.reserve((n + 1) / 2);
+    c->pair_ptr.assign(L.K + 1, 0);
+    for (int col = 0; col < L.K; ++col) {
+      for (int x = L.color_loc_ptr[col]; x < L.color_loc_ptr[col + 1]; ++x)
+        if ((L.compact_loc[x] & 1) == 0) pairs.push_back(L.compact_loc[x] >> 1);
+      c->pair_ptr[col + 1] = (int)pairs.size();
+    }
+    CK(upload(c->chunk_first_d, L.chunk_first.data(), L.chunk_first.size(), c->st));
+    CK(upload(c->loc_rank_d, c->loc_rank.data(), n, c->st));
+    CK(upload(c->pairs_d, pairs.data(), pairs.size(), c->st));
+    CK(hipStreamSynchronize(c->st));
+  }
   CK(upload(c->ent_pk_d, L.ent_pk.data(), (size_t)L.n_entries, c->st));
+  CK(upload(c->ent_pos_d, L.ent_pos.data(), (size_t)L.n_entries, c->st));
   CK(upload(c->ent_src_d, L.ent_src.data(), (size_t)L.n_entries, c->st));
   CK(hipMemsetAsync(c->ent_val_d, 0, sizeof(double) * std::max<long long>(1, L.n_entries * C), c->st));
   CK(hipMemcpyAsync(c->linv_cur_d, c->linv_cur_h, sizeof(double*) * C, hipMemcpyHostToDevice, c->st));
@@ -399,6 +434,11 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
   CK(upload(c->obs_idx_d, obs_idx.data(), n_obs, c->st));
   CK(upload(c->lm_d, lm_dev.data(), n_obs, c->st));
   CK(upload(c->y_d, observed_field, n_obs, c->st));
+  if (const char* pr = std::getenv("NNGP_PROBE"))
+    if (std::atoi(pr) == 9) {
+      CK(dalloc(&c->dbg_d, (size_t)L.nchunks * 8));
+      CK(hipMemset(c->dbg_d, 0, sizeof(unsigned long long) * L.nchunks * 8));
+    }
   CK(hipStreamSynchronize(c->st));
 #undef CK
   *out = c;
@@ -539,10 +579,10 @@ int nngp_get_precision_diag(nngp_ctx* c, double* D) {
   if (!c->ch[c->cur].have_factor[0]) return fail_msg(c, NNGP_ERR_STATE, "precision_diag: no factor");
   int rc;
   if ((rc = set_device(c))) return rc;
-  std::vector<double2> dr((size_t)c->n * c->C);
+  std::vector<double2> dr((size_t)c->lay.n_slots * c->C);
   HIPCHK(c, hipMemcpyAsync(dr.data(), c->dr_d, dr.size() * sizeof(double2), hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
-  for (int s = 0; s < c->n; ++s) D[c->lay.slot_loc[s]] = dr[(size_t)s * c->C + c->cur].x;
+  for (int i = 0; i < c->n; ++i) D[i] = dr[(size_t)c->lay.loc_slot[i] * c->C + c->cur].x;
   return NNGP_OK;
 }
 
@@ -581,7 +621,7 @@ int nngp_set_mu(nngp_ctx* c, const double* mu, double beta0) {
   if (mu) HIPCHK(c, hipMemcpyAsync(S.mu_d, mu, c->n_obs * sizeof(double), hipMemcpyHostToDevice, c->st));
   S.mu_is_const = (mu == nullptr);
   S.mu_beta0 = beta0;
-  HIPCHK(c, launch_residual_sums(c->st, c->n, sweep_dev(c), c->cur, c->obs_ptr_d, c->obs_idx_d, c->y_d,
+  HIPCHK(c, launch_residual_sums(c->st, (int)c->lay.n_slots, sweep_dev(c), c->cur, c->obs_ptr_d, c->obs_idx_d, c->y_d,
                                  mu ? S.mu_d : nullptr, beta0));
   HIPCHK(c, hipStreamSynchronize(c->st));
   S.have_mu = true;
@@ -615,7 +655,7 @@ static int sweep_prepare(nngp_ctx* c, int k, double beta0, double log_scale, dou
   }
   if (S.mu_is_const && S.mu_beta0 != beta0) {
     // residual sums depend on beta0 when mu = beta0
-    HIPCHK(c, launch_residual_sums(c->st, c->n, sweep_dev(c), k, c->obs_ptr_d, c->obs_idx_d, c->y_d,
+    HIPCHK(c, launch_residual_sums(c->st, (int)c->lay.n_slots, sweep_dev(c), k, c->obs_ptr_d, c->obs_idx_d, c->y_d,
                                    nullptr, beta0));
     S.mu_beta0 = beta0;
   }
@@ -641,7 +681,7 @@ static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, int mask, const double*
   const int n = c->n;
   for (int k = 0; k < c->C; ++k) {
     if (!((mask >> k) & 1)) continue;
-    HIPCHK(c, launch_field_to_slots(c->st, n, c->slot_dpos_d, c->ch[k].field_d, c->scal_d, c->w_slot_d, c->C, k));
+    HIPCHK(c, launch_field_to_slots(c->st, (int)c->lay.n_slots, c->slot_dpos_d, c->ch[k].field_d, c->scal_d, c->w_slot_d, c->C, k));
     // factor pointer and beta0 read from device memory so a replayed graph
     // sees the current factor and beta0
     launch_row_stats(c->st, nullptr, c->nn_d, n, c->b, c->ch[k].field_d, 0.0, c->r_d + k, c->partials_d,
@@ -649,18 +689,30 @@ static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, int mask, const double*
     HIPCHK(c, hipGetLastError());
   }
   SweepDev L = sweep_dev(c);
+  const size_t zn = (size_t)n * c->C;
+  // normals of sweep 0 (later sweeps' normals are generated inside the
+  // previous sweep's colour launches)
+  if (!z_dev) HIPCHK(c, launch_normals_compact(c->st, L, mask, 0, n, c->zbuf_d));
   for (int s = 0; s < n_sweeps; ++s) {
     for (int col = 0; col < c->lay.K; ++col) {
+      ColorLaunch a;
+      a.chunk0 = c->lay.color_chunk_ptr[col];
+      a.nch = c->lay.color_chunk_ptr[col + 1] - a.chunk0;
+      a.chain_mask = mask;
+      a.sweep_local = s;
+      a.z_cur = z_dev ? z_dev + (size_t)s * zn : c->zbuf_d + (size_t)(s & 1) * zn;
+      a.z_next = (!z_dev && s + 1 < n_sweeps) ? c->zbuf_d + (size_t)((s + 1) & 1) * zn : nullptr;
+      a.pairs = c->pairs_d + c->pair_ptr[col];
+      a.npairs = c->pair_ptr[col + 1] - c->pair_ptr[col];
+      a.n = n;
       if (evs) HIPCHK(c, hipEventRecord((*evs)[2 * ((size_t)s * c->lay.K + col)], c->st));
-      HIPCHK(c, launch_sweep_color(c->st, L, c->lay.color_chunk_ptr[col],
-                                   c->lay.color_chunk_ptr[col + 1] - c->lay.color_chunk_ptr[col], mask, s,
-                                   z_dev, n));
+      HIPCHK(c, launch_sweep_color(c->st, L, a));
       if (evs) HIPCHK(c, hipEventRecord((*evs)[2 * ((size_t)s * c->lay.K + col) + 1], c->st));
     }
   }
   for (int k = 0; k < c->C; ++k)
     if ((mask >> k) & 1)
-      HIPCHK(c, launch_slots_to_field(c->st, n, c->slot_dpos_d, c->w_slot_d, c->scal_d, c->ch[k].field_d, c->C, k));
+      HIPCHK(c, launch_slots_to_field(c->st, (int)c->lay.n_slots, c->slot_dpos_d, c->w_slot_d, c->scal_d, c->ch[k].field_d, c->C, k));
   return NNGP_OK;
 }
 
@@ -693,6 +745,7 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
   if ((rc = sweep_prepare(c, k, beta0, log_scale, lnv, seed, counter_base))) return rc;
   if ((rc = upload_scalars(c))) return rc;
   if (z) {
+    // injected normals -> compact order, chain-interleaved
     const size_t need = (size_t)n_sweeps * c->C * c->n;
     if (need > c->z_cap) {
       if (c->z_d) hipFree(c->z_d);
@@ -701,9 +754,12 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
       HIPCHK(c, dalloc(&c->z_d, need));
       c->z_cap = need;
     }
+    std::vector<double> zc(need, 0.0);
     for (int s = 0; s < n_sweeps; ++s)
-      HIPCHK(c, hipMemcpyAsync(c->z_d + ((size_t)s * c->C + k) * c->n, z + (size_t)s * c->n,
-                               c->n * sizeof(double), hipMemcpyHostToDevice, c->st));
+      for (int i = 0; i < c->n; ++i)
+        zc[((size_t)s * c->n + c->loc_rank[i]) * c->C + k] = z[(size_t)s * c->n + i];
+    HIPCHK(c, hipMemcpyAsync(c->z_d, zc.data(), need * sizeof(double), hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
     if ((rc = enqueue_sweep_body(c, n_sweeps, mask, c->z_d, nullptr))) return rc;
   } else {
     // replay a captured graph of the whole call (launch-bound at small n)
@@ -728,6 +784,17 @@ int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const doub
   if ((rc = graph_for(c, n_sweeps, (1 << c->C) - 1, &ex))) return rc;
   HIPCHK(c, hipGraphLaunch(ex, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
+  if (c->dbg_d) {
+    if (const char* path = std::getenv("NNGP_DBG_OUT")) {
+      std::vector<unsigned long long> h((size_t)c->lay.nchunks * 8);
+      HIPCHK(c, hipMemcpy(h.data(), c->dbg_d, h.size() * 8, hipMemcpyDeviceToHost));
+      if (FILE* f = std::fopen(path, "wb")) {
+        std::fwrite(c->lay.color_chunk_ptr.data(), sizeof(int), c->lay.K + 1, f);
+        std::fwrite(h.data(), 8, h.size(), f);
+        std::fclose(f);
+      }
+    }
+  }
   return NNGP_OK;
 }
 

@@ -374,58 +374,72 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
       return false;
     }
   }
-  // slots: colour-major, Morton order inside a colour
-  L.color_slot_ptr.assign(K + 1, 0);
-  for (int i = 0; i < n; ++i) L.color_slot_ptr[colors[i]]++;
-  for (int c = 0; c < K; ++c) L.color_slot_ptr[c + 1] += L.color_slot_ptr[c];
+  // locations of each colour in Morton order, packed greedily into chunks
+  // (<= cap cells, <= max_slots locations)
+  std::vector<int> cptr_col(K + 1, 0);
+  for (int i = 0; i < n; ++i) cptr_col[colors[i]]++;
+  for (int c = 0; c < K; ++c) cptr_col[c + 1] += cptr_col[c];
   for (int c = 0; c < K; ++c)
-    if (L.color_slot_ptr[c + 1] == L.color_slot_ptr[c]) { err = "coloring has an empty colour class"; return false; }
-  L.slot_loc.resize(n);
-  L.loc_slot.resize(n);
+    if (cptr_col[c + 1] == cptr_col[c]) { err = "coloring has an empty colour class"; return false; }
+  std::vector<int> by_col(n);
   {
-    std::vector<int> f(L.color_slot_ptr.begin(), L.color_slot_ptr.end() - 1);
-    for (int r = 0; r < n; ++r) { int i = perm[r]; L.slot_loc[f[colors[i] - 1]++] = i; }
-    for (int s2 = 0; s2 < n; ++s2) L.loc_slot[L.slot_loc[s2]] = s2;
+    std::vector<int> f(cptr_col.begin(), cptr_col.end() - 1);
+    for (int r = 0; r < n; ++r) { int i = perm[r]; by_col[f[colors[i] - 1]++] = i; }
   }
-  L.collen.resize(n);
-  L.slot_f0.resize(n);
-  for (int s2 = 0; s2 < n; ++s2) {
-    int i = L.slot_loc[s2];
-    L.collen[s2] = (int)(cptr[i + 1] - cptr[i]);
-  }
-  // chunks: greedy runs of whole slots (<= cap cells, <= max_slots slots)
+  L.SPC = 2 * LW;
+  std::vector<int> chunk_first;  // index into by_col of each chunk's first location
   L.color_chunk_ptr.assign(K + 1, 0);
-  L.chunk_slot0.clear();
   for (int c = 0; c < K; ++c) {
     int fill = 0, cnt = 0;
-    for (int s2 = L.color_slot_ptr[c]; s2 < L.color_slot_ptr[c + 1]; ++s2) {
-      const int len = L.collen[s2];
+    for (int x = cptr_col[c]; x < cptr_col[c + 1]; ++x) {
+      const int len = (int)(cptr[by_col[x] + 1] - cptr[by_col[x]]);
       if (cnt == 0 || fill + len > cap || cnt + 1 > max_slots) {
-        L.chunk_slot0.push_back(s2);
+        chunk_first.push_back(x);
         fill = 0;
         cnt = 0;
       }
-      L.slot_f0[s2] = fill;
       fill += len;
       ++cnt;
     }
-    L.color_chunk_ptr[c + 1] = (int)L.chunk_slot0.size();
+    L.color_chunk_ptr[c + 1] = (int)chunk_first.size();
   }
-  L.nchunks = (int)L.chunk_slot0.size();
-  L.chunk_slot0.push_back(n);
+  L.nchunks = (int)chunk_first.size();
+  chunk_first.push_back(n);
+  L.compact_loc = by_col;
+  L.color_loc_ptr = cptr_col;
+  L.chunk_first = chunk_first;
+  L.n_slots = (long long)L.nchunks * L.SPC;
   L.n_entries = (long long)L.nchunks * cap;
-  L.ent_pk.assign(L.n_entries, (int)((unsigned)kPadRow | ((unsigned)max_slots << kRowBits)));
+  L.slot_loc.assign(L.n_slots, -1);
+  L.collen.assign(L.n_slots, 0);
+  L.slot_f0.assign(L.n_slots, 0);
+  L.loc_slot.assign(n, -1);
+  L.ent_pk.assign(L.n_entries, 0);
   L.ent_src.assign(L.n_entries, -1);
+  L.ent_pos.assign(L.n_entries, 0);
+  struct Cell { int p, q, src, f; };
+  std::vector<Cell> cells;
   for (int ch = 0; ch < L.nchunks; ++ch) {
     const long long base = (long long)ch * cap;
-    for (int s2 = L.chunk_slot0[ch]; s2 < L.chunk_slot0[ch + 1]; ++s2) {
-      const int i = L.slot_loc[s2], q = s2 - L.chunk_slot0[ch];
-      long long f = L.slot_f0[s2];
-      for (long long p = cptr[i]; p < cptr[i + 1]; ++p, ++f) {
-        const long long e = base + (f % kRowsMax) * LW + f / kRowsMax;
-        L.ent_pk[e] = (int)((unsigned)L.rpos[crow[p]] | ((unsigned)q << kRowBits));
-        L.ent_src[e] = csrc[p];
-      }
+    cells.clear();
+    int f = 0;
+    for (int x = chunk_first[ch], q = 0; x < chunk_first[ch + 1]; ++x, ++q) {
+      const int i = by_col[x];
+      const long long s2 = (long long)ch * L.SPC + q;
+      L.slot_loc[s2] = i;
+      L.loc_slot[i] = (int)s2;
+      L.collen[s2] = (int)(cptr[i + 1] - cptr[i]);
+      L.slot_f0[s2] = f;
+      for (long long p = cptr[i]; p < cptr[i + 1]; ++p, ++f) cells.push_back({L.rpos[crow[p]], q, csrc[p], f});
+    }
+    // row order (rows are distinct inside a colour); padding cells last
+    std::sort(cells.begin(), cells.end(), [](const Cell& a, const Cell& b2) { return a.p < b2.p; });
+    for (int g = f; g < cap; ++g) cells.push_back({kPadRow, max_slots, -1, g});
+    for (int k = 0; k < cap; ++k) {
+      const long long e = base + k;
+      L.ent_pk[e] = (int)((unsigned)cells[k].p | ((unsigned)cells[k].q << kRowBits));
+      L.ent_src[e] = cells[k].src;
+      L.ent_pos[e] = (uint16_t)cells[k].f;
     }
   }
   return true;

@@ -37,17 +37,32 @@ constexpr int kPkPadRow = (1 << kPkRowBits) - 1;  // padding rowpos
 // arrays interleave the chains (slot*C + chain, row*C + chain) so the chains of
 // one entry share cache lines; ent_val is chain-planar (chain*n_entries + e).
 struct SweepDev {
-  const int* chunk_slot0;     // nchunks+1
-  const SlotShared* slots;    // n
-  double2* dr;                // n x C: {precision_diag, residuals_sum}
+  const SlotShared* slots;    // n_slots = nchunks * 2*LW (chunk-strided, holes: collen 0)
+  double2* dr;                // n_slots x C: {precision_diag, residuals_sum}
   const double* ent_val;      // C x n_entries
   const int* ent_pk;          // n_entries
-  double* w_slot;             // n x C
+  const uint16_t* ent_pos;    // n_entries: stream position of each (row-sorted) cell
+  double* w_slot;             // n_slots x C
   double* r;                  // n x C, Morton rows
   const SweepScalars* scal;   // C
   long long n_entries;
   int C;                      // chains in the context
-  int LW;                     // lanes per chain (64 / pow2ceil(C))
+  int LW;                     // lanes per chain (64 / pow2ceil(C)); 2*LW slots per chunk
+  const int* chunk_first;     // nchunks+1: compact index of each chunk's first slot
+  const int* loc_rank;        // n: compact index of each location (device row order independent)
+  unsigned long long* dbg;    // diagnostic timestamps (NNGP_PROBE=9 builds only), else null
+};
+
+// one colour launch of the sweep (+ the next sweep's normals of the colour)
+struct ColorLaunch {
+  int chunk0, nch;            // chunks of the colour
+  int chain_mask;
+  int sweep_local;            // sweep index inside the call
+  const double* z_cur;        // this sweep's normals, compact order x C
+  double* z_next;             // next sweep's normals (nullptr: none generated)
+  const int* pairs;           // pair ids whose normals this colour generates
+  int npairs;
+  int n;
 };
 
 // coordinate transform into the isotropic unit-range space (per covfun)
@@ -78,20 +93,22 @@ hipError_t launch_reduce4(hipStream_t st, const double* partials, int nblocks, d
 hipError_t launch_sell_refresh(hipStream_t st, const SweepDev& L, int nchunks, const int* ent_src,
                                const double* linv, int chain);
 
-// dr[s*C+chain].y = residuals_sum of the slot's observations
-hipError_t launch_residual_sums(hipStream_t st, int n, const SweepDev& L, int chain, const int* obs_ptr,
+// dr[s*C+chain].y = residuals_sum of the slot's observations (n_slots slots)
+hipError_t launch_residual_sums(hipStream_t st, int n_slots, const SweepDev& L, int chain, const int* obs_ptr,
                                 const int* obs_idx, const double* y, const double* mu, double beta0);
 
-// w[s*C+chain] = field[dpos[s]] - beta0 (and back)
+// w[s*C+chain] = field[dpos[s]] - beta0 (and back); n = n_slots, dpos -1 = hole
 hipError_t launch_field_to_slots(hipStream_t st, int n, const int* slot_dpos, const double* field,
                                  const SweepScalars* sc, double* w_slot, int C, int chain);
 hipError_t launch_slots_to_field(hipStream_t st, int n, const int* slot_dpos, const double* w_slot,
                                  const SweepScalars* sc, double* field, int C, int chain);
 
-// one colour of the chromatic sweep for the chains in chain_mask;
-// z (optional): injected normals z[((sweep*C) + chain) * n + loc]
-hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, int chunk0, int nch, int chain_mask,
-                              int sweep_local, const double* z, int n);
+// one colour of the chromatic sweep for the chains in a.chain_mask
+hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, const ColorLaunch& a);
+
+// normals of sweep (counter_base + sweep_off) for every location, compact order
+hipError_t launch_normals_compact(hipStream_t st, const SweepDev& L, int chain_mask, int sweep_off, int n,
+                                  double* z);
 
 // obs reductions: mode 0 -> partial[0] += (y - f[loc] - mu + beta0)^2
 //                 mode 1 -> partial[0] += ((y-b)^2 - (y-a)^2) / (2 sd^2),

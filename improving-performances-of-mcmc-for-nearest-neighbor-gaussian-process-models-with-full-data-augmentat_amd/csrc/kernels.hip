@@ -10,6 +10,7 @@
 //   obs_reduce_kernel                    A8  SSR, dnorm ratio
 //   tri_level_kernel                     (next) Matrix::solve by DAG level
 #include "kernels.h"
+#include <cstdlib>
 
 #include <cmath>
 
@@ -31,20 +32,28 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
   }
 }
 
-// N(0,1) for (seed, sweep, location): counter (loc, sweep_lo, sweep_hi, 0x5EED)
-__device__ __forceinline__ double normal_at(uint64_t seed, uint64_t sweep, uint32_t loc) {
-  uint32_t c[4] = {loc, (uint32_t)sweep, (uint32_t)(sweep >> 32), 0x5EEDu};
+// N(0,1) pair for locations 2p, 2p+1 of global sweep `sweep`: one Philox
+// call, counter (p, sweep_lo, sweep_hi, 0x5EED), key = seed; Box-Muller on its
+// two 53-bit uniforms: r cos(theta) -> 2p, r sin(theta) -> 2p+1.
+__device__ __forceinline__ void normal_pair(uint64_t seed, uint64_t sweep, uint32_t p, double& z0, double& z1) {
+  uint32_t c[4] = {p, (uint32_t)sweep, (uint32_t)(sweep >> 32), 0x5EEDu};
   philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
   uint64_t a = ((((uint64_t)c[1]) << 32) | c[0]) >> 11;
   uint64_t b = ((((uint64_t)c[3]) << 32) | c[2]) >> 11;
   double u1 = ((double)a + 0.5) * 0x1.0p-53;
   double u2 = (double)b * 0x1.0p-53;
-  return sqrt(-2.0 * log(u1)) * cos(6.283185307179586476925286766559 * u2);
+  const double r = sqrt(-2.0 * log(u1)), th = 6.283185307179586476925286766559 * u2;
+  z0 = r * cos(th);
+  z1 = r * sin(th);
 }
 
 __global__ void normals_kernel(uint64_t seed, uint64_t sweep, int n, double* z) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) z[i] = normal_at(seed, sweep, (uint32_t)i);
+  int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (2 * p >= n) return;
+  double z0, z1;
+  normal_pair(seed, sweep, (uint32_t)p, z0, z1);
+  z[2 * p] = z0;
+  if (2 * p + 1 < n) z[2 * p + 1] = z1;
 }
 
 // ------------------------------------------------------------------ Bessel K
@@ -475,48 +484,47 @@ hipError_t launch_reduce4(hipStream_t st, const double* partials, int nblocks, d
 }
 
 // ------------------------------------------------------------------ A5
-// Merge-path sweep layout (graph_prep.h): chunk ch of one chain is LW lanes x
-// kSweepRows rows; cell (lane l, row j) = stream position f = l*16 + j holds
-// entry ch*LW*16 + j*LW + l.  Slot q of the chunk covers stream cells
-// [f0_q, f0_q + len_q).
+// Merge-path sweep layout (graph_prep.h): chunk ch of one chain is LW*16
+// cells, sorted by row of B; cell k is entry ch*LW*16 + k and sits at stream
+// position ent_pos (slot q of the chunk covers stream [f0_q, f0_q + len_q)).
 
-// refresh chain `chain`'s B values in the sweep layout (one lane per cell)
-// and precision_diag (one lane per slot, entries summed in row order)
+// refresh chain `chain`'s B values in the sweep layout and precision_diag
+// (entries of a column summed in stream = row order); one wavefront per chunk
 template <int LW>
 __global__ __launch_bounds__(256) void sell_refresh_kernel(SweepDev L, int nchunks,
                                                            const int* __restrict__ ent_src,
                                                            const double* __restrict__ linv, int chain) {
-  // a wave covers 64/LW chunks: lanes [g*LW, (g+1)*LW) take chunk wave*(64/LW) + g
-  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int chk = wave * (64 / LW) + lane / LW;
-  const int l = lane % LW;
+  constexpr int CAP = LW * kSweepRows;
+  __shared__ double sq_s[4][CAP];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int chk = blockIdx.x * 4 + wv;
   if (chk >= nchunks) return;
-  const long long base = (long long)chk * LW * kSweepRows;
+  double* sq = sq_s[wv];
+  const long long base = (long long)chk * CAP;
   double* val = const_cast<double*>(L.ent_val) + (size_t)chain * L.n_entries;
-#pragma unroll
-  for (int j = 0; j < kSweepRows; ++j) {
-    const long long e = base + (long long)j * LW + l;
+  for (int k = lane; k < CAP; k += 64) {
+    const long long e = base + k;
     const int src = ent_src[e];
-    val[e] = src >= 0 ? linv[src] : 0.0;
+    const double v = src >= 0 ? linv[src] : 0.0;
+    val[e] = v;
+    sq[L.ent_pos[e]] = v * v;
   }
-  const int s0 = L.chunk_slot0[chk], nsl = L.chunk_slot0[chk + 1] - s0;
-  for (int t = l; t < nsl; t += LW) {
-    const SlotShared sh = L.slots[s0 + t];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (int t = lane; t < 2 * LW; t += 64) {
+    const long long s = (long long)chk * 2 * LW + t;
+    const SlotShared sh = L.slots[s];
+    if (sh.collen == 0) continue;
     double D = 0.0;
-    for (int f = sh.f0; f < sh.f0 + sh.collen; ++f) {
-      const double v = linv[ent_src[base + (long long)(f % kSweepRows) * LW + f / kSweepRows]];
-      D += v * v;
-    }
-    L.dr[(size_t)(s0 + t) * L.C + chain].x = D;
+    for (int f = sh.f0; f < sh.f0 + sh.collen; ++f) D += sq[f];
+    L.dr[(size_t)s * L.C + chain].x = D;
   }
 }
 
 hipError_t launch_sell_refresh(hipStream_t st, const SweepDev& L, int nchunks, const int* ent_src,
                                const double* linv, int chain) {
-  const int per_wave = 64 / L.LW;
-  const int waves = (nchunks + per_wave - 1) / per_wave;
-  const int g = (waves + 3) / 4;
+  const int g = (nchunks + 3) / 4;
   if (g == 0) return hipSuccess;
   switch (L.LW) {
     case 64: hipLaunchKernelGGL(sell_refresh_kernel<64>, dim3(g), dim3(kBlock), 0, st, L, nchunks, ent_src, linv, chain); break;
@@ -535,6 +543,7 @@ __global__ void residual_sums_kernel(int n, SweepDev L, int chain,
   int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;
   int loc = L.slots[s].loc;
+  if (loc < 0) return;  // hole
   double R = 0.0;
   for (int p = obs_ptr[loc]; p < obs_ptr[loc + 1]; ++p) {
     int o = obs_idx[p];
@@ -556,14 +565,14 @@ __global__ void field_to_slots_kernel(int n, const int* __restrict__ slot_dpos,
                                       const SweepScalars* __restrict__ sc, double* __restrict__ w,
                                       int C) {
   int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < n) w[(size_t)s * C] = field[slot_dpos[s]] - sc->beta0;
+  if (s < n && slot_dpos[s] >= 0) w[(size_t)s * C] = field[slot_dpos[s]] - sc->beta0;
 }
 __global__ void slots_to_field_kernel(int n, const int* __restrict__ slot_dpos,
                                       const double* __restrict__ w,
                                       const SweepScalars* __restrict__ sc, double* __restrict__ field,
                                       int C) {
   int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < n) field[slot_dpos[s]] = w[(size_t)s * C] + sc->beta0;
+  if (s < n && slot_dpos[s] >= 0) field[slot_dpos[s]] = w[(size_t)s * C] + sc->beta0;
 }
 
 hipError_t launch_field_to_slots(hipStream_t st, int n, const int* slot_dpos, const double* field,
@@ -582,171 +591,239 @@ hipError_t launch_slots_to_field(hipStream_t st, int n, const int* slot_dpos, co
 }
 
 // ------------------------------------------------------------------ A1
+// Normals of one sweep in compact order, chain-interleaved:
+// z[(rank[loc]) * C + chain].  Work item = (pair p of a pair list, chain);
+// chains outside chain_mask are skipped.
+__device__ __forceinline__ void gen_normals(int item, const int* __restrict__ pairs, int npairs,
+                                            const SweepScalars* __restrict__ scal, int C, int chain_mask,
+                                            uint64_t sweep_off, const int* __restrict__ loc_rank, int n,
+                                            double* __restrict__ z) {
+  if (item >= npairs * C) return;
+  const int chain = item % C;
+  if (!((chain_mask >> chain) & 1)) return;
+  const int p = pairs ? pairs[item / C] : item / C;
+  double z0, z1;
+  normal_pair(scal[chain].seed, scal[chain].counter_base + sweep_off, (uint32_t)p, z0, z1);
+  z[(size_t)loc_rank[2 * p] * C + chain] = z0;
+  if (2 * p + 1 < n) z[(size_t)loc_rank[2 * p + 1] * C + chain] = z1;
+}
+
+__global__ __launch_bounds__(256) void normals_compact_kernel(SweepDev L, int chain_mask, int sweep_off,
+                                                              int n, double* z) {
+  gen_normals(blockIdx.x * blockDim.x + threadIdx.x, nullptr, (n + 1) / 2, L.scal, L.C, chain_mask,
+              (uint64_t)sweep_off, L.loc_rank, n, z);
+}
+
+hipError_t launch_normals_compact(hipStream_t st, const SweepDev& L, int chain_mask, int sweep_off, int n,
+                                  double* z) {
+  const long long items = (long long)((n + 1) / 2) * L.C;
+  const int g = (int)((items + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(normals_compact_kernel, dim3(g), dim3(kBlock), 0, st, L, chain_mask, sweep_off, n, z);
+  return hipGetLastError();
+}
+
 // One colour of the chromatic sweep, local form, for up to 4 chains at once:
 //   acc  = sum_{k in col(i)} B[k,i] r_k - D_i w_i      (= (B^T B w_{!c})_i)
 //   P    = D_i/s2 + n_i/t2
 //   w_i' = (R_i/t2 - acc/s2)/P + z_i/sqrt(P)
 //   r_k += B[k,i] (w_i' - w_i)
-// One wavefront per chunk; its 64/LW chain groups run the same chunk for
-// different chains (same entry cells, chain-interleaved r / w / {D,R}).
-//  1. every lane loads its 16 cells (coalesced, address = chunk index only) and
-//     gathers r at their rows;
-//  2. segmented sums along the lane's cells: a slot that lies inside the lane
-//     goes to acc[q]; the part of a slot that continues from the previous lane
-//     goes to head[lane], the part that continues into the next lane to
-//     tail[lane] (LDS, per chain group);
-//  3. one owner lane per slot (q = lane, lane + LW): acc = tail[l0] +
-//     head[l0+1] + ... + head[l1] in lane order (deterministic), the Gibbs
-//     draw, dw[q] -> LDS;
-//  4. every cell scatters r_k += B[k,i] dw[q].
+// Workgroups [0, gs) sweep: one wavefront per chunk; its 64/LW chain groups
+// run the same chunk for different chains (same entry cells,
+// chain-interleaved r / w / {D,R} / z).
+//  1. round trip 1: the lane's 16 cells (row-sorted: one instruction's
+//     lanes cover consecutive rows), the records of the two slots it owns
+//     (q = lane, lane + LW) and the chunk's first compact index -- all
+//     addressed by the chunk index alone;
+//  2. round trip 2: r gathered at the cells' rows (a few lines per
+//     instruction); the owned slots' normals;
+//  3. products B[k,i] r_k regrouped by stream position in LDS; lane l then
+//     runs along stream cells l*16 .. l*16+15, restarting where a new slot
+//     begins, and stores every running sum (LDS rows padded against bank
+//     conflicts);
+//  4. owner of slot q: acc = its run ending in its last cell, plus the lane
+//     totals of the lanes it spans before that (in lane order: deterministic);
+//     the draw; dw[q] -> LDS;
+//  5. every cell scatters r_k += B[k,i] dw[q] (again a few lines per
+//     instruction).
+// Workgroups [gs, gs + gz) generate the NEXT sweep's normals of this
+// colour's pairs (z_next) on the SIMD time the latency-bound sweep waves
+// leave idle; the next sweep reads them >= K launches later.
 // Slots of one colour share no row of B, so the scatter is conflict-free.
-// Blocks are remapped so that consecutive (spatially adjacent) chunks run on
-// the same XCD and share its L2 for the r gathers.
+// Sweep blocks are remapped so that consecutive (spatially adjacent) chunks
+// run on the same XCD and share its L2 for the r gathers.
+// PROBE 9 (diagnostic build, NNGP_PROBE=9): per-phase s_memtime stamps.
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <bool INJECT, int LW>
-__global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, int chunk0, int nch, int chain_mask,
-                                                          int sweep_local, const double* __restrict__ z,
-                                                          int n) {
+constexpr int kCellStride = kSweepRows + 1;  // LDS row pitch (doubles): lanes hit distinct banks
+
+template <int LW, int PROBE = 0>
+__global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, ColorLaunch a) {
   constexpr int CG = 64 / LW;  // chain groups per wavefront
-  __shared__ double lds[4][CG][6 * LW];
-  const int nb = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, qq = nb >> 3, rm = nb & 7;
+  constexpr int SPC = 2 * LW;  // slot ids per chunk
+  __shared__ double cells_s[4][CG][LW * kCellStride];
+  __shared__ unsigned char qs_s[4][CG][LW * kSweepRows];
+  __shared__ double dw_s[4][CG][SPC];
+  const int gs = (a.nch + 3) / 4;
+  if ((int)blockIdx.x >= gs) {
+    gen_normals(((int)blockIdx.x - gs) * 256 + threadIdx.x, a.pairs, a.npairs, L.scal, L.C, a.chain_mask,
+                (uint64_t)a.sweep_local + 1, L.loc_rank, a.n, a.z_next);
+    return;
+  }
+  unsigned long long stamp[8];
+#define STAMP(k)                                                      \
+  do {                                                                \
+    if (PROBE == 9) {                                                 \
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");     \
+      stamp[k] = __builtin_amdgcn_s_memtime();                        \
+    }                                                                 \
+  } while (0)
+  if (PROBE == 9) stamp[7] = __builtin_amdgcn_s_memrealtime();
+  STAMP(0);
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, qq = gs >> 3, rm = gs & 7;
   const int lb = (xcd < rm ? xcd * (qq + 1) : rm * (qq + 1) + (xcd - rm) * qq) + (bid >> 3);
   const int wv = threadIdx.x >> 6;
   const int lch = lb * 4 + wv;
-  if (lch >= nch) return;
+  if (lch >= a.nch) return;
   const int lane = threadIdx.x & 63;
   const int cg = lane / LW, l = lane % LW;
   const int C = L.C;
-  if (cg >= C || !((chain_mask >> cg) & 1)) return;
+  if (cg >= C || !((a.chain_mask >> cg) & 1)) return;
   const int chain = cg;
-  double* acc_s = lds[wv][cg];        // [2*LW]: per-slot sums, then dw
-  double* head_s = acc_s + 2 * LW;    // [LW]
-  double* tail_s = head_s + LW;       // [LW]
-  const int ch = chunk0 + lch;
+  double* cells = cells_s[wv][cg];
+  unsigned char* qs = qs_s[wv][cg];
+  double* dws = dw_s[wv][cg];
+  const int ch = a.chunk0 + lch;
   const long long base = (long long)ch * LW * kSweepRows;
+  const long long sbase = (long long)ch * SPC;
   const double* val = L.ent_val + (size_t)chain * L.n_entries;
   double* r = L.r;  // gathered then scattered: no __restrict__
-  // round trip 1: the lane's cells (address from the chunk index only) + chunk slot range
+  // round trip 1
   double v[kSweepRows], rv[kSweepRows];
-  int pk[kSweepRows];
+  int pk[kSweepRows], ps[kSweepRows];
 #pragma unroll
   for (int j = 0; j < kSweepRows; ++j) {
     const long long e = base + (long long)j * LW + l;
     v[j] = val[e];
     pk[j] = L.ent_pk[e];
-  }
-  const int s0 = L.chunk_slot0[ch];
-  const int nsl = L.chunk_slot0[ch + 1] - s0;
-  // round trip 2: r gathers + the owned slots' records (independent of each other)
-#pragma unroll
-  for (int j = 0; j < kSweepRows; ++j) {
-    const int p = pk[j] & kPkPadRow;
-    rv[j] = (p != kPkPadRow) ? r[(size_t)p * C + chain] : 0.0;
+    ps[j] = L.ent_pos[e];
   }
   SlotShared sh[2];
   double2 dr[2];
   double w[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    const int t = l + u * LW;
-    const int s = s0 + min(t, nsl - 1);
+    const long long s = sbase + l + u * LW;
     sh[u] = L.slots[s];
     dr[u] = L.dr[(size_t)s * C + chain];
     w[u] = L.w_slot[(size_t)s * C + chain];
   }
+  const int cfirst = L.chunk_first[ch];
   const SweepScalars* scal = L.scal + chain;
   const double inv_s2 = scal->inv_s2, inv_t2 = scal->inv_t2;
-  // segmented sums along the lane's cells
-  int q[kSweepRows];
-#pragma unroll
-  for (int j = 0; j < kSweepRows; ++j) q[j] = (int)((unsigned)pk[j] >> kPkRowBits);
-  const int dummy = 2 * LW - 1;
-  const int q_prev_last = __shfl(q[kSweepRows - 1], lane - 1, 64);
-  const int q_next_first = __shfl(q[0], lane + 1, 64);
-  const bool started_before = l > 0 && q[0] != dummy && q[0] == q_prev_last;
-  const bool continues_after = l < LW - 1 && q[kSweepRows - 1] != dummy && q[kSweepRows - 1] == q_next_first;
-  double seg = 0.0;
-  bool first = true;
-#pragma unroll
-  for (int j = 0; j < kSweepRows; ++j) {
-    seg += v[j] * rv[j];
-    const bool end_here = (j == kSweepRows - 1) || (q[j] != q[j + 1 < kSweepRows ? j + 1 : j]);
-    if (end_here) {
-      if (first && started_before) head_s[l] = seg;
-      else if (j == kSweepRows - 1 && continues_after) tail_s[l] = seg;
-      else acc_s[q[j]] = seg;
-      seg = 0.0;
-      first = false;
-    }
-  }
-  wave_lds_sync();
-  // owner lanes: the Gibbs draw of slots q = l and q = l + LW
-  double dwv[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int t = l + u * LW;
-    dwv[u] = 0.0;
-    if (t < nsl) {
-      const int f0 = sh[u].f0, len = sh[u].collen;
-      const int l0 = f0 / kSweepRows, l1 = (f0 + len - 1) / kSweepRows;
-      double acc;
-      if (l0 == l1) {
-        acc = acc_s[t];
-      } else {
-        acc = tail_s[l0];
-        for (int ll = l0 + 1; ll <= l1; ++ll) acc += head_s[ll];
-      }
-      double zz;
-      if (INJECT) zz = z[((size_t)sweep_local * C + chain) * n + sh[u].loc];
-      else zz = normal_at(scal->seed, scal->counter_base + (uint64_t)sweep_local, (uint32_t)sh[u].loc);
-      acc -= dr[u].x * w[u];
-      const double P = dr[u].x * inv_s2 + (double)sh[u].nobs * inv_t2;
-      const double wn = (inv_t2 * dr[u].y - inv_s2 * acc) / P + zz / sqrt(P);
-      dwv[u] = wn - w[u];
-      L.w_slot[(size_t)(s0 + t) * C + chain] = wn;
-    }
-  }
-  // acc[t] is read and then overwritten by its owner lane only
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-    if (l + u * LW < nsl) acc_s[l + u * LW] = dwv[u];
-  wave_lds_sync();
+  if (PROBE == 9) { double x = sh[0].loc + sh[1].loc + dr[0].x + w[0] + cfirst; for (int j = 0; j < kSweepRows; ++j) x += v[j] + pk[j]; if (x == 12345.678) stamp[0] = 0; }
+  STAMP(1);
+  // round trip 2: gathers + normals
 #pragma unroll
   for (int j = 0; j < kSweepRows; ++j) {
     const int p = pk[j] & kPkPadRow;
-    if (p != kPkPadRow) r[(size_t)p * C + chain] = rv[j] + v[j] * acc_s[q[j]];
+    rv[j] = (p != kPkPadRow) ? r[(size_t)p * C + chain] : 0.0;
   }
+  double zz[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+    zz[u] = sh[u].collen > 0 ? a.z_cur[(size_t)(cfirst + l + u * LW) * C + chain] : 0.0;
+  // w' = (R/t2 - (acc - D w)/s2) / P + z / sqrt(P): everything but acc and z
+  double cR[2], invP[2], isP[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const double P = dr[u].x * inv_s2 + (double)sh[u].nobs * inv_t2;
+    invP[u] = sh[u].collen > 0 ? 1.0 / P : 0.0;
+    isP[u] = sh[u].collen > 0 ? 1.0 / sqrt(P) : 0.0;
+    cR[u] = inv_t2 * dr[u].y + inv_s2 * (dr[u].x * w[u]);
+  }
+  if (PROBE == 9) { double x = zz[0] + zz[1] + cR[0] + invP[0] + isP[0]; for (int j = 0; j < kSweepRows; ++j) x += rv[j]; if (x == 12345.678) stamp[0] = 0; }
+  STAMP(2);
+  // products regrouped by stream position, then running sums along the
+  // lane's stream cells, restarted at every slot start
+  int q[kSweepRows];
+#pragma unroll
+  for (int j = 0; j < kSweepRows; ++j) {
+    q[j] = (int)((unsigned)pk[j] >> kPkRowBits);
+    cells[(ps[j] / kSweepRows) * kCellStride + ps[j] % kSweepRows] = v[j] * rv[j];
+    qs[ps[j]] = (unsigned char)q[j];
+  }
+  wave_lds_sync();
+  {
+    double run = 0.0;
+    int qprev = -1;
+#pragma unroll
+    for (int j = 0; j < kSweepRows; ++j) {
+      const double x = cells[l * kCellStride + j];
+      const int qq = qs[l * kSweepRows + j];
+      run = (qq == qprev) ? run + x : x;
+      qprev = qq;
+      cells[l * kCellStride + j] = run;
+    }
+  }
+  wave_lds_sync();
+  STAMP(3);
+  // owners: the Gibbs draw of slots q = l and q = l + LW
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (sh[u].collen > 0) {
+      const int t = l + u * LW;
+      const int f0 = sh[u].f0, fe = f0 + sh[u].collen - 1;
+      const int l0 = f0 / kSweepRows, l1 = fe / kSweepRows;
+      double acc;
+      if (l0 == l1) {
+        acc = cells[l1 * kCellStride + fe % kSweepRows];
+      } else {
+        acc = cells[l0 * kCellStride + kSweepRows - 1];
+        for (int ll = l0 + 1; ll < l1; ++ll) acc += cells[ll * kCellStride + kSweepRows - 1];
+        acc += cells[l1 * kCellStride + fe % kSweepRows];
+      }
+      const double wn = (cR[u] - inv_s2 * acc) * invP[u] + zz[u] * isP[u];
+      dws[t] = wn - w[u];
+      L.w_slot[(size_t)(sbase + t) * C + chain] = wn;
+    }
+  }
+  wave_lds_sync();
+  STAMP(4);
+#pragma unroll
+  for (int j = 0; j < kSweepRows; ++j) {
+    const int p = pk[j] & kPkPadRow;
+    if (p != kPkPadRow) r[(size_t)p * C + chain] = rv[j] + v[j] * dws[q[j]];
+  }
+  STAMP(5);
+  if (PROBE == 9 && l == 0 && chain == 0) {
+    unsigned long long* o = L.dbg + (size_t)ch * 8;
+    for (int k = 0; k < 6; ++k) o[k] = stamp[k];
+    o[6] = 0;
+    o[7] = stamp[7];
+  }
+#undef STAMP
 }
 
-hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, int chunk0, int nch, int chain_mask,
-                              int sweep_local, const double* z, int n) {
-  const int g = (nch + 3) / 4;
-  if (g == 0) return hipSuccess;
-#define NNGP_SWEEP_LAUNCH(I, W)                                                                     \
-  hipLaunchKernelGGL((sweep_color_kernel<I, W>), dim3(g), dim3(kBlock), 0, st, L, chunk0, nch,     \
-                     chain_mask, sweep_local, z, n)
-  if (z) {
-    switch (L.LW) {
-      case 64: NNGP_SWEEP_LAUNCH(true, 64); break;
-      case 32: NNGP_SWEEP_LAUNCH(true, 32); break;
-      case 16: NNGP_SWEEP_LAUNCH(true, 16); break;
-      default: return hipErrorInvalidValue;
-    }
-  } else {
-    switch (L.LW) {
-      case 64: NNGP_SWEEP_LAUNCH(false, 64); break;
-      case 32: NNGP_SWEEP_LAUNCH(false, 32); break;
-      case 16: NNGP_SWEEP_LAUNCH(false, 16); break;
-      default: return hipErrorInvalidValue;
-    }
+hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, const ColorLaunch& a) {
+  const int gs = (a.nch + 3) / 4;
+  const int gz = a.z_next ? (int)(((long long)a.npairs * L.C + 255) / 256) : 0;
+  if (gs + gz == 0) return hipSuccess;
+  static const int probe = [] { const char* e = std::getenv("NNGP_PROBE"); return e ? std::atoi(e) : 0; }();
+  if (probe == 9 && L.LW == 64 && L.dbg) {
+    hipLaunchKernelGGL((sweep_color_kernel<64, 9>), dim3(gs + gz), dim3(kBlock), 0, st, L, a);
+    return hipGetLastError();
   }
-#undef NNGP_SWEEP_LAUNCH
+  switch (L.LW) {
+    case 64: hipLaunchKernelGGL((sweep_color_kernel<64>), dim3(gs + gz), dim3(kBlock), 0, st, L, a); break;
+    case 32: hipLaunchKernelGGL((sweep_color_kernel<32>), dim3(gs + gz), dim3(kBlock), 0, st, L, a); break;
+    case 16: hipLaunchKernelGGL((sweep_color_kernel<16>), dim3(gs + gz), dim3(kBlock), 0, st, L, a); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
@@ -837,7 +914,7 @@ hipError_t launch_spin(hipStream_t st, double seconds) {
 }
 
 hipError_t launch_normals(hipStream_t st, uint64_t seed, uint64_t sweep, int n, double* z) {
-  int g = (n + kBlock - 1) / kBlock;
+  int g = ((n + 1) / 2 + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(normals_kernel, dim3(g), dim3(kBlock), 0, st, seed, sweep, n, z);
   return hipGetLastError();
 }

@@ -64,10 +64,11 @@ void or_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out
 }
 
 /* Standard normal for location `loc` (0-based) in global sweep `sweep` with
- * 64-bit `seed`: counter = (loc, sweep_lo, sweep_hi, 0x5EEDu), key = seed;
- * Box-Muller on two 53-bit uniforms. */
+ * 64-bit `seed`: locations 2p and 2p+1 share one Philox call, counter =
+ * (p, sweep_lo, sweep_hi, 0x5EEDu), key = seed; Box-Muller on its two 53-bit
+ * uniforms gives r cos(theta) to the even and r sin(theta) to the odd one. */
 double or_normal(uint64_t seed, uint64_t sweep, uint32_t loc) {
-  uint32_t ctr[4] = {loc, (uint32_t)sweep, (uint32_t)(sweep >> 32), 0x5EEDu};
+  uint32_t ctr[4] = {loc >> 1, (uint32_t)sweep, (uint32_t)(sweep >> 32), 0x5EEDu};
   uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
   uint32_t o[4];
   or_philox4x32_10(ctr, key, o);
@@ -75,7 +76,8 @@ double or_normal(uint64_t seed, uint64_t sweep, uint32_t loc) {
   uint64_t b = (((uint64_t)o[3] << 32) | o[2]) >> 11;
   double u1 = ((double)a + 0.5) * 0x1.0p-53;   /* (0,1) */
   double u2 = (double)b * 0x1.0p-53;           /* [0,1) */
-  return sqrt(-2.0 * log(u1)) * cos(6.283185307179586476925286766559 * u2);
+  double r = sqrt(-2.0 * log(u1)), th = 6.283185307179586476925286766559 * u2;
+  return (loc & 1u) ? r * sin(th) : r * cos(th);
 }
 
 void or_normals(uint64_t seed, uint64_t sweep, int n, double *z) {

@@ -1,7 +1,7 @@
 // Invariants of the sweep layout planner (graph_prep.cpp), checked on CPU:
-// every nonzero B[k,i] appears exactly once, in its slot's stream range, at
-// the closed-form address the sweep kernel computes (fixed chunk stride,
-// lane-major stream); padding is inert and only at the stream tail.  Usage:
+// every nonzero B[k,i] appears exactly once, in its slot's stream range
+// (through ent_pos), in a chunk whose cells are sorted by row; padding is
+// inert and only at the stream tail.  Usage:
 //   layout_check <n> <m> <lanes_per_chain> <seed>   (prints "ok <stats>")
 #include <cstdio>
 #include <cstdlib>
@@ -9,6 +9,7 @@
 #include <set>
 #include <string>
 #include <vector>
+#include <algorithm>
 
 #include "graph_prep.h"
 
@@ -54,46 +55,62 @@ int main(int argc, char** argv) {
       ++nnz;
     }
   REQUIRE(nnz == L.nnz);
-  const int cap = LW * kRowsMax, dummy = 2 * LW - 1;
+  const int cap = LW * kRowsMax, dummy = 2 * LW - 1, SPC = 2 * LW;
+  REQUIRE(L.SPC == SPC);
   REQUIRE(L.n_entries == (long long)L.nchunks * cap);
-  REQUIRE(L.chunk_slot0[L.nchunks] == n);
-  std::vector<char> used((size_t)L.n_entries, 0);
+  REQUIRE(L.n_slots == (long long)L.nchunks * SPC);
   long long found = 0;
+  int located = 0;
+  std::vector<long long> at(cap);  // stream position -> entry
   for (int c = 0; c < K; ++c) {
-    REQUIRE(L.chunk_slot0[L.color_chunk_ptr[c]] == L.color_slot_ptr[c]);
     for (int ch = L.color_chunk_ptr[c]; ch < L.color_chunk_ptr[c + 1]; ++ch) {
-      const int s0 = L.chunk_slot0[ch], s1 = L.chunk_slot0[ch + 1];
-      REQUIRE(s1 > s0 && s1 - s0 <= 2 * LW - 1);
-      REQUIRE(s1 <= L.color_slot_ptr[c + 1]);
       const long long base = (long long)ch * cap;  // the kernel's closed form
-      int f = 0;
-      for (int s = s0; s < s1; ++s) {
-        const int i = L.slot_loc[s], q = s - s0;
+      std::fill(at.begin(), at.end(), -1);
+      int prev_row = -1;
+      for (int k = 0; k < cap; ++k) {
+        const long long e = base + k;
+        const int f = L.ent_pos[e];
+        REQUIRE(f < cap && at[f] < 0);  // a permutation of the stream
+        at[f] = e;
+        const int row = L.ent_pk[e] & kPadRow;
+        REQUIRE(row > prev_row || row == kPadRow);  // sorted by row, padding last
+        if (row != kPadRow) prev_row = row;
+      }
+      int f = 0, q = 0;
+      for (; q < SPC; ++q) {
+        const long long s = (long long)ch * SPC + q;
+        const int i = L.slot_loc[s];
+        if (i < 0) break;
+        ++located;
+        REQUIRE(q < SPC - 1);
         REQUIRE(col[i] == c + 1);
+        REQUIRE(L.loc_slot[i] == s);
         REQUIRE(L.slot_f0[s] == f);
         const int len = L.collen[s];
         REQUIRE(len == (int)want[i].size());
         for (int t = 0; t < len; ++t, ++f) {
-          const long long e = base + (long long)(f % kRowsMax) * LW + f / kRowsMax;
-          REQUIRE(!used[e]);
-          used[e] = 1;
+          const long long e = at[f];
           const int pk = L.ent_pk[e];
           REQUIRE((int)((unsigned)pk >> kRowBits) == q);
           REQUIRE(want[i].count({pk & kPadRow, L.ent_src[e]}) == 1);
           ++found;
         }
       }
+      REQUIRE(q >= 1);
+      for (int q2 = q; q2 < SPC; ++q2) {  // holes
+        const long long s = (long long)ch * SPC + q2;
+        REQUIRE(L.slot_loc[s] == -1 && L.collen[s] == 0);
+      }
       REQUIRE(f <= cap);
-      for (int g = f; g < cap; ++g) {  // padding tail
-        const long long e = base + (long long)(g % kRowsMax) * LW + g / kRowsMax;
-        REQUIRE(!used[e]);
+      for (int g = f; g < cap; ++g) {  // padding tail of the stream
+        const long long e = at[g];
         REQUIRE((L.ent_pk[e] & kPadRow) == kPadRow && (int)((unsigned)L.ent_pk[e] >> kRowBits) == dummy);
         REQUIRE(L.ent_src[e] == -1);
       }
     }
   }
   REQUIRE(found == nnz);
-  for (int i = 0; i < n; ++i) REQUIRE(L.slot_loc[L.loc_slot[i]] == i);
+  REQUIRE(located == n);
   std::printf("ok K=%d nnz=%lld entries=%lld chunks=%d max_collen=%d\n", K, nnz, L.n_entries, L.nchunks,
               L.max_collen);
   return 0;
