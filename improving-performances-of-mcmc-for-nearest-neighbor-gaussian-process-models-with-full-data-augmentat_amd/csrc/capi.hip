@@ -56,7 +56,8 @@ struct nngp_ctx {
   const double** linv_cur_d = nullptr;  // C pointers: current factor of each chain
   const double** linv_cur_h = nullptr;  // pinned mirror
   int* fail_d = nullptr;
-  SlotShared* slots_d = nullptr;
+  int2* sinfo_d = nullptr;       // n compact: {obs_per_loc, f0 | collen << 16}
+  int* compact_loc_d = nullptr;  // n
   double2* dr_d = nullptr;
   int* slot_dpos_d = nullptr;
   int* chunk_first_d = nullptr;  // nchunks+1
@@ -67,6 +68,7 @@ struct nngp_ctx {
   double* zbuf_d = nullptr;      // 2 x n x C: normals of the current / next sweep
   int* ent_pk_d = nullptr;
   uint16_t* ent_pos_d = nullptr;
+  uint16_t* start_mask_d = nullptr;
   int* ent_src_d = nullptr;
   double* ent_val_d = nullptr;   // C x n_entries
   double* w_slot_d = nullptr;    // n x C
@@ -132,11 +134,13 @@ int set_device(nngp_ctx* c) {
 // sweep-layout pointers
 SweepDev sweep_dev(nngp_ctx* c) {
   SweepDev L;
-  L.slots = c->slots_d;
+  L.sinfo = c->sinfo_d;
+  L.compact_loc = c->compact_loc_d;
   L.dr = c->dr_d;
   L.ent_val = c->ent_val_d;
   L.ent_pk = c->ent_pk_d;
   L.ent_pos = c->ent_pos_d;
+  L.start_mask = c->start_mask_d;
   L.w_slot = c->w_slot_d;
   L.r = c->r_d;
   L.scal = c->scal_d;
@@ -243,11 +247,11 @@ void nngp_ctx_destroy(nngp_ctx* c) {
   if (c->st) hipStreamSynchronize(c->st);
   for (auto& kv : c->graphs) hipGraphExecDestroy(kv.second);
   for (auto g : c->graph_objs) hipGraphDestroy(g);
-  std::vector<void*> ptrs = {c->locs_d, c->sc_d, c->nn_d, c->linv_cur_d, c->fail_d, c->slots_d,
+  std::vector<void*> ptrs = {c->locs_d, c->sc_d, c->nn_d, c->linv_cur_d, c->fail_d, c->sinfo_d, c->compact_loc_d,
                              c->dr_d, c->slot_dpos_d, c->ent_pk_d, c->ent_src_d, c->ent_val_d, c->w_slot_d,
                              c->r_d, c->level_rows_d, c->obs_ptr_d, c->obs_idx_d, c->lm_d, c->y_d, c->tmp_d,
                              c->tmp2_d, c->partials_d, c->res_d, c->z_d, c->scal_d, c->dbg_d,
-                             c->chunk_first_d, c->loc_rank_d, c->pairs_d, c->zbuf_d, c->ent_pos_d};
+                             c->chunk_first_d, c->loc_rank_d, c->pairs_d, c->zbuf_d, c->ent_pos_d, c->start_mask_d};
   for (int k = 0; k < kMaxChains; ++k) {
     ChainState& s = c->ch[k];
     ptrs.insert(ptrs.end(), {s.linv_d[0], s.linv_d[1], s.field_d, s.field_prop_d, s.mu_d});
@@ -311,6 +315,7 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
     std::vector<int> f(obs_cnt.begin(), obs_cnt.end() - 1);
     for (int o = 0; o < n_obs; ++o) obs_idx[f[lm0[o]]++] = o;
   }
+  // lanes per chain: 3 chains use the 4-chain shape (measured faster than 21 lanes)
   const int LW = n_chains == 1 ? 64 : (n_chains == 2 ? 32 : 16);
   if (!build_sweep_layout(nn.data(), n, b, coloring, locs, d, LW, c->lay, err)) {
     delete c;
@@ -332,10 +337,10 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
       int a = nn[(size_t)i * b + j];
       nn_dev[(size_t)dp[i] * b + j] = a < 0 ? -1 : dp[a];
     }
-  const size_t NS = (size_t)L.n_slots;
+  const size_t NS = (size_t)n;
   std::vector<int> lm_dev(n_obs), slot_dpos(NS);
   for (int o = 0; o < n_obs; ++o) lm_dev[o] = dp[lm0[o]];
-  for (size_t s = 0; s < NS; ++s) slot_dpos[s] = L.slot_loc[s] < 0 ? -1 : dp[L.slot_loc[s]];
+  for (size_t x = 0; x < NS; ++x) slot_dpos[x] = dp[L.compact_loc[x]];
 
   if ((rc = set_device(c))) { delete c; return rc; }
 #define CK(x)                                                     \
@@ -364,7 +369,8 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
   CK(hipHostMalloc((void**)&c->linv_cur_h, sizeof(double*) * C, hipHostMallocDefault));
   for (int k = 0; k < C; ++k) c->linv_cur_h[k] = c->ch[k].linv_d[0];
   CK(dalloc(&c->fail_d, 1));
-  CK(dalloc(&c->slots_d, NS));
+  CK(dalloc(&c->sinfo_d, NS));
+  CK(dalloc(&c->compact_loc_d, NS));
   CK(dalloc(&c->dr_d, NS * C));
   CK(dalloc(&c->slot_dpos_d, NS));
   CK(dalloc(&c->chunk_first_d, L.chunk_first.size()));
@@ -373,6 +379,7 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
   CK(dalloc(&c->zbuf_d, (size_t)2 * n * C));
   CK(dalloc(&c->ent_pk_d, (size_t)L.n_entries));
   CK(dalloc(&c->ent_pos_d, (size_t)L.n_entries));
+  CK(dalloc(&c->start_mask_d, L.start_mask.size()));
   CK(dalloc(&c->ent_src_d, (size_t)L.n_entries));
   CK(dalloc(&c->ent_val_d, (size_t)L.n_entries * C));
   CK(dalloc(&c->w_slot_d, NS * C));
@@ -393,15 +400,14 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
   CK(upload(c->locs_d, locs_rm.data(), locs_rm.size(), c->st));
   CK(upload(c->nn_d, nn_dev.data(), nn_dev.size(), c->st));
   {
-    std::vector<SlotShared> sd(NS);
-    for (size_t s = 0; s < NS; ++s) {
-      const int i = L.slot_loc[s];
-      sd[s].loc = i;
-      sd[s].nobs = i < 0 ? 0 : obs_cnt[i + 1] - obs_cnt[i];
-      sd[s].collen = L.collen[s];
-      sd[s].f0 = L.slot_f0[s];
+    std::vector<int2> sd(NS);
+    for (size_t x = 0; x < NS; ++x) {
+      const int i = L.compact_loc[x];
+      sd[x].x = obs_cnt[i + 1] - obs_cnt[i];
+      sd[x].y = L.slot_f0[x] | (L.collen[x] << 16);
     }
-    CK(hipMemcpy(c->slots_d, sd.data(), sizeof(SlotShared) * sd.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(c->sinfo_d, sd.data(), sizeof(int2) * sd.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(c->compact_loc_d, L.compact_loc.data(), sizeof(int) * NS, hipMemcpyHostToDevice));
   }
   CK(hipMemsetAsync(c->dr_d, 0, sizeof(double2) * NS * C, c->st));
   CK(hipMemsetAsync(c->w_slot_d, 0, sizeof(double) * NS * C, c->st));
@@ -426,6 +432,7 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
   }
   CK(upload(c->ent_pk_d, L.ent_pk.data(), (size_t)L.n_entries, c->st));
   CK(upload(c->ent_pos_d, L.ent_pos.data(), (size_t)L.n_entries, c->st));
+  CK(upload(c->start_mask_d, L.start_mask.data(), L.start_mask.size(), c->st));
   CK(upload(c->ent_src_d, L.ent_src.data(), (size_t)L.n_entries, c->st));
   CK(hipMemsetAsync(c->ent_val_d, 0, sizeof(double) * std::max<long long>(1, L.n_entries * C), c->st));
   CK(hipMemcpyAsync(c->linv_cur_d, c->linv_cur_h, sizeof(double*) * C, hipMemcpyHostToDevice, c->st));
@@ -579,10 +586,10 @@ int nngp_get_precision_diag(nngp_ctx* c, double* D) {
   if (!c->ch[c->cur].have_factor[0]) return fail_msg(c, NNGP_ERR_STATE, "precision_diag: no factor");
   int rc;
   if ((rc = set_device(c))) return rc;
-  std::vector<double2> dr((size_t)c->lay.n_slots * c->C);
+  std::vector<double2> dr((size_t)c->n * c->C);
   HIPCHK(c, hipMemcpyAsync(dr.data(), c->dr_d, dr.size() * sizeof(double2), hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
-  for (int i = 0; i < c->n; ++i) D[i] = dr[(size_t)c->lay.loc_slot[i] * c->C + c->cur].x;
+  for (int x = 0; x < c->n; ++x) D[c->lay.compact_loc[x]] = dr[(size_t)x * c->C + c->cur].x;
   return NNGP_OK;
 }
 
@@ -621,7 +628,7 @@ int nngp_set_mu(nngp_ctx* c, const double* mu, double beta0) {
   if (mu) HIPCHK(c, hipMemcpyAsync(S.mu_d, mu, c->n_obs * sizeof(double), hipMemcpyHostToDevice, c->st));
   S.mu_is_const = (mu == nullptr);
   S.mu_beta0 = beta0;
-  HIPCHK(c, launch_residual_sums(c->st, (int)c->lay.n_slots, sweep_dev(c), c->cur, c->obs_ptr_d, c->obs_idx_d, c->y_d,
+  HIPCHK(c, launch_residual_sums(c->st, c->n, sweep_dev(c), c->cur, c->obs_ptr_d, c->obs_idx_d, c->y_d,
                                  mu ? S.mu_d : nullptr, beta0));
   HIPCHK(c, hipStreamSynchronize(c->st));
   S.have_mu = true;
@@ -655,7 +662,7 @@ static int sweep_prepare(nngp_ctx* c, int k, double beta0, double log_scale, dou
   }
   if (S.mu_is_const && S.mu_beta0 != beta0) {
     // residual sums depend on beta0 when mu = beta0
-    HIPCHK(c, launch_residual_sums(c->st, (int)c->lay.n_slots, sweep_dev(c), k, c->obs_ptr_d, c->obs_idx_d, c->y_d,
+    HIPCHK(c, launch_residual_sums(c->st, c->n, sweep_dev(c), k, c->obs_ptr_d, c->obs_idx_d, c->y_d,
                                    nullptr, beta0));
     S.mu_beta0 = beta0;
   }
@@ -681,7 +688,7 @@ static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, int mask, const double*
   const int n = c->n;
   for (int k = 0; k < c->C; ++k) {
     if (!((mask >> k) & 1)) continue;
-    HIPCHK(c, launch_field_to_slots(c->st, (int)c->lay.n_slots, c->slot_dpos_d, c->ch[k].field_d, c->scal_d, c->w_slot_d, c->C, k));
+    HIPCHK(c, launch_field_to_slots(c->st, c->n, c->slot_dpos_d, c->ch[k].field_d, c->scal_d, c->w_slot_d, c->C, k));
     // factor pointer and beta0 read from device memory so a replayed graph
     // sees the current factor and beta0
     launch_row_stats(c->st, nullptr, c->nn_d, n, c->b, c->ch[k].field_d, 0.0, c->r_d + k, c->partials_d,
@@ -712,7 +719,7 @@ static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, int mask, const double*
   }
   for (int k = 0; k < c->C; ++k)
     if ((mask >> k) & 1)
-      HIPCHK(c, launch_slots_to_field(c->st, (int)c->lay.n_slots, c->slot_dpos_d, c->w_slot_d, c->scal_d, c->ch[k].field_d, c->C, k));
+      HIPCHK(c, launch_slots_to_field(c->st, c->n, c->slot_dpos_d, c->w_slot_d, c->scal_d, c->ch[k].field_d, c->C, k));
   return NNGP_OK;
 }
 

@@ -328,7 +328,7 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
                         int LW, SweepLayout& L, std::string& err) {
   L = SweepLayout();
   L.n = n; L.b = b; L.LW = LW;
-  if (LW != 64 && LW != 32 && LW != 16) { err = "lanes_per_chain must be 64, 32 or 16"; return false; }
+  if (LW != 64 && LW != 32 && LW != 21 && LW != 16) { err = "lanes_per_chain must be 64, 32, 21 or 16"; return false; }
   if (n >= kPadRow) { err = "n too large for the packed sweep row index (< 2^25 - 1)"; return false; }
   int K = 0;
   for (int i = 0; i < n; ++i) {
@@ -386,7 +386,6 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
     std::vector<int> f(cptr_col.begin(), cptr_col.end() - 1);
     for (int r = 0; r < n; ++r) { int i = perm[r]; by_col[f[colors[i] - 1]++] = i; }
   }
-  L.SPC = 2 * LW;
   std::vector<int> chunk_first;  // index into by_col of each chunk's first location
   L.color_chunk_ptr.assign(K + 1, 0);
   for (int c = 0; c < K; ++c) {
@@ -408,15 +407,13 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
   L.compact_loc = by_col;
   L.color_loc_ptr = cptr_col;
   L.chunk_first = chunk_first;
-  L.n_slots = (long long)L.nchunks * L.SPC;
   L.n_entries = (long long)L.nchunks * cap;
-  L.slot_loc.assign(L.n_slots, -1);
-  L.collen.assign(L.n_slots, 0);
-  L.slot_f0.assign(L.n_slots, 0);
-  L.loc_slot.assign(n, -1);
+  L.collen.assign(n, 0);
+  L.slot_f0.assign(n, 0);
   L.ent_pk.assign(L.n_entries, 0);
   L.ent_src.assign(L.n_entries, -1);
   L.ent_pos.assign(L.n_entries, 0);
+  L.start_mask.assign((size_t)L.nchunks * LW, 0);
   struct Cell { int p, q, src, f; };
   std::vector<Cell> cells;
   for (int ch = 0; ch < L.nchunks; ++ch) {
@@ -425,16 +422,15 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
     int f = 0;
     for (int x = chunk_first[ch], q = 0; x < chunk_first[ch + 1]; ++x, ++q) {
       const int i = by_col[x];
-      const long long s2 = (long long)ch * L.SPC + q;
-      L.slot_loc[s2] = i;
-      L.loc_slot[i] = (int)s2;
-      L.collen[s2] = (int)(cptr[i + 1] - cptr[i]);
-      L.slot_f0[s2] = f;
+      L.collen[x] = (int)(cptr[i + 1] - cptr[i]);
+      L.slot_f0[x] = f;
+      L.start_mask[(size_t)ch * LW + f / kRowsMax] |= (uint16_t)(1u << (f % kRowsMax));
       for (long long p = cptr[i]; p < cptr[i + 1]; ++p, ++f) cells.push_back({L.rpos[crow[p]], q, csrc[p], f});
     }
     // row order (rows are distinct inside a colour); padding cells last
     std::sort(cells.begin(), cells.end(), [](const Cell& a, const Cell& b2) { return a.p < b2.p; });
     for (int g = f; g < cap; ++g) cells.push_back({kPadRow, max_slots, -1, g});
+    if (f < cap) L.start_mask[(size_t)ch * LW + f / kRowsMax] |= (uint16_t)(1u << (f % kRowsMax));
     for (int k = 0; k < cap; ++k) {
       const long long e = base + k;
       L.ent_pk[e] = (int)((unsigned)cells[k].p | ((unsigned)cells[k].q << kRowBits));

@@ -26,8 +26,8 @@ void morton_keys(const double* locs_colmajor, int n, int d, std::vector<uint64_t
 
 // Device layout of the chromatic sweep ("merge-path slot streams").
 //  - r / field / Linv rows: Morton rank of the location (rpos);
-//  - chunk: one chain group of a wavefront (LW lanes = 64 / chains per
-//    wave) x kRowsMax rows = LW*16 entry cells.  A chunk holds a contiguous
+//  - chunk: one chain group of a wavefront (LW lanes = floor(64 / chains per
+//    wave)) x kRowsMax rows = LW*16 entry cells.  A chunk holds a contiguous
 //    run of whole locations ("slots") of one colour, Morton order, at most
 //    2*LW - 1 of them: their columns of B concatenated in the lane-major
 //    stream f = lane*16 + row, so a column may continue from one lane into
@@ -38,38 +38,34 @@ void morton_keys(const double* locs_colmajor, int n, int d, std::vector<uint64_t
 //    64 lanes of one load/gather/scatter instruction touch a few consecutive
 //    lines of r; ent_pos[e] (uint16) is the cell's stream position f, through
 //    which the kernel regroups the products by slot in LDS;
-//  - slot ids are chunk-strided: slot q of chunk ch is ch*2*LW + q (holes
-//    where a chunk holds fewer slots: slot_loc = -1, collen = 0), so a lane
-//    finds the records of the slots it owns from the chunk index alone;
 //  - ent_pk[e] = rowpos | q << 25 (padding: rowpos = kPadRow, q = 2*LW - 1);
-//  - slot_f0[s] = first stream cell of slot s inside its chunk;
 //  - compact order: the locations colour-major, Morton order inside a colour
-//    (= chunk order); chunk ch starts at compact index chunk_first[ch], so the
-//    compact index of slot q of chunk ch is chunk_first[ch] + q (per-sweep
-//    normals are stored in compact order).
+//    (= chunk order); chunk ch holds compact indices [chunk_first[ch],
+//    chunk_first[ch+1]), slot q of the chunk is compact index chunk_first[ch]+q.
+//    Per-slot data (column length, first stream cell f0, per-chain state and
+//    normals) is stored in compact order.
 constexpr int kRowsMax = 16;          // rows per lane (== kSweepRows)
 constexpr int kRowBits = 25;          // rowpos bits of ent_pk (n < 2^25)
 constexpr int kPadRow = (1 << kRowBits) - 1;
 
 struct SweepLayout {
-  int n = 0, b = 0, K = 0, nchunks = 0, LW = 64, SPC = 128;
-  long long nnz = 0, n_entries = 0, n_slots = 0;  // n_slots = nchunks * SPC (with holes)
+  int n = 0, b = 0, K = 0, nchunks = 0, LW = 64;
+  long long nnz = 0, n_entries = 0;
   int max_collen = 0;
   std::vector<int> color_chunk_ptr;  // K+1
-  std::vector<int> slot_loc;         // n_slots (-1: hole)
-  std::vector<int> loc_slot;         // n
   std::vector<int> rpos;             // n: loc -> device row (Morton rank): r, field, Linv rows
-  std::vector<int> collen;           // n_slots (0: hole)
-  std::vector<int> slot_f0;          // n_slots
+  std::vector<int> collen;           // n, compact order
+  std::vector<int> slot_f0;          // n, compact order
   std::vector<int> ent_pk;           // n_entries
   std::vector<int> ent_src;          // n_entries (device Linv index rpos[k]*b+j; padding: -1)
   std::vector<uint16_t> ent_pos;     // n_entries: stream position of the cell
+  std::vector<uint16_t> start_mask;  // nchunks x LW: bit j = stream cell lane*16+j starts a slot (or the padding tail)
   std::vector<int> compact_loc;      // n: location at each compact index
   std::vector<int> color_loc_ptr;    // K+1: compact range of each colour
   std::vector<int> chunk_first;      // nchunks+1: first compact index of each chunk
 };
 
-// lanes_per_chain: 64, 32 or 16 (1, 2 or 3-4 chains per wavefront).  Fails if
+// lanes_per_chain: 64, 32, 21 or 16 (1, 2, 3 or 4 chains per wavefront).  Fails if
 // a column of B is longer than a chunk (lanes_per_chain * 16 entries) or n
 // does not fit the packed row index.
 bool build_sweep_layout(const int* nn_rowmajor, int n, int b, const int* colors,

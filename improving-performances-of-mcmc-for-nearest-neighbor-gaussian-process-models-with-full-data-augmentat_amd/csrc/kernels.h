@@ -22,32 +22,28 @@ struct SweepScalars {
 constexpr int kSweepRows = 16;  // == kRowsMax of the layout planner
 constexpr int kMaxChains = 4;
 
-// per-slot constants shared by the chains of a context (16 bytes)
-struct __attribute__((aligned(16))) SlotShared {
-  int loc;         // location index (0-based, Vecchia order)
-  int nobs;        // obs_per_loc
-  int collen;      // length of column loc of B
-  int f0;          // first stream cell of the slot inside its chunk
-};
-
 constexpr int kPkRowBits = 25;                    // ent_pk = rowpos | q << 25
 constexpr int kPkPadRow = (1 << kPkRowBits) - 1;  // padding rowpos
 
 // device pointers of the merge-path sweep layout (graph_prep.h); per-chain
 // arrays interleave the chains (slot*C + chain, row*C + chain) so the chains of
 // one entry share cache lines; ent_val is chain-planar (chain*n_entries + e).
+// Per-slot arrays are in compact order (graph_prep.h): slot q of chunk ch is
+// compact index chunk_first[ch] + q.
 struct SweepDev {
-  const SlotShared* slots;    // n_slots = nchunks * 2*LW (chunk-strided, holes: collen 0)
-  double2* dr;                // n_slots x C: {precision_diag, residuals_sum}
+  const int2* sinfo;          // n: {obs_per_loc, f0 | collen << 16}
+  const int* compact_loc;     // n: location of each compact index
+  double2* dr;                // n x C: {precision_diag, residuals_sum}
   const double* ent_val;      // C x n_entries
   const int* ent_pk;          // n_entries
   const uint16_t* ent_pos;    // n_entries: stream position of each (row-sorted) cell
-  double* w_slot;             // n_slots x C
+  const uint16_t* start_mask; // nchunks x LW: bit j = stream cell lane*16+j begins a slot
+  double* w_slot;             // n x C
   double* r;                  // n x C, Morton rows
   const SweepScalars* scal;   // C
   long long n_entries;
   int C;                      // chains in the context
-  int LW;                     // lanes per chain (64 / pow2ceil(C)); 2*LW slots per chunk
+  int LW;                     // lanes per chain (64, 32, 16, 16 for 1..4 chains); <= 2*LW-1 slots per chunk
   const int* chunk_first;     // nchunks+1: compact index of each chunk's first slot
   const int* loc_rank;        // n: compact index of each location (device row order independent)
   unsigned long long* dbg;    // diagnostic timestamps (NNGP_PROBE=9 builds only), else null
@@ -93,11 +89,11 @@ hipError_t launch_reduce4(hipStream_t st, const double* partials, int nblocks, d
 hipError_t launch_sell_refresh(hipStream_t st, const SweepDev& L, int nchunks, const int* ent_src,
                                const double* linv, int chain);
 
-// dr[s*C+chain].y = residuals_sum of the slot's observations (n_slots slots)
-hipError_t launch_residual_sums(hipStream_t st, int n_slots, const SweepDev& L, int chain, const int* obs_ptr,
+// dr[x*C+chain].y = residuals_sum of the observations of compact slot x
+hipError_t launch_residual_sums(hipStream_t st, int n, const SweepDev& L, int chain, const int* obs_ptr,
                                 const int* obs_idx, const double* y, const double* mu, double beta0);
 
-// w[s*C+chain] = field[dpos[s]] - beta0 (and back); n = n_slots, dpos -1 = hole
+// w[x*C+chain] = field[dpos[x]] - beta0 (and back); x compact
 hipError_t launch_field_to_slots(hipStream_t st, int n, const int* slot_dpos, const double* field,
                                  const SweepScalars* sc, double* w_slot, int C, int chain);
 hipError_t launch_slots_to_field(hipStream_t st, int n, const int* slot_dpos, const double* w_slot,

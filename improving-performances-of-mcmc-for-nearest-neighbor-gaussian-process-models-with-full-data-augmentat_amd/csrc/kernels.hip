@@ -512,13 +512,13 @@ __global__ __launch_bounds__(256) void sell_refresh_kernel(SweepDev L, int nchun
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  for (int t = lane; t < 2 * LW; t += 64) {
-    const long long s = (long long)chk * 2 * LW + t;
-    const SlotShared sh = L.slots[s];
-    if (sh.collen == 0) continue;
+  const int x0 = L.chunk_first[chk], nsl = L.chunk_first[chk + 1] - x0;
+  for (int t = lane; t < nsl; t += 64) {
+    const int2 si = L.sinfo[x0 + t];
+    const int f0 = si.y & 0xFFFF, len = si.y >> 16;
     double D = 0.0;
-    for (int f = sh.f0; f < sh.f0 + sh.collen; ++f) D += sq[f];
-    L.dr[(size_t)s * L.C + chain].x = D;
+    for (int f = f0; f < f0 + len; ++f) D += sq[f];
+    L.dr[(size_t)(x0 + t) * L.C + chain].x = D;
   }
 }
 
@@ -542,8 +542,7 @@ __global__ void residual_sums_kernel(int n, SweepDev L, int chain,
                                      double beta0) {
   int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;
-  int loc = L.slots[s].loc;
-  if (loc < 0) return;  // hole
+  int loc = L.compact_loc[s];
   double R = 0.0;
   for (int p = obs_ptr[loc]; p < obs_ptr[loc + 1]; ++p) {
     int o = obs_idx[p];
@@ -565,14 +564,14 @@ __global__ void field_to_slots_kernel(int n, const int* __restrict__ slot_dpos,
                                       const SweepScalars* __restrict__ sc, double* __restrict__ w,
                                       int C) {
   int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < n && slot_dpos[s] >= 0) w[(size_t)s * C] = field[slot_dpos[s]] - sc->beta0;
+  if (s < n) w[(size_t)s * C] = field[slot_dpos[s]] - sc->beta0;
 }
 __global__ void slots_to_field_kernel(int n, const int* __restrict__ slot_dpos,
                                       const double* __restrict__ w,
                                       const SweepScalars* __restrict__ sc, double* __restrict__ field,
                                       int C) {
   int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < n && slot_dpos[s] >= 0) field[slot_dpos[s]] = w[(size_t)s * C] + sc->beta0;
+  if (s < n) field[slot_dpos[s]] = w[(size_t)s * C] + sc->beta0;
 }
 
 hipError_t launch_field_to_slots(hipStream_t st, int n, const int* slot_dpos, const double* field,
@@ -638,8 +637,8 @@ hipError_t launch_normals_compact(hipStream_t st, const SweepDev& L, int chain_m
 //     instruction); the owned slots' normals;
 //  3. products B[k,i] r_k regrouped by stream position in LDS; lane l then
 //     runs along stream cells l*16 .. l*16+15, restarting where a new slot
-//     begins, and stores every running sum (LDS rows padded against bank
-//     conflicts);
+//     begins (start_mask), and stores every running sum (LDS rows padded
+//     against bank conflicts);
 //  4. owner of slot q: acc = its run ending in its last cell, plus the lane
 //     totals of the lanes it spans before that (in lane order: deterministic);
 //     the draw; dw[q] -> LDS;
@@ -663,9 +662,8 @@ constexpr int kCellStride = kSweepRows + 1;  // LDS row pitch (doubles): lanes h
 template <int LW, int PROBE = 0>
 __global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, ColorLaunch a) {
   constexpr int CG = 64 / LW;  // chain groups per wavefront
-  constexpr int SPC = 2 * LW;  // slot ids per chunk
+  constexpr int SPC = 2 * LW;  // slots per chunk (bound)
   __shared__ double cells_s[4][CG][LW * kCellStride];
-  __shared__ unsigned char qs_s[4][CG][LW * kSweepRows];
   __shared__ double dw_s[4][CG][SPC];
   const int gs = (a.nch + 3) / 4;
   if ((int)blockIdx.x >= gs) {
@@ -695,11 +693,9 @@ __global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, ColorLaunc
   if (cg >= C || !((a.chain_mask >> cg) & 1)) return;
   const int chain = cg;
   double* cells = cells_s[wv][cg];
-  unsigned char* qs = qs_s[wv][cg];
   double* dws = dw_s[wv][cg];
   const int ch = a.chunk0 + lch;
   const long long base = (long long)ch * LW * kSweepRows;
-  const long long sbase = (long long)ch * SPC;
   const double* val = L.ent_val + (size_t)chain * L.n_entries;
   double* r = L.r;  // gathered then scattered: no __restrict__
   // round trip 1
@@ -712,61 +708,60 @@ __global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, ColorLaunc
     pk[j] = L.ent_pk[e];
     ps[j] = L.ent_pos[e];
   }
-  SlotShared sh[2];
-  double2 dr[2];
-  double w[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const long long s = sbase + l + u * LW;
-    sh[u] = L.slots[s];
-    dr[u] = L.dr[(size_t)s * C + chain];
-    w[u] = L.w_slot[(size_t)s * C + chain];
-  }
-  const int cfirst = L.chunk_first[ch];
+  const int x0 = L.chunk_first[ch];
+  const int nsl = L.chunk_first[ch + 1] - x0;
+  const unsigned smask = L.start_mask[(size_t)ch * LW + l];
   const SweepScalars* scal = L.scal + chain;
   const double inv_s2 = scal->inv_s2, inv_t2 = scal->inv_t2;
-  if (PROBE == 9) { double x = sh[0].loc + sh[1].loc + dr[0].x + w[0] + cfirst; for (int j = 0; j < kSweepRows; ++j) x += v[j] + pk[j]; if (x == 12345.678) stamp[0] = 0; }
+  if (PROBE == 9) { double x = x0 + nsl; for (int j = 0; j < kSweepRows; ++j) x += v[j] + pk[j] + ps[j]; if (x == 12345.678) stamp[0] = 0; }
   STAMP(1);
-  // round trip 2: gathers + normals
+  // round trip 2: gathers + the owned slots' records and normals
 #pragma unroll
   for (int j = 0; j < kSweepRows; ++j) {
     const int p = pk[j] & kPkPadRow;
     rv[j] = (p != kPkPadRow) ? r[(size_t)p * C + chain] : 0.0;
   }
-  double zz[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-    zz[u] = sh[u].collen > 0 ? a.z_cur[(size_t)(cfirst + l + u * LW) * C + chain] : 0.0;
-  // w' = (R/t2 - (acc - D w)/s2) / P + z / sqrt(P): everything but acc and z
-  double cR[2], invP[2], isP[2];
+  int2 si[2];
+  double2 dr[2];
+  double w[2], zz[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    const double P = dr[u].x * inv_s2 + (double)sh[u].nobs * inv_t2;
-    invP[u] = sh[u].collen > 0 ? 1.0 / P : 0.0;
-    isP[u] = sh[u].collen > 0 ? 1.0 / sqrt(P) : 0.0;
+    const int t = l + u * LW;
+    const size_t x = (size_t)x0 + min(t, nsl - 1);
+    si[u] = L.sinfo[x];
+    dr[u] = L.dr[x * C + chain];
+    w[u] = L.w_slot[x * C + chain];
+    zz[u] = a.z_cur[x * C + chain];
+  }
+  // w' = (R/t2 - (acc - D w)/s2) / P + z / sqrt(P): everything but acc
+  double cR[2], invP[2], zs[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const double P = dr[u].x * inv_s2 + (double)si[u].x * inv_t2;
+    invP[u] = 1.0 / P;
+    zs[u] = zz[u] / sqrt(P);
     cR[u] = inv_t2 * dr[u].y + inv_s2 * (dr[u].x * w[u]);
   }
-  if (PROBE == 9) { double x = zz[0] + zz[1] + cR[0] + invP[0] + isP[0]; for (int j = 0; j < kSweepRows; ++j) x += rv[j]; if (x == 12345.678) stamp[0] = 0; }
+  if (PROBE == 9) { double x = zs[0] + zs[1] + cR[0] + invP[0]; for (int j = 0; j < kSweepRows; ++j) x += rv[j]; if (x == 12345.678) stamp[0] = 0; }
   STAMP(2);
   // products regrouped by stream position, then running sums along the
-  // lane's stream cells, restarted at every slot start
+  // lane's stream cells, restarted at every slot start (start_mask bit j:
+  // stream cell l*16 + j begins a slot)
   int q[kSweepRows];
 #pragma unroll
   for (int j = 0; j < kSweepRows; ++j) {
     q[j] = (int)((unsigned)pk[j] >> kPkRowBits);
     cells[(ps[j] / kSweepRows) * kCellStride + ps[j] % kSweepRows] = v[j] * rv[j];
-    qs[ps[j]] = (unsigned char)q[j];
   }
   wave_lds_sync();
   {
+    double x[kSweepRows];
+#pragma unroll
+    for (int j = 0; j < kSweepRows; ++j) x[j] = cells[l * kCellStride + j];
     double run = 0.0;
-    int qprev = -1;
 #pragma unroll
     for (int j = 0; j < kSweepRows; ++j) {
-      const double x = cells[l * kCellStride + j];
-      const int qq = qs[l * kSweepRows + j];
-      run = (qq == qprev) ? run + x : x;
-      qprev = qq;
+      run = ((smask >> j) & 1u) ? x[j] : run + x[j];
       cells[l * kCellStride + j] = run;
     }
   }
@@ -775,10 +770,12 @@ __global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, ColorLaunc
   // owners: the Gibbs draw of slots q = l and q = l + LW
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    if (sh[u].collen > 0) {
-      const int t = l + u * LW;
-      const int f0 = sh[u].f0, fe = f0 + sh[u].collen - 1;
+    const int t = l + u * LW;
+    if (t < nsl) {
+      const int f0 = si[u].y & 0xFFFF, fe = f0 + (si[u].y >> 16) - 1;
       const int l0 = f0 / kSweepRows, l1 = fe / kSweepRows;
+      // its run ending in its last cell, after the totals of the lanes it
+      // spans before (lane order)
       double acc;
       if (l0 == l1) {
         acc = cells[l1 * kCellStride + fe % kSweepRows];
@@ -787,9 +784,9 @@ __global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, ColorLaunc
         for (int ll = l0 + 1; ll < l1; ++ll) acc += cells[ll * kCellStride + kSweepRows - 1];
         acc += cells[l1 * kCellStride + fe % kSweepRows];
       }
-      const double wn = (cR[u] - inv_s2 * acc) * invP[u] + zz[u] * isP[u];
+      const double wn = (cR[u] - inv_s2 * acc) * invP[u] + zs[u];
       dws[t] = wn - w[u];
-      L.w_slot[(size_t)(sbase + t) * C + chain] = wn;
+      L.w_slot[((size_t)x0 + t) * C + chain] = wn;
     }
   }
   wave_lds_sync();

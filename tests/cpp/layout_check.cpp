@@ -55,10 +55,10 @@ int main(int argc, char** argv) {
       ++nnz;
     }
   REQUIRE(nnz == L.nnz);
-  const int cap = LW * kRowsMax, dummy = 2 * LW - 1, SPC = 2 * LW;
-  REQUIRE(L.SPC == SPC);
+  const int cap = LW * kRowsMax, dummy = 2 * LW - 1;
   REQUIRE(L.n_entries == (long long)L.nchunks * cap);
-  REQUIRE(L.n_slots == (long long)L.nchunks * SPC);
+  REQUIRE((int)L.chunk_first.size() == L.nchunks + 1 && L.chunk_first[L.nchunks] == n);
+  REQUIRE(L.color_loc_ptr[K] == n);
   long long found = 0;
   int located = 0;
   std::vector<long long> at(cap);  // stream position -> entry
@@ -76,17 +76,17 @@ int main(int argc, char** argv) {
         REQUIRE(row > prev_row || row == kPadRow);  // sorted by row, padding last
         if (row != kPadRow) prev_row = row;
       }
-      int f = 0, q = 0;
-      for (; q < SPC; ++q) {
-        const long long s = (long long)ch * SPC + q;
-        const int i = L.slot_loc[s];
-        if (i < 0) break;
+      REQUIRE(L.chunk_first[ch] >= L.color_loc_ptr[c] && L.chunk_first[ch + 1] <= L.color_loc_ptr[c + 1]);
+      const int nsl = L.chunk_first[ch + 1] - L.chunk_first[ch];
+      REQUIRE(nsl >= 1 && nsl <= 2 * LW - 1);
+      int f = 0;
+      for (int q = 0; q < nsl; ++q) {
+        const int x = L.chunk_first[ch] + q;
+        const int i = L.compact_loc[x];
         ++located;
-        REQUIRE(q < SPC - 1);
         REQUIRE(col[i] == c + 1);
-        REQUIRE(L.loc_slot[i] == s);
-        REQUIRE(L.slot_f0[s] == f);
-        const int len = L.collen[s];
+        REQUIRE(L.slot_f0[x] == f);
+        const int len = L.collen[x];
         REQUIRE(len == (int)want[i].size());
         for (int t = 0; t < len; ++t, ++f) {
           const long long e = at[f];
@@ -96,12 +96,14 @@ int main(int argc, char** argv) {
           ++found;
         }
       }
-      REQUIRE(q >= 1);
-      for (int q2 = q; q2 < SPC; ++q2) {  // holes
-        const long long s = (long long)ch * SPC + q2;
-        REQUIRE(L.slot_loc[s] == -1 && L.collen[s] == 0);
-      }
       REQUIRE(f <= cap);
+      // start mask: exactly the slot starts (and the padding tail start)
+      for (int g = 0; g < cap; ++g) {
+        bool start = (g == f && f < cap);
+        for (int q2 = 0; q2 < nsl; ++q2) start = start || (L.slot_f0[L.chunk_first[ch] + q2] == g);
+        const bool bit = (L.start_mask[(size_t)ch * LW + g / kRowsMax] >> (g % kRowsMax)) & 1;
+        REQUIRE(bit == start);
+      }
       for (int g = f; g < cap; ++g) {  // padding tail of the stream
         const long long e = at[g];
         REQUIRE((L.ent_pk[e] & kPadRow) == kPadRow && (int)((unsigned)L.ent_pk[e] >> kRowBits) == dummy);

@@ -119,7 +119,7 @@ def test_gelman_rubin_on_identical_chains(P):
 
 
 @pytest.mark.parametrize("n,m,lw,seed", [(3000, 10, 64, 1), (5000, 15, 32, 2), (8000, 15, 16, 3),
-                                         (2000, 30, 16, 4), (50, 3, 64, 5), (1, 0, 64, 6)])
+                                         (2000, 30, 16, 4), (4000, 12, 21, 7), (50, 3, 64, 5), (1, 0, 64, 6)])
 def test_sweep_layout_invariants(tmp_path, n, m, lw, seed):
     """C++ check of the planner: every nonzero of B exactly once, at the
     address the sweep kernel computes from the colour class table."""
