@@ -703,10 +703,11 @@ __global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, ColorLaunc
   int pk[kSweepRows], ps[kSweepRows];
 #pragma unroll
   for (int j = 0; j < kSweepRows; ++j) {
+    // read once per sweep: non-temporal, so the XCD's L2 keeps r
     const long long e = base + (long long)j * LW + l;
-    v[j] = val[e];
-    pk[j] = L.ent_pk[e];
-    ps[j] = L.ent_pos[e];
+    v[j] = __builtin_nontemporal_load(val + e);
+    pk[j] = __builtin_nontemporal_load(L.ent_pk + e);
+    ps[j] = __builtin_nontemporal_load(L.ent_pos + e);
   }
   const int x0 = L.chunk_first[ch];
   const int nsl = L.chunk_first[ch + 1] - x0;
