@@ -73,9 +73,16 @@ def open_context(P, wl, covfun, cp, device, chains, seed):
     return ctx
 
 
-def cpu_baseline(P, wl, covfun, cp, budget_s):
-    """Reference-faithful masked-form sweep (update_Gaussian.R:269) of the CPU
-    oracle (a C restatement, 1 core) on the same workload, bounded in time."""
+def cpu_baseline(P, wl, covfun, cp, budget_s, chains):
+    """The reference's CPU path restated: the masked-form chromatic sweep
+    (update_Gaussian.R:257-275, full masked SpMV + column crossprod per colour)
+    of the C oracle, one chain per host thread as the reference runs one chain
+    per mclapply worker (update_Gaussian.R:25-26), on the same workload; whole
+    sweeps until ~budget_s/2.  ctypes releases the GIL, so the threads run in
+    parallel without forking this GPU-initialised process.  The single-thread
+    local-form oracle is reported beside it."""
+    import threading
+
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle as O
 
@@ -84,26 +91,53 @@ def cpu_baseline(P, wl, covfun, cp, budget_s):
     Lo = O.vecchia_linv(covfun, cp, wl["locs"], wl["NN"])
     D = O.precision_diag(Lo, wl["NN"])
     t_factor = time.time() - t
-    field = np.asarray(wl["field0"])
     opl = np.ones(n, np.int32)
     mu = np.full(n, wl["beta0"])
-    res = {}
-    for form in ("masked", "local"):
-        z = O.sweep_normals(3, 0, 1, n)
+    z = O.sweep_normals(3, 0, 1, n)
+
+    def run(form, out, k):
+        field = np.asarray(wl["field0"]).copy()
         done, t0 = 0, time.time()
         while True:
-            O.sweep(form, field, Lo, wl["NN"], wl["col"], D, opl, wl["y"], mu, wl["lm"], wl["beta0"],
-                    wl["log_scale"], wl["log_noise_variance"], z)
+            field = O.sweep(form, field, Lo, wl["NN"], wl["col"], D, opl, wl["y"], mu, wl["lm"], wl["beta0"],
+                            wl["log_scale"], wl["log_noise_variance"], z)
             done += 1
             if time.time() - t0 > budget_s / 2 or done >= 20:
                 break
-        res[form] = done / (time.time() - t0)
-    return {"value": res["masked"], "unit": "sweeps/s", "cores": 1, "kind": "port",
+        out[k] = (done, time.time() - t0)
+
+    res = [None] * chains
+    th = [threading.Thread(target=run, args=("masked", res, k)) for k in range(chains)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    masked = sum(d / el for d, el in res)
+    loc = [None]
+    run("local", loc, 0)
+    return {"value": masked, "unit": "sweeps/s", "cores": chains, "kind": "port",
             "sample": (f"oracle C restatement of the reference's masked-form chromatic sweep "
-                       f"(update_Gaussian.R:257-275), same n={n} workload, whole sweeps until "
-                       f"~{budget_s / 2:.0f}s; local-form oracle {res['local']:.3g} sweeps/s; "
-                       f"oracle factor build {t_factor:.1f}s"),
-            "local_form_value": res["local"]}
+                       f"(update_Gaussian.R:257-275), {chains} chains on {chains} host threads (the reference's "
+                       f"mclapply over chains), same n={n} workload, whole sweeps until ~{budget_s / 2:.0f}s each "
+                       f"({sum(d for d, _ in res)} sweeps); local-form oracle 1 thread "
+                       f"{loc[0][0] / loc[0][1]:.3g} sweeps/s; oracle factor build {t_factor:.1f}s"),
+            "local_form_value_1_thread": loc[0][0] / loc[0][1]}
+
+
+def pmc_traffic(chains, n, m):
+    """Per-launch HBM bytes of the sweep kernel from the committed rocprofv3
+    PMC summary of the same workload (profiles/, scripts/pmc.sh: FETCH_SIZE and
+    WRITE_SIZE passes, calibrated on known-byte kernels)."""
+    best = None
+    for f in sorted((ROOT / "profiles").glob("r*_pmc_sweep_c*.json")):
+        try:
+            d = json.loads(f.read_text())
+        except Exception:
+            continue
+        w = d.get("workload", {})
+        if w.get("chains") == chains and w.get("n") == n and w.get("m") == m and d.get("traffic_bytes_per_launch"):
+            best = (d["traffic_bytes_per_launch"], f.name)
+    return best
 
 
 def main():
@@ -208,16 +242,21 @@ def main():
         per_sweep_ms = kms / ksw
         achieved = bytes_sweep / (per_sweep_ms * 1e-3) / 1e9
         launches = ksw * info["n_colors"]
+        tr = pmc_traffic(C, n, args.m)
         roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                    "frac": achieved / HBM_PEAK_GBS,
+                    "traffic": tr[0] / (kms * 1e-3 / launches) / 1e9 if tr else None,
+                    "traffic_unit": "GB/s (PMC bytes per launch / measured launch time)",
+                    "traffic_bytes_per_launch": tr[0] if tr else None,
+                    "traffic_source": f"profiles/{tr[1]}" if tr else None,
                     "kernel": "sweep_color_kernel", "kernel_avg_us": kms * 1e3 / launches,
                     "algorithmic_bytes_per_sweep": bytes_sweep,
                     "algorithmic_bytes_per_launch": bytes_sweep / info["n_colors"],
                     "launches_per_sweep": info["n_colors"]}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        log("cpu baseline (oracle, 1 core)...", rank)
-        cpu = cpu_baseline(P, wl, covfun, cp, args.cpu_budget)
+        log(f"cpu baseline (oracle, {C} threads)...", rank)
+        cpu = cpu_baseline(P, wl, covfun, cp, args.cpu_budget, C)
     ctx.close()
     value = args.steps * C * world / elapsed
     out = {"metric": "full-field Gibbs sweeps/sec at n=1e6, m=15; achieved HBM GB/s vs roofline",

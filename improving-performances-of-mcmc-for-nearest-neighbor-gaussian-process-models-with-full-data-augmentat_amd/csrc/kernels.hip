@@ -603,8 +603,8 @@ __device__ __forceinline__ void gen_normals(int item, const int* __restrict__ pa
   const int p = pairs ? pairs[item / C] : item / C;
   double z0, z1;
   normal_pair(scal[chain].seed, scal[chain].counter_base + sweep_off, (uint32_t)p, z0, z1);
-  z[(size_t)loc_rank[2 * p] * C + chain] = z0;
-  if (2 * p + 1 < n) z[(size_t)loc_rank[2 * p + 1] * C + chain] = z1;
+  __builtin_nontemporal_store(z0, z + (size_t)loc_rank[2 * p] * C + chain);
+  if (2 * p + 1 < n) __builtin_nontemporal_store(z1, z + (size_t)loc_rank[2 * p + 1] * C + chain);
 }
 
 __global__ __launch_bounds__(256) void normals_compact_kernel(SweepDev L, int chain_mask, int sweep_off,
@@ -729,10 +729,16 @@ __global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, ColorLaunc
   for (int u = 0; u < 2; ++u) {
     const int t = l + u * LW;
     const size_t x = (size_t)x0 + min(t, nsl - 1);
-    si[u] = L.sinfo[x];
-    dr[u] = L.dr[x * C + chain];
-    w[u] = L.w_slot[x * C + chain];
-    zz[u] = a.z_cur[x * C + chain];
+    // per-slot data is touched once per sweep: non-temporal like the cells
+    {
+      const long long raw = __builtin_nontemporal_load(reinterpret_cast<const long long*>(L.sinfo + x));
+      si[u].x = (int)(raw & 0xFFFFFFFFll);
+      si[u].y = (int)(raw >> 32);
+    }
+    dr[u].x = __builtin_nontemporal_load(&L.dr[x * C + chain].x);
+    dr[u].y = __builtin_nontemporal_load(&L.dr[x * C + chain].y);
+    w[u] = __builtin_nontemporal_load(L.w_slot + x * C + chain);
+    zz[u] = __builtin_nontemporal_load(a.z_cur + x * C + chain);
   }
   // w' = (R/t2 - (acc - D w)/s2) / P + z / sqrt(P): everything but acc
   double cR[2], invP[2], zs[2];
@@ -787,7 +793,7 @@ __global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, ColorLaunc
       }
       const double wn = (cR[u] - inv_s2 * acc) * invP[u] + zs[u];
       dws[t] = wn - w[u];
-      L.w_slot[((size_t)x0 + t) * C + chain] = wn;
+      __builtin_nontemporal_store(wn, L.w_slot + ((size_t)x0 + t) * C + chain);
     }
   }
   wave_lds_sync();

@@ -175,8 +175,9 @@ int nngp_tri_solve(nngp_ctx* ctx, int which, const double* u, double* x);
 
 /* ---------- measurement ---------- */
 /* nngp_sweep_chains bracketed by HIP events on the context's stream;
- * *ms = elapsed; per-colour-kernel durations are summed into *kernel_ms when
- * kernel_ms != NULL (each colour launch bracketed by its own events). */
+ * *ms = elapsed for the whole call; *kernel_ms (if not NULL) = elapsed for the
+ * n_sweeps x n_colors sweep-kernel launches alone (a graph of only those
+ * launches between two events: mean launch time = kernel_ms / launches). */
 int nngp_sweep_timed(nngp_ctx* ctx, int n_sweeps, const double* beta0, const double* log_scale,
                      const double* log_noise_variance, const uint64_t* seed,
                      const uint64_t* counter_base, double* ms, double* kernel_ms);
