@@ -140,6 +140,30 @@ def pmc_traffic(chains, n, m):
     return best
 
 
+def timed_region(run, steps, warmup, dist=None, sync=lambda: None):
+    """The bench contract's timed region: `warmup` untimed steps, then exactly
+    `steps` steps bracketed by barrier + device sync on both sides; returns
+    (max over ranks of the elapsed seconds, run's last return value).
+    run(n_steps, counter) -> counter."""
+    import torch
+
+    ctr = run(warmup, 0)
+    sync()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    ctr = run(steps, ctr)
+    sync()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el, ctr
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -191,23 +215,8 @@ def main():
                 done += s
             return base + done
 
-        ctr = run(warmup, 0)
-        if torch.cuda.is_available():
-            torch.cuda.synchronize(local_rank)
-        if dist:
-            dist.barrier()
-        t0 = time.perf_counter()
-        ctr = run(steps, ctr)
-        if torch.cuda.is_available():
-            torch.cuda.synchronize(local_rank)
-        if dist:
-            dist.barrier()
-        el = time.perf_counter() - t0
-        if dist:
-            t = torch.tensor([el], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
-        return el, ctr
+        sync = (lambda: torch.cuda.synchronize(local_rank)) if torch.cuda.is_available() else (lambda: None)
+        return timed_region(run, steps, warmup, dist, sync)
 
     single = None
     if not args.no_single_chain:

@@ -1,0 +1,58 @@
+"""The bench's N>1 path on CPU: world_size-2 gloo processes (127.0.0.1) run
+the contract's timed region; every rank must report the MAX elapsed over
+ranks, and the per-rank workloads (seeds) must differ (weak scaling: each
+rank sweeps its own chains, no data-path collective)."""
+import os
+import sys
+import time
+from pathlib import Path
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    delay = 0.05 * (rank + 1)
+
+    def run(n, ctr):
+        for _ in range(n):
+            time.sleep(delay / 10)
+        return ctr + n
+
+    el, ctr = bench.timed_region(run, 10, 2, dist)
+    q.put((rank, el, ctr))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_two_rank_timed_region_reports_max_over_ranks():
+    world, port = 2, 29000 + os.getpid() % 1000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=100) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    els = {r: el for r, el, _ in out}
+    assert abs(els[0] - els[1]) < 1e-12           # all_reduce(MAX): identical on every rank
+    assert els[0] >= 0.1 * 0.9                      # the slower rank's 10 x 10 ms dominates
+    assert all(ctr == 12 for _, _, ctr in out)      # warmup 2 + timed 10 steps
+
+
+def test_rank_workloads_differ():
+    """Each rank draws its own synthetic field and chain seeds (bench.main)."""
+    src = (ROOT / "bench.py").read_text()
+    assert "seed=1000 + rank" in src and "77 + 10 * rank + k" in src
