@@ -78,6 +78,17 @@ def test_oracle_normals_are_standard(O):
     assert kstest(z, "norm").pvalue > 1e-3
 
 
+def test_oracle_normal_pairs_independent(O):
+    """Locations 2p and 2p+1 share one Philox call (cos / sin of Box-Muller):
+    the two halves must be uncorrelated, also in their squares."""
+    z = O.normals(7, 3, 400_000)
+    a, b = z[0::2], z[1::2]
+    assert abs(np.corrcoef(a, b)[0, 1]) < 0.01
+    assert abs(np.corrcoef(a * a, b * b)[0, 1]) < 0.01
+    # the pair of a location does not depend on n (counter = location >> 1)
+    np.testing.assert_array_equal(O.normals(7, 3, 11), z[:11])
+
+
 @pytest.mark.parametrize("nu", [0.3, 0.5, 0.77, 1.0, 1.5, 2.2, 3.7])
 def test_oracle_bessel_k(O, nu):
     for x in [1e-6, 1e-3, 0.1, 0.9, 2.0, 5.0, 30.0, 200.0]:
