@@ -74,6 +74,8 @@ struct nngp_ctx {
   double* w_slot_d = nullptr;    // n x C
   double* r_d = nullptr;         // n x C
   int* level_rows_d = nullptr;
+  int* level_ptr_d = nullptr;    // DAG level offsets (device copy)
+  std::vector<int> tri_seg;      // solve plan: (lv0, lv1, kind) triples, kind 1 = one-workgroup run
   int* obs_ptr_d = nullptr;
   int* obs_idx_d = nullptr;
   int* lm_d = nullptr;  // locs_match, 0-based
@@ -251,7 +253,7 @@ void nngp_ctx_destroy(nngp_ctx* c) {
                              c->dr_d, c->slot_dpos_d, c->ent_pk_d, c->ent_src_d, c->ent_val_d, c->w_slot_d,
                              c->r_d, c->level_rows_d, c->obs_ptr_d, c->obs_idx_d, c->lm_d, c->y_d, c->tmp_d,
                              c->tmp2_d, c->partials_d, c->res_d, c->z_d, c->scal_d, c->dbg_d,
-                             c->chunk_first_d, c->loc_rank_d, c->pairs_d, c->zbuf_d, c->ent_pos_d, c->start_mask_d};
+                             c->chunk_first_d, c->loc_rank_d, c->pairs_d, c->level_ptr_d, c->zbuf_d, c->ent_pos_d, c->start_mask_d};
   for (int k = 0; k < kMaxChains; ++k) {
     ChainState& s = c->ch[k];
     ptrs.insert(ptrs.end(), {s.linv_d[0], s.linv_d[1], s.field_d, s.field_prop_d, s.mu_d});
@@ -327,6 +329,9 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
   c->dpos = L.rpos;
   const std::vector<int>& dp = c->dpos;
   for (auto& r : c->level_rows) r = dp[r];
+  // rows of a level in device (Morton) order: coalesced row loads, local x gathers
+  for (size_t l = 0; l + 1 < c->level_ptr.size(); ++l)
+    std::sort(c->level_rows.begin() + c->level_ptr[l], c->level_rows.begin() + c->level_ptr[l + 1]);
   // device-order copies
   std::vector<double> locs_rm((size_t)n * d);
   for (int i = 0; i < n; ++i)
@@ -385,6 +390,31 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
   CK(dalloc(&c->w_slot_d, NS * C));
   CK(dalloc(&c->r_d, (size_t)n * C));
   CK(dalloc(&c->level_rows_d, n));
+  CK(dalloc(&c->level_ptr_d, c->level_ptr.size()));
+  CK(upload(c->level_ptr_d, c->level_ptr.data(), c->level_ptr.size(), c->st));
+  {
+    // triangular-solve plan: runs of levels with <= kSmallLevel rows go to one
+    // workgroup (a barrier per level; one CU streams ~10 B/cycle, so only
+    // small levels are cheaper there than behind a launch), larger levels get
+    // a launch each
+    // (NNGP_TRI=level: one launch per level, the reference plan of the tests)
+    const char* e = std::getenv("NNGP_TRI");
+    const bool per_level = e && std::string(e) == "level";
+    const int L = (int)c->level_ptr.size() - 1;
+    for (int lv = 0; lv < L;) {
+      const int sz = c->level_ptr[lv + 1] - c->level_ptr[lv];
+      constexpr int kSmallLevel = 128;
+      if (per_level || sz > kSmallLevel) {
+        c->tri_seg.insert(c->tri_seg.end(), {lv, lv + 1, 0});
+        ++lv;
+        continue;
+      }
+      int lv1 = lv;
+      while (lv1 < L && c->level_ptr[lv1 + 1] - c->level_ptr[lv1] <= kSmallLevel) ++lv1;
+      c->tri_seg.insert(c->tri_seg.end(), {lv, lv1, 1});
+      lv = lv1;
+    }
+  }
   CK(dalloc(&c->obs_ptr_d, (size_t)n + 1));
   CK(dalloc(&c->obs_idx_d, n_obs));
   CK(dalloc(&c->lm_d, n_obs));
@@ -849,9 +879,14 @@ int nngp_sweep_timed(nngp_ctx* c, int n_sweeps, const double* beta0, const doubl
 
 // ---------------------------------------------------------------- MH helpers
 static int tri_solve_dev(nngp_ctx* c, const double* linv, const double* u, double* x) {
-  for (size_t l = 0; l + 1 < c->level_ptr.size(); ++l) {
-    int a = c->level_ptr[l], e = c->level_ptr[l + 1];
-    if (e > a) HIPCHK(c, launch_tri_level(c->st, c->level_rows_d + a, e - a, linv, c->nn_d, c->b, u, x));
+  for (size_t k = 0; k + 2 < c->tri_seg.size(); k += 3) {
+    const int lv0 = c->tri_seg[k], lv1 = c->tri_seg[k + 1];
+    if (c->tri_seg[k + 2]) {
+      HIPCHK(c, launch_tri_levels_block(c->st, c->level_rows_d, c->level_ptr_d, lv0, lv1, linv, c->nn_d, c->b, u, x));
+    } else {
+      const int a = c->level_ptr[lv0], e = c->level_ptr[lv1];
+      if (e > a) HIPCHK(c, launch_tri_level(c->st, c->level_rows_d + a, e - a, linv, c->nn_d, c->b, u, x));
+    }
   }
   return NNGP_OK;
 }

@@ -115,6 +115,9 @@ int launch_obs_reduce(hipStream_t st, int mode, int n_obs, const double* y, cons
 
 hipError_t launch_tri_level(hipStream_t st, const int* rows, int nrows, const double* linv,
                             const int* nn, int b, const double* u, double* x);
+// levels [lv0, lv1) of the DAG (each <= 1024 rows) in one 1024-thread workgroup
+hipError_t launch_tri_levels_block(hipStream_t st, const int* rows, const int* lptr, int lv0, int lv1,
+                                   const double* linv, const int* nn, int b, const double* u, double* x);
 hipError_t launch_axpby_shift(hipStream_t st, int n, const double* x, double scale, double shift,
                               double* y);
 

@@ -889,6 +889,38 @@ hipError_t launch_tri_level(hipStream_t st, const int* rows, int nrows, const do
   return hipGetLastError();
 }
 
+// A run of consecutive SMALL levels of the Vecchia DAG in one workgroup:
+// the rows of level lv are rows[lptr[lv] .. lptr[lv+1]) (<= blockDim each);
+// the workgroup barrier between levels replaces a kernel launch (same
+// arithmetic as tri_level_kernel).
+__global__ __launch_bounds__(1024) void tri_levels_block_kernel(const int* __restrict__ rows,
+                                                                const int* __restrict__ lptr, int lv0, int lv1,
+                                                                const double* __restrict__ linv,
+                                                                const int* __restrict__ nn, int b,
+                                                                const double* __restrict__ u, double* x) {
+  for (int lv = lv0; lv < lv1; ++lv) {
+    const int a = lptr[lv], e = lptr[lv + 1];
+    for (int t = a + (int)threadIdx.x; t < e; t += blockDim.x) {
+      const int i = rows[t];
+      const double* lr = linv + (size_t)i * b;
+      const int* nr = nn + (size_t)i * b;
+      double s = u[i];
+      for (int j = 1; j < b; ++j) {
+        const int idx = nr[j];
+        if (idx >= 0) s -= lr[j] * x[idx];
+      }
+      x[i] = s / lr[0];
+    }
+    __syncthreads();
+  }
+}
+
+hipError_t launch_tri_levels_block(hipStream_t st, const int* rows, const int* lptr, int lv0, int lv1,
+                                   const double* linv, const int* nn, int b, const double* u, double* x) {
+  hipLaunchKernelGGL(tri_levels_block_kernel, dim3(1), dim3(1024), 0, st, rows, lptr, lv0, lv1, linv, nn, b, u, x);
+  return hipGetLastError();
+}
+
 __global__ void axpby_shift_kernel(int n, const double* __restrict__ x, double scale, double shift,
                                    double* __restrict__ y) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;

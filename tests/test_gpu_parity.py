@@ -386,3 +386,25 @@ def test_single_chain_sweep_inside_batched_context(P, O):
     ref = O.sweep("local", fields[1], Lo, NN, col, O.precision_diag(Lo, NN), np.ones(n, np.int32), y,
                   np.zeros(n), lm, 0.0, 0.0, 0.0, z)
     np.testing.assert_allclose(got[1], ref, rtol=1e-9, atol=1e-10)
+
+
+@pytest.mark.parametrize("n,m", [(5000, 5), (120000, 15)])
+def test_blocked_tri_solve_equals_level_schedule(P, O, n, m, monkeypatch):
+    """The blocked solve plan (runs of small DAG levels in one workgroup) gives
+    exactly the bits of one launch per level, repeatedly, and matches the
+    oracle."""
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=n + 1)
+    cp = COVS["matern15_isotropic"]
+    rng = np.random.default_rng(3)
+    us = [rng.normal(size=n) for _ in range(3)]
+    with _ctx(P, locs, NN, col, lm, y) as ctx:
+        ctx.factor(0, "matern15_isotropic", cp)
+        got = [ctx.tri_solve(0, u) for u in us]
+        Lo = ctx.get_linv(0)
+    monkeypatch.setenv("NNGP_TRI", "level")
+    with _ctx(P, locs, NN, col, lm, y) as ctx:
+        ctx.factor(0, "matern15_isotropic", cp)
+        ref = [ctx.tri_solve(0, u) for u in us]
+    for g, r in zip(got, ref):
+        np.testing.assert_array_equal(g, r)
+    np.testing.assert_allclose(got[0], O.tri_solve(Lo, NN, us[0]), rtol=1e-9, atol=1e-10)
