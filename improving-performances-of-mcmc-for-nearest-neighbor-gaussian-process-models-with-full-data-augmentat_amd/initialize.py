@@ -55,7 +55,9 @@ def _model_matrix(df):
             cols.append(np.asarray(s, np.float64))
             names.append(str(c))
         else:
-            cat = pd.Categorical(s)
+            # a pandas Categorical keeps its level order (R's `levels`
+            # attribute); other columns become factors with sorted levels
+            cat = s.array if isinstance(s.dtype, pd.CategoricalDtype) else pd.Categorical(s)
             for lev in cat.categories[1:]:
                 cols.append((cat == lev).astype(np.float64))
                 names.append(f"{c}{lev}")

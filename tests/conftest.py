@@ -54,3 +54,23 @@ def make_problem(P, n, m, d=2, seed=0, order=True, dup_frac=0.0):
         lm = np.concatenate([lm, extra.astype(np.int32)])
     y = rng.normal(size=len(lm))
     return locs, NN, col, lm, y
+
+
+@pytest.fixture(scope="session")
+def heavy():
+    """Heavy_metals/processed_data.RDS (run_script.R:8-12) as parsed by
+    tests/golden/make_heavy_metals.py: observed_locs (lon/lat), observed_field,
+    X_locs as a data.frame with its 3 factors in their stored level order."""
+    import pandas as pd
+
+    d = np.load(Path(__file__).resolve().parent / "golden" / "heavy_metals.npz")
+    cols = {}
+    num = dict(zip(d["X_num_names"], d["X_num"].T))
+    for c in d["column_order"]:
+        if c in num:
+            cols[c] = num[c]
+        else:
+            levels = list(d[f"levels_{c}"])
+            cols[c] = pd.Categorical.from_codes(d[f"fac_{c}"] - 1, categories=levels)
+    return {"observed_locs": d["observed_locs"], "observed_field": d["observed_field"],
+            "X_locs": pd.DataFrame(cols)}

@@ -1,0 +1,79 @@
+"""The reference's real-data configuration (BASELINE configs[2]):
+Heavy_metals/processed_data.RDS, exponential_sphere, m = 5 as in
+Heavy_metals/run_script.R:8-12 (the paper run).  The fixture holds the RDS's
+data (tests/golden/make_heavy_metals.py); the reference's fitted output
+(myfit.RDS) is not in the reference tree, so the device path is checked
+against the oracle on this real input (parity) and for a finite, sane fit."""
+import numpy as np
+import pytest
+
+
+def test_fixture_matches_the_rds_summary(heavy):
+    """64,274 observations at 58,097 lon/lat locations."""
+    locs, y = heavy["observed_locs"], heavy["observed_field"]
+    assert locs.shape == (64274, 2) and y.shape == (64274,)
+    assert locs[:, 0].min() == pytest.approx(-124.60355, abs=1e-5)
+    assert locs[:, 1].max() == pytest.approx(49.34043, abs=1e-5)
+    assert y.mean() == pytest.approx(2.838, abs=1e-3) and y.var(ddof=1) == pytest.approx(0.4293, abs=1e-4)
+    _, counts = np.unique(locs, axis=0, return_counts=True)
+    assert len(counts) == 58097 and counts.max() == 20
+    assert np.bincount(counts)[1:4].tolist() == [52512, 5332, 108]
+
+
+def test_model_matrix_has_r_treatment_contrasts(P, heavy):
+    """model.matrix(~., X_locs)[, -1] (initialize.R:124-127): 11 numeric
+    columns plus (27-1) + (8-1) + (113-1) dummies in data.frame column order,
+    first level of each factor dropped."""
+    from nngp_amd.initialize import _model_matrix
+
+    X = heavy["X_locs"]
+    mm, names = _model_matrix(X)
+    assert mm.shape == (64274, 11 + 26 + 7 + 112)
+    assert names[:6] == ["dairp", "dmino", "dquksig", "dTRI", "gcarb", "globedem"]
+    lv = list(X["minotype"].cat.categories)
+    assert names[6] == f"minotype{lv[1]}" and names[6 + 25] == f"minotype{lv[26]}"
+    np.testing.assert_array_equal(mm[:, 6], (np.asarray(X["minotype"]) == lv[1]).astype(float))
+    assert names[-1] == f"MAJOR1{list(X['MAJOR1'].cat.categories)[-1]}"
+
+
+@pytest.mark.gpu
+def test_heavy_metals_device_path_matches_oracle(P, O, heavy):
+    """exponential_sphere, m = 5 on the real locations: the device factor,
+    one chromatic sweep and a few full Gibbs iterations (with the 156-column
+    design and interweaving) agree with the oracle."""
+    import mcmc_oracle as MO
+    from nngp_amd.update_gaussian import _philox_key, _run_chain
+
+    L = P.mcmc_nngp_initialize(heavy["observed_locs"], heavy["observed_field"], X_locs=heavy["X_locs"],
+                               stationary_covfun="exponential_sphere", m=5, n_chains=1, seed=1)
+    va, st = L["vecchia_approx"], L["states"]["chain_1"]
+    ctx = L["_contexts"][0]
+    assert va["n_locs"] == 58097 and L["X"]["X"].shape[1] == 156
+    from nngp_amd.model import covparms
+
+    cp = covparms(L["space_time_model"]["covfun"]["shape_params"], st["params"]["shape"])
+    ctx.factor(0, "exponential_sphere", cp)
+    Ld = ctx.get_linv(0)
+    Lo = O.vecchia_linv("exponential_sphere", cp, L["locs"], va["NNarray"])
+    # per-row forward-error bound eps * cond(local covariance) * max|row|:
+    # near-coincident real locations make some local covariances
+    # ill-conditioned (rows checked against the bound where 1e-10 fails)
+    err = np.abs(Ld - Lo).max(1)
+    scale = np.abs(Lo).max(1)
+    for i in np.nonzero(err > 1e-10 * scale)[0]:
+        NN = va["NNarray"]
+        idx = NN[i][NN[i] != O.NA] - 1
+        kappa = np.linalg.cond(O.covmat("exponential_sphere", cp, L["locs"][idx]))
+        assert err[i] <= max(1e-10, 1e-14 * kappa) * scale[i], (i, kappa, err[i])
+    iters, nc = 5, 3
+    res = _run_chain(0, st, ctx, L["X"], L["observed_field"], L["space_time_model"], va, iters, 1.0, True, nc, 0, 1)
+    ref = MO.run_chain(0, st, L["locs"], va["NNarray"], va["coloring"], L["X"], L["observed_field"],
+                       L["space_time_model"], va, iters, 1.0, nc, 0, _philox_key(0, 1, 1))
+    # same MH decisions; values to the factor's conditioning-limited agreement
+    np.testing.assert_array_equal(res["acceptance"]["covariance_acceptance_sufficient"], ref["acceptance"]["sufficient"])
+    np.testing.assert_array_equal(res["acceptance"]["covariance_acceptance_ancillary"], ref["acceptance"]["ancillary"])
+    np.testing.assert_allclose(res["records"]["log_scale"][:, 0], ref["records"]["log_scale"], rtol=1e-6, atol=1e-8)
+    np.testing.assert_allclose(res["records"]["beta_0"][:, 0], ref["records"]["beta_0"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(res["state"]["params"]["field"], ref["params"]["field"], rtol=1e-4, atol=1e-5)
+    assert np.all(np.isfinite(res["records"]["beta"]))
+    ctx.close()
