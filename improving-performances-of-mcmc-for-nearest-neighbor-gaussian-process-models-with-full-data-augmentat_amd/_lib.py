@@ -29,7 +29,8 @@ ABI_SYMBOLS = (
     "nngp_greedy_coloring", "nngp_ctx_create", "nngp_ctx_destroy", "nngp_ctx_last_error",
     "nngp_set_chain", "nngp_ctx_info", "nngp_factor", "nngp_get_linv", "nngp_set_linv", "nngp_accept_factor",
     "nngp_get_precision_diag", "nngp_set_field", "nngp_get_field", "nngp_set_mu",
-    "nngp_loglik", "nngp_sweep", "nngp_sweep_chains", "nngp_ancillary_propose", "nngp_field_response_ratio",
+    "nngp_loglik", "nngp_sweep", "nngp_sweep_chains", "nngp_ancillary_propose", "nngp_ancillary_propose_chains",
+    "nngp_field_response_ratio",
     "nngp_accept_field", "nngp_beta0_stats", "nngp_sum_squared_residuals", "nngp_spmv",
     "nngp_tri_solve", "nngp_sweep_timed", "nngp_device_normals",
 )
@@ -93,6 +94,7 @@ def _load():
     L.nngp_tri_solve.argtypes = [_vp, C.c_int, _dp, _dp]
     _up = np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS")
     L.nngp_sweep_chains.argtypes = [_vp, C.c_int, _dp, _dp, _dp, _up, _up]
+    L.nngp_ancillary_propose_chains.argtypes = [_vp, C.c_int, _dp, _dp]
     L.nngp_sweep_timed.argtypes = [_vp, C.c_int, _dp, _dp, _dp, _up, _up,
                                    C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.nngp_device_normals.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_int, _dp]

@@ -156,6 +156,14 @@ class ChainContext:
     def ancillary_propose(self, beta0: float, dlog_scale: float) -> None:
         self._chk(lib.nngp_ancillary_propose(self._h, float(beta0), float(dlog_scale)))
 
+    def ancillary_propose_chains(self, chain_mask: int, beta0, dlog_scale) -> None:
+        """ancillary_propose for every chain in chain_mask (bit k = chain k) in
+        one triangular-solve schedule; beta0/dlog_scale indexed by chain."""
+        k = self.n_chains
+        b = np.ascontiguousarray(np.broadcast_to(np.asarray(beta0, np.float64), (k,)))
+        d = np.ascontiguousarray(np.broadcast_to(np.asarray(dlog_scale, np.float64), (k,)))
+        self._chk(lib.nngp_ancillary_propose_chains(self._h, int(chain_mask), b, d))
+
     def field_response_ratio(self, beta0: float, log_noise_variance: float) -> float:
         out = C.c_double()
         self._chk(lib.nngp_field_response_ratio(self._h, float(beta0), float(log_noise_variance),
@@ -200,7 +208,8 @@ class ChainView:
 
     def __getattr__(self, name):
         attr = getattr(self.ctx, name)
-        if not callable(attr) or name in ("close", "view", "sweep_chains", "sweep_timed"):
+        if not callable(attr) or name in ("close", "view", "sweep_chains", "sweep_timed",
+                                                     "ancillary_propose_chains"):
             return attr
 
         def bound(*a, **kw):

@@ -419,8 +419,8 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
   CK(dalloc(&c->obs_idx_d, n_obs));
   CK(dalloc(&c->lm_d, n_obs));
   CK(dalloc(&c->y_d, n_obs));
-  CK(dalloc(&c->tmp_d, n));
-  CK(dalloc(&c->tmp2_d, n));
+  CK(dalloc(&c->tmp_d, (size_t)n * C));   // scratch vectors, chain-strided for batched solves
+  CK(dalloc(&c->tmp2_d, (size_t)n * C));
   CK(dalloc(&c->partials_d, 4 * kRedBlocks));
   CK(dalloc(&c->res_d, 8));
   CK(dalloc(&c->scal_d, C));
@@ -878,17 +878,27 @@ int nngp_sweep_timed(nngp_ctx* c, int n_sweeps, const double* beta0, const doubl
 }
 
 // ---------------------------------------------------------------- MH helpers
-static int tri_solve_dev(nngp_ctx* c, const double* linv, const double* u, double* x) {
+static int tri_solve_dev(nngp_ctx* c, const TriArgs& ta, const double* u, double* x) {
   for (size_t k = 0; k + 2 < c->tri_seg.size(); k += 3) {
     const int lv0 = c->tri_seg[k], lv1 = c->tri_seg[k + 1];
     if (c->tri_seg[k + 2]) {
-      HIPCHK(c, launch_tri_levels_block(c->st, c->level_rows_d, c->level_ptr_d, lv0, lv1, linv, c->nn_d, c->b, u, x));
+      HIPCHK(c, launch_tri_levels_block(c->st, ta, c->level_rows_d, c->level_ptr_d, lv0, lv1, c->nn_d, c->b, u, x));
     } else {
       const int a = c->level_ptr[lv0], e = c->level_ptr[lv1];
-      if (e > a) HIPCHK(c, launch_tri_level(c->st, c->level_rows_d + a, e - a, linv, c->nn_d, c->b, u, x));
+      if (e > a) HIPCHK(c, launch_tri_level(c->st, ta, c->level_rows_d + a, e - a, c->nn_d, c->b, u, x));
     }
   }
   return NNGP_OK;
+}
+
+static TriArgs tri_one(const double* linv) {
+  TriArgs ta;
+  std::memset(&ta, 0, sizeof ta);
+  ta.linv[0] = linv;
+  ta.kidx[0] = 0;
+  ta.nc = 1;
+  ta.stride = 1;
+  return ta;
 }
 
 int nngp_ancillary_propose(nngp_ctx* c, double beta0, double dlog_scale) {
@@ -901,8 +911,40 @@ int nngp_ancillary_propose(nngp_ctx* c, double beta0, double dlog_scale) {
   // tmp = B_cur (field - beta0)
   launch_row_stats(c->st, S.linv_d[0], c->nn_d, c->n, c->b, S.field_d, beta0, c->tmp_d, c->partials_d);
   HIPCHK(c, hipGetLastError());
-  if ((rc = tri_solve_dev(c, S.linv_d[1], c->tmp_d, c->tmp2_d))) return rc;
-  HIPCHK(c, launch_axpby_shift(c->st, c->n, c->tmp2_d, std::exp(0.5 * dlog_scale), beta0, S.field_prop_d));
+  if ((rc = tri_solve_dev(c, tri_one(S.linv_d[1]), c->tmp_d, c->tmp2_d))) return rc;
+  HIPCHK(c, launch_axpby_shift(c->st, c->n, c->tmp2_d, 1, std::exp(0.5 * dlog_scale), beta0, S.field_prop_d));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  return NNGP_OK;
+}
+
+int nngp_ancillary_propose_chains(nngp_ctx* c, int chain_mask, const double* beta0, const double* dlog_scale) {
+  if (!c || !beta0 || !dlog_scale || chain_mask <= 0 || chain_mask >= (1 << c->C)) return NNGP_ERR_ARG;
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  TriArgs ta;
+  std::memset(&ta, 0, sizeof ta);
+  ta.stride = c->C;
+  for (int k = 0; k < c->C; ++k) {
+    if (!((chain_mask >> k) & 1)) continue;
+    ChainState& S = c->ch[k];
+    if (!S.have_factor[0] || !S.have_factor[1] || !S.have_field) {
+      char buf[96];
+      std::snprintf(buf, sizeof buf, "ancillary_propose_chains: chain %d needs both factors and the field", k);
+      return fail_msg(c, NNGP_ERR_STATE, buf);
+    }
+    // tmp[d*C + k] = B_cur (field - beta0)
+    launch_row_stats(c->st, S.linv_d[0], c->nn_d, c->n, c->b, S.field_d, beta0[k], c->tmp_d + k, c->partials_d,
+                     nullptr, nullptr, c->C);
+    HIPCHK(c, hipGetLastError());
+    ta.linv[ta.nc] = S.linv_d[1];
+    ta.kidx[ta.nc] = k;
+    ++ta.nc;
+  }
+  if ((rc = tri_solve_dev(c, ta, c->tmp_d, c->tmp2_d))) return rc;
+  for (int k = 0; k < c->C; ++k)
+    if ((chain_mask >> k) & 1)
+      HIPCHK(c, launch_axpby_shift(c->st, c->n, c->tmp2_d + k, c->C, std::exp(0.5 * dlog_scale[k]), beta0[k],
+                                   c->ch[k].field_prop_d));
   HIPCHK(c, hipStreamSynchronize(c->st));
   return NNGP_OK;
 }
@@ -990,7 +1032,7 @@ int nngp_tri_solve(nngp_ctx* c, int which, const double* u, double* x) {
   std::vector<double> in(c->n), outv(c->n);
   for (int i = 0; i < c->n; ++i) in[c->dpos[i]] = u[i];
   HIPCHK(c, hipMemcpyAsync(c->tmp_d, in.data(), c->n * sizeof(double), hipMemcpyHostToDevice, c->st));
-  if ((rc = tri_solve_dev(c, S.linv_d[which], c->tmp_d, c->tmp2_d))) return rc;
+  if ((rc = tri_solve_dev(c, tri_one(S.linv_d[which]), c->tmp_d, c->tmp2_d))) return rc;
   HIPCHK(c, hipMemcpyAsync(outv.data(), c->tmp2_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
   for (int i = 0; i < c->n; ++i) x[i] = outv[c->dpos[i]];

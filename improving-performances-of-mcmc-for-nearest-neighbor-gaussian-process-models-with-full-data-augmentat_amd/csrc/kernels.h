@@ -113,12 +113,21 @@ int launch_obs_reduce(hipStream_t st, int mode, int n_obs, const double* y, cons
                       double beta0, const int* locs_match0, const double* field,
                       const double* field_new, double inv_2var, double* partials);
 
-hipError_t launch_tri_level(hipStream_t st, const int* rows, int nrows, const double* linv,
-                            const int* nn, int b, const double* u, double* x);
-// levels [lv0, lv1) of the DAG (each <= 1024 rows) in one 1024-thread workgroup
-hipError_t launch_tri_levels_block(hipStream_t st, const int* rows, const int* lptr, int lv0, int lv1,
-                                   const double* linv, const int* nn, int b, const double* u, double* x);
-hipError_t launch_axpby_shift(hipStream_t st, int n, const double* x, double scale, double shift,
+// triangular solve over up to kMaxChains chains: factor of chain slot kk =
+// linv[kk], vector element (row d, chain kidx[kk]) at d*stride + kidx[kk]
+struct TriArgs {
+  const double* linv[kMaxChains];
+  int kidx[kMaxChains];
+  int nc;
+  int stride;
+};
+hipError_t launch_tri_level(hipStream_t st, const TriArgs& a, const int* rows, int nrows, const int* nn, int b,
+                            const double* u, double* x);
+// levels [lv0, lv1) of the DAG (small ones) in one 1024-thread workgroup
+hipError_t launch_tri_levels_block(hipStream_t st, const TriArgs& a, const int* rows, const int* lptr, int lv0,
+                                   int lv1, const int* nn, int b, const double* u, double* x);
+// y[i] = shift + scale * x[i*xstride]
+hipError_t launch_axpby_shift(hipStream_t st, int n, const double* x, int xstride, double scale, double shift,
                               double* y);
 
 // busy-wait on the device for `seconds` (bounded; measurement helper)

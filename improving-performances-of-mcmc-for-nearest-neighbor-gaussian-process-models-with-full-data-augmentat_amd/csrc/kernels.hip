@@ -866,71 +866,68 @@ int launch_obs_reduce(hipStream_t st, int mode, int n_obs, const double* y, cons
 }
 
 // ------------------------------------------------------------------ tri solve
-__global__ void tri_level_kernel(const int* __restrict__ rows, int nrows, const double* __restrict__ linv,
+// Sparse triangular solve B x = u for up to 4 chains at once (same DAG, per
+// chain factor): work item = (row of the level, chain slot kk); u and x are
+// chain-strided (element d*stride + kidx[kk]).  One chain: stride 1.
+__device__ __forceinline__ void tri_row(const TriArgs& a, int i, int kk, const int* __restrict__ nn, int b,
+                                        const double* __restrict__ u, double* __restrict__ x) {
+  const double* lr = a.linv[kk] + (size_t)i * b;
+  const int* nr = nn + (size_t)i * b;
+  const int k = a.kidx[kk], S = a.stride;
+  double s = u[(size_t)i * S + k];
+  for (int j = 1; j < b; ++j) {
+    int idx = nr[j];
+    if (idx >= 0) s -= lr[j] * x[(size_t)idx * S + k];
+  }
+  x[(size_t)i * S + k] = s / lr[0];
+}
+
+__global__ void tri_level_kernel(TriArgs a, const int* __restrict__ rows, int nrows,
                                  const int* __restrict__ nn, int b, const double* __restrict__ u,
                                  double* __restrict__ x) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nrows) return;
-  int i = rows[t];
-  const double* lr = linv + (size_t)i * b;
-  const int* nr = nn + (size_t)i * b;
-  double s = u[i];
-  for (int j = 1; j < b; ++j) {
-    int idx = nr[j];
-    if (idx >= 0) s -= lr[j] * x[idx];
-  }
-  x[i] = s / lr[0];
+  if (t >= nrows * a.nc) return;
+  tri_row(a, rows[t / a.nc], t % a.nc, nn, b, u, x);
 }
 
-hipError_t launch_tri_level(hipStream_t st, const int* rows, int nrows, const double* linv,
-                            const int* nn, int b, const double* u, double* x) {
-  int g = (nrows + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(tri_level_kernel, dim3(g), dim3(kBlock), 0, st, rows, nrows, linv, nn, b, u, x);
+hipError_t launch_tri_level(hipStream_t st, const TriArgs& a, const int* rows, int nrows, const int* nn, int b,
+                            const double* u, double* x) {
+  int g = (nrows * a.nc + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(tri_level_kernel, dim3(g), dim3(kBlock), 0, st, a, rows, nrows, nn, b, u, x);
   return hipGetLastError();
 }
 
 // A run of consecutive SMALL levels of the Vecchia DAG in one workgroup:
-// the rows of level lv are rows[lptr[lv] .. lptr[lv+1]) (<= blockDim each);
-// the workgroup barrier between levels replaces a kernel launch (same
-// arithmetic as tri_level_kernel).
-__global__ __launch_bounds__(1024) void tri_levels_block_kernel(const int* __restrict__ rows,
+// the rows of level lv are rows[lptr[lv] .. lptr[lv+1]); the workgroup
+// barrier between levels replaces a kernel launch (same arithmetic as
+// tri_level_kernel).
+__global__ __launch_bounds__(1024) void tri_levels_block_kernel(TriArgs a, const int* __restrict__ rows,
                                                                 const int* __restrict__ lptr, int lv0, int lv1,
-                                                                const double* __restrict__ linv,
                                                                 const int* __restrict__ nn, int b,
                                                                 const double* __restrict__ u, double* x) {
   for (int lv = lv0; lv < lv1; ++lv) {
-    const int a = lptr[lv], e = lptr[lv + 1];
-    for (int t = a + (int)threadIdx.x; t < e; t += blockDim.x) {
-      const int i = rows[t];
-      const double* lr = linv + (size_t)i * b;
-      const int* nr = nn + (size_t)i * b;
-      double s = u[i];
-      for (int j = 1; j < b; ++j) {
-        const int idx = nr[j];
-        if (idx >= 0) s -= lr[j] * x[idx];
-      }
-      x[i] = s / lr[0];
-    }
+    const int r0 = lptr[lv], cnt = (lptr[lv + 1] - r0) * a.nc;
+    for (int t = (int)threadIdx.x; t < cnt; t += blockDim.x) tri_row(a, rows[r0 + t / a.nc], t % a.nc, nn, b, u, x);
     __syncthreads();
   }
 }
 
-hipError_t launch_tri_levels_block(hipStream_t st, const int* rows, const int* lptr, int lv0, int lv1,
-                                   const double* linv, const int* nn, int b, const double* u, double* x) {
-  hipLaunchKernelGGL(tri_levels_block_kernel, dim3(1), dim3(1024), 0, st, rows, lptr, lv0, lv1, linv, nn, b, u, x);
+hipError_t launch_tri_levels_block(hipStream_t st, const TriArgs& a, const int* rows, const int* lptr, int lv0,
+                                   int lv1, const int* nn, int b, const double* u, double* x) {
+  hipLaunchKernelGGL(tri_levels_block_kernel, dim3(1), dim3(1024), 0, st, a, rows, lptr, lv0, lv1, nn, b, u, x);
   return hipGetLastError();
 }
 
-__global__ void axpby_shift_kernel(int n, const double* __restrict__ x, double scale, double shift,
+__global__ void axpby_shift_kernel(int n, const double* __restrict__ x, int xstride, double scale, double shift,
                                    double* __restrict__ y) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) y[i] = shift + scale * x[i];
+  if (i < n) y[i] = shift + scale * x[(size_t)i * xstride];
 }
 
-hipError_t launch_axpby_shift(hipStream_t st, int n, const double* x, double scale, double shift,
+hipError_t launch_axpby_shift(hipStream_t st, int n, const double* x, int xstride, double scale, double shift,
                               double* y) {
   int g = (n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(axpby_shift_kernel, dim3(g), dim3(kBlock), 0, st, n, x, scale, shift, y);
+  hipLaunchKernelGGL(axpby_shift_kernel, dim3(g), dim3(kBlock), 0, st, n, x, xstride, scale, shift, y);
   return hipGetLastError();
 }
 

@@ -62,9 +62,10 @@ def _interweave_prep(ctx, X, va):
 
 def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_iterations_update,
                    field_thinning, ancillary, n_chromatic, iter_start, seed):
-    """Chain i's n_iterations_update Gibbs iterations; yields its sweep
-    requests (n_sweeps, beta_0, log_scale, log_noise_variance, key, counter)
-    and returns {"state", "records", "acceptance"}."""
+    """Chain i's n_iterations_update Gibbs iterations; yields its device
+    requests -- ("anc", beta_0, dlog_scale, ok) for the ancillary proposal and
+    ("sweep", n_sweeps, beta_0, log_scale, log_noise_variance, key, counter)
+    for the chromatic sweeps -- and returns {"state", "records", "acceptance"}."""
     rng = np.random.default_rng(int(iter_start) + i + 1)
     key = _philox_key(iter_start, i + 1, seed)
     covfun = space_time_model["covfun"]["stationary_covfun"]
@@ -111,8 +112,10 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
                 ctx.factor(1, covfun, covparms(sp_names, new_shape))
             except Exception:
                 ok = False  # non-PD local covariance: the proposal is rejected
+            # every chain stops here each iteration (ok=False: nothing to
+            # propose) so the chains of one context stay in lockstep
+            yield ("anc", params["beta_0"], new_ls - params["log_scale"], ok)
             if ok:
-                ctx.ancillary_propose(params["beta_0"], new_ls - params["log_scale"])
                 ratio = ctx.field_response_ratio(params["beta_0"], params["log_noise_variance"])
                 if ratio > np.log(rng.uniform()):
                     params["shape"] = new_shape
@@ -185,7 +188,7 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
         ctx.set_mu(mu_of(), params["beta_0"])
 
         # ---- chromatic sampling of the field (:257-275)
-        yield (n_chromatic, params["beta_0"], params["log_scale"], params["log_noise_variance"],
+        yield ("sweep", n_chromatic, params["beta_0"], params["log_scale"], params["log_noise_variance"],
                key, (int(iter_start) + it - 1) * n_chromatic)
 
         # ---- noise variance (:281-293)
@@ -213,23 +216,61 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
                            "covariance_acceptance_ancillary": acc_anc}}
 
 
+def _serve_one(ctx, req):
+    if req[0] == "anc":
+        if req[3]:
+            ctx.ancillary_propose(req[1], req[2])
+    else:
+        ctx.sweep(*req[1:])
+
+
 def _run_chain(i, state, ctx, X, observed_field, space_time_model, va, n_iterations_update,
                field_thinning, ancillary, n_chromatic, iter_start, seed):
-    """One chain alone (each sweep through ctx.sweep)."""
+    """One chain alone (each request served on its own)."""
     prog = _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_iterations_update,
                           field_thinning, ancillary, n_chromatic, iter_start, seed)
     try:
         req = next(prog)
         while True:
-            ctx.sweep(*req)
+            _serve_one(ctx, req)
             req = next(prog)
     except StopIteration as stop:
         return stop.value
 
 
+def _serve_group(owner, ids, reqs, contexts):
+    """Serve the same-kind requests of the chains `ids` of one ChainContext
+    with one batched call; False if they cannot be batched."""
+    if owner is None or owner.n_chains < 2:
+        return False
+    kinds = {reqs[i][0] for i in ids}
+    if len(kinds) != 1:
+        return False
+    kind = kinds.pop()
+    k = owner.n_chains
+    if kind == "anc":
+        mask, b0, dls = 0, np.zeros(k), np.zeros(k)
+        for i in ids:
+            _, beta0, dl, ok = reqs[i]
+            if ok:
+                c = contexts[i].chain
+                mask |= 1 << c
+                b0[c], dls[c] = beta0, dl
+        if mask:
+            owner.ancillary_propose_chains(mask, b0, dls)
+        return True
+    if len(ids) != k or len({reqs[i][1] for i in ids}) != 1:
+        return False
+    order = sorted(ids, key=lambda i: contexts[i].chain)
+    cols = list(zip(*[reqs[i][1:] for i in order]))
+    owner.sweep_chains(cols[0][0], cols[1], cols[2], cols[3], cols[4], cols[5])
+    return True
+
+
 def _drive(programs, contexts):
-    """Advance chain programs in lockstep; the sweeps of all chains of one
-    ChainContext go through one sweep_chains call."""
+    """Advance chain programs in lockstep; the requests of the chains of one
+    ChainContext go through one batched call (sweep_chains /
+    ancillary_propose_chains)."""
     results = [None] * len(programs)
     reqs = {}
     for i, g in enumerate(programs):
@@ -244,14 +285,9 @@ def _drive(programs, contexts):
             groups.setdefault(id(owner) if owner is not None else ("solo", i), []).append(i)
         for ids in groups.values():
             owner = getattr(contexts[ids[0]], "ctx", None)
-            same_n = len({reqs[i][0] for i in ids}) == 1
-            if owner is not None and len(ids) == owner.n_chains and same_n and owner.n_chains > 1:
-                order = sorted(ids, key=lambda i: contexts[i].chain)
-                cols = list(zip(*[reqs[i] for i in order]))
-                owner.sweep_chains(cols[0][0], cols[1], cols[2], cols[3], cols[4], cols[5])
-            else:
+            if not _serve_group(owner, ids, reqs, contexts):
                 for i in ids:
-                    contexts[i].sweep(*reqs[i])
+                    _serve_one(contexts[i], reqs[i])
         nxt = {}
         for i in reqs:
             try:

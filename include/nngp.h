@@ -32,7 +32,7 @@
  *   nngp_sweep_chains ........ the same for every chain (mclapply over chains,
  *                              update_Gaussian.R:25-26, around :257-275)
  *   nngp_ancillary_propose ... new_field, update_Gaussian.R:127 (SpMV + sparse
- *                              triangular solve)
+ *                              triangular solve); _chains: every chain at once
  *   nngp_field_response_ratio  dnorm ratio, update_Gaussian.R:129-131
  *   nngp_beta0_stats ......... beta_0 Gibbs block, update_Gaussian.R:221-222
  *   nngp_sum_squared_residuals update_Gaussian.R:281
@@ -159,6 +159,12 @@ int nngp_sweep_chains(nngp_ctx* ctx, int n_sweeps, const double* beta0, const do
 /* Ancillary proposal: proposal field = beta0 + exp(0.5*dlog_scale) *
  * B_prop^{-1} (B_cur (field - beta0)) (update_Gaussian.R:127). */
 int nngp_ancillary_propose(nngp_ctx* ctx, double beta0, double dlog_scale);
+/* nngp_ancillary_propose for the chains in chain_mask (bit k = chain k) in
+ * the same kernels (one triangular-solve schedule for all of them); beta0 and
+ * dlog_scale have n_chains entries (others ignored).  Chain k's proposal is
+ * bitwise identical to nngp_ancillary_propose on chain k alone. */
+int nngp_ancillary_propose_chains(nngp_ctx* ctx, int chain_mask, const double* beta0,
+                                  const double* dlog_scale);
 /* sum dnorm(y | proposal) - sum dnorm(y | field), sd = exp(lnv/2) (A8) */
 int nngp_field_response_ratio(nngp_ctx* ctx, double beta0, double log_noise_variance,
                               double* ratio);

@@ -34,3 +34,21 @@ t("beta0_stats", lambda: ctx.beta0_stats())
 t("sum_squared_residuals", lambda: ctx.sum_squared_residuals(1.0))
 t("sweep x10 (1 chain)", lambda: ctx.sweep(10, 1.0, 0.0, np.log(0.25), 7, 0))
 ctx.close()
+
+# 3 chains in one context: per-chain calls vs the batched ones
+C = 3
+ctx = bench.open_context(P, wl, "matern15_isotropic", cp, 0, C, seed=3)
+for k in range(C):
+    ctx.select(k).factor(1, "matern15_isotropic", [1.0, 0.051, 0.0])
+
+
+def anc_seq():
+    for k in range(C):
+        ctx.select(k).ancillary_propose(1.0, 0.01)
+
+
+t("ancillary x3 per chain", anc_seq)
+t("ancillary_propose_chains x3", lambda: ctx.ancillary_propose_chains(7, [1.0] * C, [0.01] * C))
+t("sweep_chains x10 (3 chains)", lambda: ctx.sweep_chains(10, [1.0] * C, [0.0] * C, [np.log(0.25)] * C,
+                                                          [7, 8, 9], [0] * C))
+ctx.close()

@@ -408,3 +408,47 @@ def test_blocked_tri_solve_equals_level_schedule(P, O, n, m, monkeypatch):
     for g, r in zip(got, ref):
         np.testing.assert_array_equal(g, r)
     np.testing.assert_allclose(got[0], O.tri_solve(Lo, NN, us[0]), rtol=1e-9, atol=1e-10)
+
+
+@pytest.mark.parametrize("n,m,C,mask", [(5000, 5, 3, 0b101), (120000, 15, 4, 0b1111), (3000, 10, 2, 0b11)])
+def test_batched_ancillary_bitwise_equal_per_chain(P, O, n, m, C, mask):
+    """nngp_ancillary_propose_chains (one solve schedule for the masked
+    chains) gives every masked chain exactly the proposal of
+    nngp_ancillary_propose on that chain alone; chain 0 matches the oracle
+    form beta0 + exp(dls/2) B1^{-1} B0 (field - beta0) (update_Gaussian.R:127)."""
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=n + C + 5)
+    rng = np.random.default_rng(C + 11)
+    c0s = [[1.0 + 0.1 * k, 0.05 + 0.01 * k, 0.0] for k in range(C)]
+    c1s = [[1.2 + 0.1 * k, 0.06 + 0.01 * k, 0.0] for k in range(C)]
+    fields = [rng.normal(size=n) + 0.5 * k for k in range(C)]
+    b0 = np.array([0.3 * k for k in range(C)])
+    dls = np.array([0.2 - 0.1 * k for k in range(C)])
+
+    def setup(ctx):
+        for k in range(C):
+            ctx.select(k)
+            ctx.factor(0, "exponential_isotropic", c0s[k])
+            ctx.factor(1, "exponential_isotropic", c1s[k])
+            ctx.set_field(fields[k])
+            ctx.set_mu(None, b0[k])
+
+    chains = [k for k in range(C) if (mask >> k) & 1]
+    with P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=C) as ctx:
+        setup(ctx)
+        ctx.ancillary_propose_chains(mask, b0, dls)
+        got = {}
+        for k in chains:
+            ctx.select(k).accept_field()
+            got[k] = ctx.get_field()
+        untouched = [ctx.select(k).get_field() for k in range(C) if k not in chains]
+        L0, L1 = ctx.select(0).get_linv(0), ctx.select(0).get_linv(1)
+    for f, k in zip(untouched, [k for k in range(C) if k not in chains]):
+        np.testing.assert_array_equal(f, fields[k])
+    with P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=C) as seq:
+        setup(seq)
+        for k in chains:
+            seq.select(k).ancillary_propose(b0[k], dls[k])
+            seq.accept_field()
+            np.testing.assert_array_equal(got[k], seq.get_field())
+    w = O.tri_solve(L1, NN, O.linv_mult(L0, fields[0] - b0[0], NN))
+    np.testing.assert_allclose(got[0], b0[0] + np.exp(0.5 * dls[0]) * w, rtol=1e-9, atol=1e-10)
