@@ -145,6 +145,67 @@ __device__ double bessel_k(double nu, double x) {
   return rkmu;
 }
 
+// 2^(j/64), j = 0..63, correctly rounded (staged into LDS by the factor kernel)
+__constant__ double kExp2Tab[64] = {
+    1.0, 1.0108892860517005, 1.0218971486541166, 1.0330248790212284,
+    1.0442737824274138, 1.0556451783605572, 1.0671404006768237, 1.0787607977571199,
+    1.0905077326652577, 1.102382583307841, 1.1143867425958924, 1.1265216186082418,
+    1.1387886347566916, 1.1511892299529827, 1.1637248587775775, 1.1763969916502812,
+    1.189207115002721, 1.202156731452703, 1.215247359980469, 1.22848053610687,
+    1.241857812073484, 1.255380757024691, 1.2690509571917332, 1.2828700160787783,
+    1.2968395546510096, 1.3109612115247644, 1.3252366431597413, 1.339667524053303,
+    1.3542555469368927, 1.3690024229745905, 1.383909881963832, 1.3989796725383112,
+    1.4142135623730951, 1.42961333839197, 1.4451808069770467, 1.460917794180647,
+    1.4768261459394993, 1.4929077282912648, 1.5091644275934228, 1.5255981507445384,
+    1.5422108254079407, 1.559004400237837, 1.5759808451078865, 1.593142151342267,
+    1.6104903319492543, 1.6280274218573478, 1.645755478153965, 1.6636765803267364,
+    1.681792830507429, 1.7001063537185235, 1.718619298122478, 1.7373338352737062,
+    1.7562521603732995, 1.7753764925265212, 1.7947090750031072, 1.8142521755003989,
+    1.8340080864093424, 1.8539791250833855, 1.8741676341103, 1.8945759815869656,
+    1.9152065613971474, 1.9360617934922943, 1.9571441241754002, 1.978456026387951};
+
+// exp(x) for x <= 0 (the factor's correlations): x = (64 m + j) ln2/64 + r,
+// |r| <= ln2/128, exp(x) = 2^m 2^(j/64) e^r with e^r - 1 by a degree-6
+// Taylor polynomial; within 1 ulp of the correctly rounded exp (measured,
+// scripts/micro/dmath.hip).  Very negative x (including the padding
+// distances of ~1e30) gives exactly 0.
+__device__ __forceinline__ double exp_nonpos(double x, const double* tab) {
+  const double k = __builtin_rint(x * 92.33248261689366);  // 64/ln2
+  double r = __builtin_fma(-k, 0.010830424696249145, x);    // ln2/64, high part
+  r = __builtin_fma(-k, 3.623510646634843e-19, r);          // low part
+  const int ki = (int)k;                                      // saturates for huge |x|
+  double p = 1.3888888888888889e-03;
+  p = __builtin_fma(p, r, 8.3333333333333332e-03);
+  p = __builtin_fma(p, r, 4.1666666666666664e-02);
+  p = __builtin_fma(p, r, 1.6666666666666666e-01);
+  p = __builtin_fma(p, r, 0.5);
+  p = __builtin_fma(p, r, 1.0);
+  const double t = tab[ki & 63];
+  return __builtin_ldexp(__builtin_fma(p * r, t, t), ki >> 6);
+}
+
+// sqrt(s) for normal s > 0 (squared distances): hardware rsq (~2^-24) and
+// two residual corrections; correctly rounded on every sample measured.
+__device__ __forceinline__ double sqrt_pos(double s) {
+  const double y = __builtin_amdgcn_rsq(s);
+  const double h = 0.5 * y;
+  double g = s * y;
+  double e = __builtin_fma(-g, g, s);
+  g = __builtin_fma(e, h, g);
+  e = __builtin_fma(-g, g, s);
+  return __builtin_fma(e, h, g);
+}
+
+// 1/sqrt(s) for normal s > 0: hardware rsq + two Newton-Raphson steps
+// (within ~1 ulp).
+__device__ __forceinline__ double rsqrt_pos(double s) {
+  double y = __builtin_amdgcn_rsq(s);
+  const double hs = 0.5 * s;
+  y = y * __builtin_fma(-hs * y, y, 1.5);
+  y = y * __builtin_fma(-hs * y, y, 1.5);
+  return y;
+}
+
 // correlation at unit-range distance dist.  FAM 0: exponential, 1: Matern 3/2,
 // 2: general Matern with norm = 2^(1-nu)/Gamma(nu)
 template <int FAM>
@@ -208,57 +269,46 @@ hipError_t launch_scale_coords(hipStream_t st, int covfun, const double* cp, int
 // rows of a short neighbourhood (bs < BM) are padded IN FRONT with identity
 // rows, which leaves the real block's factor and solution unchanged.
 // Linv[i, j] = x[BM-1-j] with L^T x = e_last.
-template <int BM, int FAM, int DS>
-__global__ __launch_bounds__(64) void factor_kernel(double var, double nugget, double nu, double norm,
-                                                   const double* __restrict__ sc,
-                                                   const int* __restrict__ nn, int n, int b,
-                                                   double* __restrict__ linv, int* __restrict__ fail) {
-  const int i = blockIdx.x * 64 + threadIdx.x;
-  if (i >= n) return;
-  int bs = b;  // rows are in device (Morton) order: count the valid neighbours
-  while (bs > 1 && nn[(size_t)i * b + bs - 1] < 0) --bs;
-  double X[BM][DS];
-#pragma unroll
-  for (int r = 0; r < BM; ++r) {
-    const int j = BM - 1 - r;  // NNarray column feeding locsub row r
-    const int idx = (j < bs) ? nn[(size_t)i * b + j] : i;
-#pragma unroll
-    for (int k = 0; k < DS; ++k) X[r][k] = sc[(size_t)idx * DS + k];
-  }
+// One row of the factor from its neighbour coordinates xa(r, k) (locsub
+// order: the point itself last) and its count of valid neighbours bs.
+template <int BM, int FAM, int DS, class XA>
+__device__ __forceinline__ void factor_row(const XA& xa, int bs, int i, double var, double nugget, int b,
+                                           const double* __restrict__ tab, double* __restrict__ linv,
+                                           int* __restrict__ fail) {
   constexpr int T = BM * (BM + 1) / 2;
   double L[T];
   double inv[BM];
   bool bad = false;
+  // row t of the local covariance, then row t of its Cholesky factor
+  // (left-looking).  No masks: padded rows sit ~1e30 away from everything
+  // (gather_coords), so their correlations come out exactly 0.
 #pragma unroll
   for (int t = 0; t < BM; ++t) {
     const bool dt = (BM - 1 - t) >= bs;
 #pragma unroll
-    for (int q = 0; q <= t; ++q) {
-      const bool dq = (BM - 1 - q) >= bs;
-      double c;
-      if (q == t) {
-        c = dt ? 1.0 : var * (1.0 + nugget);
-      } else if (dt || dq) {
-        c = 0.0;
-      } else {
-        double s2 = 0.0;
+    for (int q = 0; q < t; ++q) {
+      double s2 = 0.0;
 #pragma unroll
-        for (int k = 0; k < DS; ++k) {
-          double u = X[t][k] - X[q][k];
-          s2 += u * u;
-        }
-        c = var * corr<FAM>(sqrt(s2), nu, norm);
+      for (int k = 0; k < DS; ++k) {
+        const double u = xa(t, k) - xa(q, k);
+        s2 = __builtin_fma(u, u, s2);
       }
-      double s = c;
+      const double dist = sqrt_pos(s2);
+      const double e = exp_nonpos(-dist, tab);
+      L[t * (t + 1) / 2 + q] = FAM == 1 ? var * ((1.0 + dist) * e) : var * e;
+    }
+#pragma unroll
+    for (int q = 0; q <= t; ++q) {
+      double s = q == t ? (dt ? 1.0 : var * (1.0 + nugget)) : L[t * (t + 1) / 2 + q];
 #pragma unroll
       for (int p = 0; p < q; ++p) s -= L[t * (t + 1) / 2 + p] * L[q * (q + 1) / 2 + p];
       if (q < t) {
         L[t * (t + 1) / 2 + q] = s * inv[q];
       } else {
         if (!(s > 0.0)) { bad = true; s = 1.0; }
-        double l = sqrt(s);
-        L[t * (t + 1) / 2 + t] = l;
-        inv[t] = 1.0 / l;
+        const double ri = rsqrt_pos(s);
+        L[t * (t + 1) / 2 + t] = s * ri;
+        inv[t] = ri;
       }
     }
   }
@@ -275,6 +325,70 @@ __global__ __launch_bounds__(64) void factor_kernel(double var, double nugget, d
 #pragma unroll
   for (int j = 0; j < BM; ++j)
     if (j < b) linv[(size_t)i * b + j] = (j < bs) ? x[BM - 1 - j] : 0.0;
+}
+
+// neighbour indices of row i (clamped to n-1; entries j >= b read as -1)
+template <int BM>
+__device__ __forceinline__ void load_nn_row(int (&nc)[BM], const int* __restrict__ nn, int i, int n, int b) {
+  const int r = i < n ? i : n - 1;
+#pragma unroll
+  for (int j = 0; j < BM; ++j) nc[j] = j < b ? __builtin_nontemporal_load(nn + (size_t)r * b + j) : -1;
+}
+
+// coordinates feeding locsub row r = NNarray column BM-1-r (missing
+// neighbours: distinct points ~1e30 away); returns the valid count bs
+template <int BM, int DS>
+__device__ __forceinline__ int gather_coords(double (&X)[BM][DS], const int (&nc)[BM],
+                                             const double* __restrict__ sc, int i, int n) {
+  const int self = i < n ? i : n - 1;
+  int bs = 1;
+#pragma unroll
+  for (int j = 1; j < BM; ++j)
+    if (nc[j] >= 0) bs = j + 1;
+#pragma unroll
+  for (int r = 0; r < BM; ++r) {
+    const int j = BM - 1 - r;
+    const int idx = (j < bs) ? nc[j] : self;
+#pragma unroll
+    for (int k = 0; k < DS; ++k) {
+      const double v = sc[(size_t)idx * DS + k];
+      X[r][k] = (j < bs) ? v : (k == 0 ? 1e30 * (r + 1) : 0.0);  // padding: far apart from all
+    }
+  }
+  return bs;
+}
+
+// Grid-stride over groups of 64 rows with a two-deep software pipeline: the
+// next group's coordinate gathers and the group after's neighbour indices
+// are in flight while this group's covariance/Cholesky runs (one wave per
+// SIMD fits the register footprint, so no other wave hides that latency).
+template <int BM, int FAM, int DS>
+__global__ __launch_bounds__(64) void factor_kernel(double var, double nugget, double nu, double norm,
+                                                   const double* __restrict__ sc,
+                                                   const int* __restrict__ nn, int n, int b,
+                                                   double* __restrict__ linv, int* __restrict__ fail) {
+  __shared__ double tab[64];
+  tab[threadIdx.x] = kExp2Tab[threadIdx.x];
+  __syncthreads();
+  const int stride = gridDim.x * 64;
+  int i = blockIdx.x * 64 + threadIdx.x;
+  int nc[BM], nx[BM];
+  double X[BM][DS];
+  load_nn_row<BM>(nc, nn, i, n, b);
+  int bs = gather_coords<BM, DS>(X, nc, sc, i, n);
+  load_nn_row<BM>(nx, nn, i + stride, n, b);
+  for (int base = blockIdx.x * 64; base < n; base += stride, i += stride) {
+    double Xn[BM][DS];
+    const int bsn = gather_coords<BM, DS>(Xn, nx, sc, i + stride, n);
+    load_nn_row<BM>(nx, nn, i + 2 * stride, n, b);
+    if (i < n)
+      factor_row<BM, FAM, DS>([&](int r, int k) { return X[r][k]; }, bs, i, var, nugget, b, tab, linv, fail);
+#pragma unroll
+    for (int r = 0; r < BM; ++r)
+#pragma unroll
+      for (int k = 0; k < DS; ++k) X[r][k] = Xn[r][k];
+    bs = bsn;
+  }
 }
 
 // Runtime-b variant (b <= 32, and the general Matern family whose Bessel
@@ -334,16 +448,50 @@ __global__ __launch_bounds__(64) void factor_kernel_rt(double var, double nugget
   for (int j = 0; j < b; ++j) linv[(size_t)i * b + j] = (j < bs) ? x[bs - 1 - j] : 0.0;
 }
 
+// Planar coordinates (DS = 2): the coordinates of the next group of 64 rows
+// are DMA'd global -> LDS (global_load_lds_dwordx4, one 16-byte point per
+// lane and neighbour) into the second of two stages while this group
+// computes, so the in-flight coordinates occupy no VGPRs (the factor's L
+// needs nearly all of them).  Stage layout [r][lane] x 16 B; 32 KB per
+// one-wave workgroup at BM = 16.  Missing neighbours load the point itself
+// and read back as the far-away padding of gather_coords.
 #define NNGP_FACTOR_ARGS var, nugget, nu, norm, sc, nn, n, b, linv, fail
+// workgroups of a grid-stride kernel: NNGP_FACTOR_GRID (default 2) x the
+// resident one-wave workgroups of the current device, at most the row
+// groups.  Twice resident measured best at n = 1e6 (0.350 vs 0.354 ms at 1x,
+// 0.373 at 4x): a shorter last round without giving up the pipeline.
+static int resident_grid(const void* kern, int groups) {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                              hipSuccess || cus <= 0)
+    cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, 0) != hipSuccess || per_cu <= 0) per_cu = 4;
+  static const int mult = [] {
+    const char* e = std::getenv("NNGP_FACTOR_GRID");
+    int v = e ? std::atoi(e) : 2;
+    return v >= 1 && v <= 64 ? v : 2;
+  }();
+  const long long g = (long long)cus * per_cu * mult;
+  return (int)(g < groups ? g : groups);
+}
+
+template <int BM, int FAM, int DS>
+static hipError_t launch_factor_one(hipStream_t st, double var, double nugget, double nu, double norm,
+                                    const double* sc, const int* nn, int n, int b, double* linv, int* fail) {
+  const auto kern = factor_kernel<BM, FAM, DS>;
+  const int g = resident_grid(reinterpret_cast<const void*>(kern), (n + 63) / 64);
+  hipLaunchKernelGGL(kern, dim3(g), dim3(64), 0, st, NNGP_FACTOR_ARGS);
+  return hipGetLastError();
+}
+
 template <int BM, int FAM>
 static hipError_t launch_factor_ds(hipStream_t st, int ds, double var, double nugget, double nu,
                                    double norm, const double* sc, const int* nn, int n, int b,
                                    double* linv, int* fail) {
-  int g = (n + 63) / 64;
   switch (ds) {
-    case 2: hipLaunchKernelGGL((factor_kernel<BM, FAM, 2>), dim3(g), dim3(64), 0, st, NNGP_FACTOR_ARGS); break;
-    case 3: hipLaunchKernelGGL((factor_kernel<BM, FAM, 3>), dim3(g), dim3(64), 0, st, NNGP_FACTOR_ARGS); break;
-    case 4: hipLaunchKernelGGL((factor_kernel<BM, FAM, 4>), dim3(g), dim3(64), 0, st, NNGP_FACTOR_ARGS); break;
+    case 2: return launch_factor_one<BM, FAM, 2>(st, NNGP_FACTOR_ARGS);
+    case 3: return launch_factor_one<BM, FAM, 3>(st, NNGP_FACTOR_ARGS);
+    case 4: return launch_factor_one<BM, FAM, 4>(st, NNGP_FACTOR_ARGS);
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -869,31 +1017,49 @@ int launch_obs_reduce(hipStream_t st, int mode, int n_obs, const double* y, cons
 // Sparse triangular solve B x = u for up to 4 chains at once (same DAG, per
 // chain factor): work item = (row of the level, chain slot kk); u and x are
 // chain-strided (element d*stride + kidx[kk]).  One chain: stride 1.
+// b <= BMAX (ctx_create caps b at 32): the row's neighbour indices, then its
+// gathers, are all issued before the first use -- two memory round trips per
+// row instead of 2(b-1) -- and subtracted in neighbour order.
+template <int BMAX>
 __device__ __forceinline__ void tri_row(const TriArgs& a, int i, int kk, const int* __restrict__ nn, int b,
                                         const double* __restrict__ u, double* __restrict__ x) {
   const double* lr = a.linv[kk] + (size_t)i * b;
   const int* nr = nn + (size_t)i * b;
   const int k = a.kidx[kk], S = a.stride;
   double s = u[(size_t)i * S + k];
-  for (int j = 1; j < b; ++j) {
-    int idx = nr[j];
-    if (idx >= 0) s -= lr[j] * x[(size_t)idx * S + k];
+  int idx[BMAX];
+  double xv[BMAX], lv[BMAX];
+#pragma unroll
+  for (int j = 1; j < BMAX; ++j) idx[j] = j < b ? __builtin_nontemporal_load(nr + j) : -1;
+#pragma unroll
+  for (int j = 1; j < BMAX; ++j) {
+    xv[j] = idx[j] >= 0 ? x[(size_t)idx[j] * S + k] : 0.0;
+    lv[j] = idx[j] >= 0 ? lr[j] : 0.0;
   }
+#pragma unroll
+  for (int j = 1; j < BMAX; ++j)
+    if (idx[j] >= 0) s -= lv[j] * xv[j];
   x[(size_t)i * S + k] = s / lr[0];
 }
 
+template <int BMAX>
 __global__ void tri_level_kernel(TriArgs a, const int* __restrict__ rows, int nrows,
                                  const int* __restrict__ nn, int b, const double* __restrict__ u,
                                  double* __restrict__ x) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nrows * a.nc) return;
-  tri_row(a, rows[t / a.nc], t % a.nc, nn, b, u, x);
+  tri_row<BMAX>(a, rows[t / a.nc], t % a.nc, nn, b, u, x);
 }
 
 hipError_t launch_tri_level(hipStream_t st, const TriArgs& a, const int* rows, int nrows, const int* nn, int b,
                             const double* u, double* x) {
   int g = (nrows * a.nc + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(tri_level_kernel, dim3(g), dim3(kBlock), 0, st, a, rows, nrows, nn, b, u, x);
+  if (b <= 8)
+    hipLaunchKernelGGL(tri_level_kernel<8>, dim3(g), dim3(kBlock), 0, st, a, rows, nrows, nn, b, u, x);
+  else if (b <= 16)
+    hipLaunchKernelGGL(tri_level_kernel<16>, dim3(g), dim3(kBlock), 0, st, a, rows, nrows, nn, b, u, x);
+  else
+    hipLaunchKernelGGL(tri_level_kernel<32>, dim3(g), dim3(kBlock), 0, st, a, rows, nrows, nn, b, u, x);
   return hipGetLastError();
 }
 
@@ -901,20 +1067,28 @@ hipError_t launch_tri_level(hipStream_t st, const TriArgs& a, const int* rows, i
 // the rows of level lv are rows[lptr[lv] .. lptr[lv+1]); the workgroup
 // barrier between levels replaces a kernel launch (same arithmetic as
 // tri_level_kernel).
+template <int BMAX>
 __global__ __launch_bounds__(1024) void tri_levels_block_kernel(TriArgs a, const int* __restrict__ rows,
                                                                 const int* __restrict__ lptr, int lv0, int lv1,
                                                                 const int* __restrict__ nn, int b,
                                                                 const double* __restrict__ u, double* x) {
   for (int lv = lv0; lv < lv1; ++lv) {
     const int r0 = lptr[lv], cnt = (lptr[lv + 1] - r0) * a.nc;
-    for (int t = (int)threadIdx.x; t < cnt; t += blockDim.x) tri_row(a, rows[r0 + t / a.nc], t % a.nc, nn, b, u, x);
+    for (int t = (int)threadIdx.x; t < cnt; t += blockDim.x) tri_row<BMAX>(a, rows[r0 + t / a.nc], t % a.nc, nn, b, u, x);
     __syncthreads();
   }
 }
 
 hipError_t launch_tri_levels_block(hipStream_t st, const TriArgs& a, const int* rows, const int* lptr, int lv0,
                                    int lv1, const int* nn, int b, const double* u, double* x) {
-  hipLaunchKernelGGL(tri_levels_block_kernel, dim3(1), dim3(1024), 0, st, a, rows, lptr, lv0, lv1, nn, b, u, x);
+  if (b <= 8)
+    hipLaunchKernelGGL(tri_levels_block_kernel<8>, dim3(1), dim3(1024), 0, st, a, rows, lptr, lv0, lv1, nn, b, u, x);
+  else if (b <= 16)
+    hipLaunchKernelGGL(tri_levels_block_kernel<16>, dim3(1), dim3(1024), 0, st, a, rows, lptr, lv0, lv1, nn, b, u,
+                       x);
+  else
+    hipLaunchKernelGGL(tri_levels_block_kernel<32>, dim3(1), dim3(1024), 0, st, a, rows, lptr, lv0, lv1, nn, b, u,
+                       x);
   return hipGetLastError();
 }
 

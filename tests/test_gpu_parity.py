@@ -452,3 +452,20 @@ def test_batched_ancillary_bitwise_equal_per_chain(P, O, n, m, C, mask):
             np.testing.assert_array_equal(got[k], seq.get_field())
     w = O.tri_solve(L1, NN, O.linv_mult(L0, fields[0] - b0[0], NN))
     np.testing.assert_allclose(got[0], b0[0] + np.exp(0.5 * dls[0]) * w, rtol=1e-9, atol=1e-10)
+
+
+@pytest.mark.parametrize("m", [3, 7, 15, 20, 31])
+def test_tri_solve_every_row_width(P, O, m):
+    """The solve's row kernel is specialised on b = m+1 (<= 8, 16, 32):
+    each variant matches the oracle, batched over chains too."""
+    n = 6000
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=m)
+    rng = np.random.default_rng(m)
+    u = rng.normal(size=n)
+    with P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=2) as ctx:
+        for k in range(2):
+            ctx.select(k).factor(0, "exponential_isotropic", [1.0, 0.08 + 0.02 * k, 0.01])
+        got = [ctx.select(k).tri_solve(0, u) for k in range(2)]
+        Ls = [ctx.select(k).get_linv(0) for k in range(2)]
+    for g, L in zip(got, Ls):
+        np.testing.assert_allclose(g, O.tri_solve(L, NN, u), rtol=1e-9, atol=1e-10)
