@@ -124,6 +124,48 @@ def cpu_baseline(P, wl, covfun, cp, budget_s, chains):
             "local_form_value_1_thread": loc[0][0] / loc[0][1]}
 
 
+def mcmc_iterations(P, wl, covfun, cp, ctx, iters, warmup, sync):
+    """Secondary metric: full MCMC iterations of
+    update_Gaussian.R:101-313 (ancillary + sufficient covariance MH steps,
+    beta_0 Gibbs step, n_chromatic = 10 sweeps, noise-variance MH, records with
+    field_thinning = 1) for every chain of ctx, through the package's
+    mcmc_nngp_update_Gaussian (chains driven in lockstep).  -> iterations/s of
+    the whole chain set and seconds per iteration."""
+    n = len(wl["y"])
+    C = ctx.n_chains
+    va = {"NNarray": wl["NN"], "coloring": wl["col"], "locs_match": wl["lm"], "n_obs": n, "n_locs": n}
+    stm = {"response_model": "Gaussian",
+           "covfun": {"stationary_covfun": covfun, "shape_params": ["log_range"]}}
+    rng = np.random.default_rng(11)
+    states = {}
+    for k in range(C):
+        states[f"chain_{k + 1}"] = {
+            "params": {"shape": np.array([np.log(cp[1]) + 0.05 * rng.normal()]), "beta_0": wl["beta0"],
+                       "beta": None, "log_scale": wl["log_scale"],
+                       "log_noise_variance": wl["log_noise_variance"], "field": wl["field0"].copy()},
+            "transition_kernels": {"covariance_params_sufficient": {"logvar": -4.0},
+                                   "covariance_params_ancillary": {"logvar": -4.0},
+                                   "log_noise_variance": {"logvar": -1.0}}}
+    views = [ctx.view(k) for k in range(C)]
+    X = {"X": None, "locs": np.zeros(0, np.int64)}
+
+    def run(it, start):
+        out = P.mcmc_nngp_update_Gaussian(wl["locs"], X, wl["y"], stm, va, states, it, contexts=views,
+                                          iterations=np.array([[start, 0.0]]))
+        for name, r in out.items():
+            states[name] = r["state"]
+
+    run(warmup, 0)
+    sync()
+    t0 = time.perf_counter()
+    run(iters, warmup)
+    sync()
+    el = time.perf_counter() - t0
+    return {"metric": "MCMC iterations/s (update_Gaussian.R:101-313, n_chromatic=10, all chains of the GPU)",
+            "value": iters / el, "unit": "iterations/s", "chains": C, "iterations": iters,
+            "ms_per_iteration": el * 1e3 / iters, "field_thinning": 1.0}
+
+
 def pmc_traffic(chains, n, m):
     """Per-launch HBM bytes of the sweep kernel from the committed rocprofv3
     PMC summary of the same workload (profiles/, scripts/pmc.sh: FETCH_SIZE and
@@ -179,6 +221,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--mcmc-iters", type=int, default=10,
+                    help="timed MCMC iterations for the secondary metric (0: skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -262,6 +306,13 @@ def main():
                     "algorithmic_bytes_per_sweep": bytes_sweep,
                     "algorithmic_bytes_per_launch": bytes_sweep / info["n_colors"],
                     "launches_per_sweep": info["n_colors"]}
+    mcmc = None
+    if args.mcmc_iters > 0:
+        sync = (lambda: torch.cuda.synchronize(local_rank)) if torch.cuda.is_available() else (lambda: None)
+        try:
+            mcmc = mcmc_iterations(P, wl, covfun, cp, ctx, args.mcmc_iters, 2, sync)
+        except Exception as e:  # report, do not hide the throughput line
+            log(f"mcmc iterations failed: {e}", rank)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log(f"cpu baseline (oracle, {C} threads)...", rank)
@@ -279,7 +330,7 @@ def main():
                       "n_entries": info["n_entries"], "n_chromatic_per_call": nc,
                       "single_chain": single,
                       "parallelism": f"chains {C} per GPU x {world} GPUs (independent)"},
-           "roofline": roofline, "cpu_baseline": cpu}
+           "roofline": roofline, "cpu_baseline": cpu, "secondary": mcmc}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -60,6 +60,9 @@ struct nngp_ctx {
   int* compact_loc_d = nullptr;  // n
   double2* dr_d = nullptr;
   int* slot_dpos_d = nullptr;
+  int* dpos_d = nullptr;          // loc -> device row, on the device
+  double* stage_h = nullptr;      // pinned n-double staging for field-sized copies
+  double* perm_d = nullptr;       // device n-double scratch of those copies (R order)
   int* chunk_first_d = nullptr;  // nchunks+1
   int* loc_rank_d = nullptr;     // n: compact index of each location (Vecchia order)
   int* pairs_d = nullptr;        // normal pairs grouped by the colour of their even member
@@ -253,7 +256,8 @@ void nngp_ctx_destroy(nngp_ctx* c) {
                              c->dr_d, c->slot_dpos_d, c->ent_pk_d, c->ent_src_d, c->ent_val_d, c->w_slot_d,
                              c->r_d, c->level_rows_d, c->obs_ptr_d, c->obs_idx_d, c->lm_d, c->y_d, c->tmp_d,
                              c->tmp2_d, c->partials_d, c->res_d, c->z_d, c->scal_d, c->dbg_d,
-                             c->chunk_first_d, c->loc_rank_d, c->pairs_d, c->level_ptr_d, c->zbuf_d, c->ent_pos_d, c->start_mask_d};
+                             c->chunk_first_d, c->loc_rank_d, c->pairs_d, c->level_ptr_d, c->zbuf_d, c->ent_pos_d, c->start_mask_d,
+                             c->dpos_d, c->perm_d};
   for (int k = 0; k < kMaxChains; ++k) {
     ChainState& s = c->ch[k];
     ptrs.insert(ptrs.end(), {s.linv_d[0], s.linv_d[1], s.field_d, s.field_prop_d, s.mu_d});
@@ -262,6 +266,7 @@ void nngp_ctx_destroy(nngp_ctx* c) {
   if (c->scal_h) hipHostFree(c->scal_h);
   if (c->res_h) hipHostFree(c->res_h);
   if (c->linv_cur_h) hipHostFree(c->linv_cur_h);
+  if (c->stage_h) hipHostFree(c->stage_h);
   if (c->st) hipStreamDestroy(c->st);
   delete c;
 }
@@ -378,6 +383,9 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
   CK(dalloc(&c->compact_loc_d, NS));
   CK(dalloc(&c->dr_d, NS * C));
   CK(dalloc(&c->slot_dpos_d, NS));
+  CK(dalloc(&c->dpos_d, n));
+  CK(dalloc(&c->perm_d, n));
+  CK(hipHostMalloc((void**)&c->stage_h, sizeof(double) * n, hipHostMallocDefault));
   CK(dalloc(&c->chunk_first_d, L.chunk_first.size()));
   CK(dalloc(&c->loc_rank_d, n));
   CK(dalloc(&c->pairs_d, (n + 1) / 2));
@@ -442,6 +450,7 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
   CK(hipMemsetAsync(c->dr_d, 0, sizeof(double2) * NS * C, c->st));
   CK(hipMemsetAsync(c->w_slot_d, 0, sizeof(double) * NS * C, c->st));
   CK(upload(c->slot_dpos_d, slot_dpos.data(), NS, c->st));
+  CK(upload(c->dpos_d, dp.data(), n, c->st));
   {
     // normals: compact rank of each location; pair p = (2p, 2p+1) is generated
     // by the colour of 2p, pairs ordered by the compact rank of 2p
@@ -624,15 +633,30 @@ int nngp_get_precision_diag(nngp_ctx* c, double* D) {
 }
 
 // ---------------------------------------------------------------- state
+// field-sized host <-> device copies through the pinned stage, permuted
+// between R order and device row order on the device
+static int upload_field(nngp_ctx* c, const double* host, double* dev) {
+  std::memcpy(c->stage_h, host, sizeof(double) * c->n);
+  HIPCHK(c, hipMemcpyAsync(c->perm_d, c->stage_h, c->n * sizeof(double), hipMemcpyHostToDevice, c->st));
+  HIPCHK(c, launch_permute_scatter(c->st, c->n, c->dpos_d, c->perm_d, dev));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  return NNGP_OK;
+}
+
+static int download_field(nngp_ctx* c, const double* dev, double* host) {
+  HIPCHK(c, launch_permute_gather(c->st, c->n, c->dpos_d, dev, c->perm_d));
+  HIPCHK(c, hipMemcpyAsync(c->stage_h, c->perm_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  std::memcpy(host, c->stage_h, sizeof(double) * c->n);
+  return NNGP_OK;
+}
+
 int nngp_set_field(nngp_ctx* c, const double* field) {
   if (!c || !field) return NNGP_ERR_ARG;
   int rc;
   if ((rc = set_device(c))) return rc;
   ChainState& S = c->ch[c->cur];
-  std::vector<double> f(c->n);
-  for (int i = 0; i < c->n; ++i) f[c->dpos[i]] = field[i];
-  HIPCHK(c, hipMemcpyAsync(S.field_d, f.data(), c->n * sizeof(double), hipMemcpyHostToDevice, c->st));
-  HIPCHK(c, hipStreamSynchronize(c->st));
+  if ((rc = upload_field(c, field, S.field_d))) return rc;
   S.have_field = true;
   return NNGP_OK;
 }
@@ -643,11 +667,7 @@ int nngp_get_field(nngp_ctx* c, double* field) {
   if (!S.have_field) return fail_msg(c, NNGP_ERR_STATE, "get_field: no field");
   int rc;
   if ((rc = set_device(c))) return rc;
-  std::vector<double> f(c->n);
-  HIPCHK(c, hipMemcpyAsync(f.data(), S.field_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
-  HIPCHK(c, hipStreamSynchronize(c->st));
-  for (int i = 0; i < c->n; ++i) field[i] = f[c->dpos[i]];
-  return NNGP_OK;
+  return download_field(c, S.field_d, field);
 }
 
 int nngp_set_mu(nngp_ctx* c, const double* mu, double beta0) {
@@ -1029,14 +1049,9 @@ int nngp_tri_solve(nngp_ctx* c, int which, const double* u, double* x) {
   if (!S.have_factor[which]) return fail_msg(c, NNGP_ERR_STATE, "tri_solve: no factor");
   int rc;
   if ((rc = set_device(c))) return rc;
-  std::vector<double> in(c->n), outv(c->n);
-  for (int i = 0; i < c->n; ++i) in[c->dpos[i]] = u[i];
-  HIPCHK(c, hipMemcpyAsync(c->tmp_d, in.data(), c->n * sizeof(double), hipMemcpyHostToDevice, c->st));
+  if ((rc = upload_field(c, u, c->tmp_d))) return rc;
   if ((rc = tri_solve_dev(c, tri_one(S.linv_d[which]), c->tmp_d, c->tmp2_d))) return rc;
-  HIPCHK(c, hipMemcpyAsync(outv.data(), c->tmp2_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
-  HIPCHK(c, hipStreamSynchronize(c->st));
-  for (int i = 0; i < c->n; ++i) x[i] = outv[c->dpos[i]];
-  return NNGP_OK;
+  return download_field(c, c->tmp2_d, x);
 }
 
 int nngp_device_normals(int device, uint64_t seed, uint64_t sweep, int n, double* z) {

@@ -127,6 +127,10 @@ hipError_t launch_tri_level(hipStream_t st, const TriArgs& a, const int* rows, i
 hipError_t launch_tri_levels_block(hipStream_t st, const TriArgs& a, const int* rows, const int* lptr, int lv0,
                                    int lv1, const int* nn, int b, const double* u, double* x);
 // y[i] = shift + scale * x[i*xstride]
+// dst[i] = src[idx[i]] (gather) / dst[idx[i]] = src[i] (scatter), i < n:
+// R order <-> device row order of a field-sized vector
+hipError_t launch_permute_gather(hipStream_t st, int n, const int* idx, const double* src, double* dst);
+hipError_t launch_permute_scatter(hipStream_t st, int n, const int* idx, const double* src, double* dst);
 hipError_t launch_axpby_shift(hipStream_t st, int n, const double* x, int xstride, double scale, double shift,
                               double* y);
 

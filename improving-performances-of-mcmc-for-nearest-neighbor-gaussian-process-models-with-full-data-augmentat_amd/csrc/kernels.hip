@@ -1092,6 +1092,29 @@ hipError_t launch_tri_levels_block(hipStream_t st, const TriArgs& a, const int* 
   return hipGetLastError();
 }
 
+__global__ void permute_gather_kernel(int n, const int* __restrict__ idx, const double* __restrict__ src,
+                                      double* __restrict__ dst) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[idx[i]];
+}
+
+__global__ void permute_scatter_kernel(int n, const int* __restrict__ idx, const double* __restrict__ src,
+                                       double* __restrict__ dst) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[idx[i]] = src[i];
+}
+
+hipError_t launch_permute_gather(hipStream_t st, int n, const int* idx, const double* src, double* dst) {
+  hipLaunchKernelGGL(permute_gather_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, n, idx, src, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_permute_scatter(hipStream_t st, int n, const int* idx, const double* src, double* dst) {
+  hipLaunchKernelGGL(permute_scatter_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, n, idx, src,
+                     dst);
+  return hipGetLastError();
+}
+
 __global__ void axpby_shift_kernel(int n, const double* __restrict__ x, int xstride, double scale, double shift,
                                    double* __restrict__ y) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
