@@ -46,7 +46,9 @@ class Info(C.Structure):
     _fields_ = [("n", C.c_int), ("b", C.c_int), ("d", C.c_int), ("n_obs", C.c_int),
                 ("n_colors", C.c_int), ("n_levels", C.c_int), ("nnz", C.c_longlong),
                 ("n_entries", C.c_longlong), ("max_collen", C.c_int), ("device", C.c_int),
-                ("n_chains", C.c_int), ("lanes_per_chain", C.c_int), ("n_chunks", C.c_int)]
+                ("n_chains", C.c_int), ("lanes_per_chain", C.c_int), ("n_chunks", C.c_int),
+                ("sweep_engine", C.c_int), ("n_tiles", C.c_int), ("tile_rows_max", C.c_int),
+                ("n_ghost_cells", C.c_longlong)]
 
 
 _dp = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")

@@ -93,11 +93,35 @@ struct nngp_ctx {
   SweepScalars* scal_h = nullptr;  // pinned, C
   double* res_h = nullptr;         // pinned, 8 doubles
   unsigned long long* dbg_d = nullptr;  // NNGP_PROBE=9: per-chunk timestamps
+  // tile-resident sweep engine (engine == 1; graph_prep.h TileLayout)
+  int engine = 0;                 // 0: colour launches, 1: tiles
+  TileLayout tl;
+  int4* tb_d = nullptr;           // own batches
+  int* tb_ptr_d = nullptr;
+  uint32_t* cell_pk_d = nullptr;
+  int* cell_src_d = nullptr;
+  double* cell_val_d = nullptr;   // C x cells
+  int2* gcell_d = nullptr;
+  int* gsrc_d = nullptr;
+  double* gval_d = nullptr;       // C x ghost cells
+  int* gptr_d = nullptr;
+  int* nb_ptr_d = nullptr;
+  int* nb_d = nullptr;
+  int* erow_ptr_d = nullptr;
+  int* erow_d = nullptr;
+  double* dwx_d = nullptr;        // n x C granules of 16 B
+  unsigned* ctl_d = nullptr;      // [0] call id, [1] timeout word
+  unsigned* tmo_h = nullptr;      // pinned copy of the timeout word after each launch
+  unsigned long long* tdbg_d = nullptr;  // NNGP_PROBE=9: per-tile phase times
   std::map<long long, hipGraphExec_t> graphs;  // key: n_sweeps << 8 | chain mask
   std::vector<hipGraph_t> graph_objs;
 };
 
 namespace {
+
+constexpr int kTileNT = 512;       // threads per tile workgroup (NNGP_TILE_NT: 256, 512, 1024)
+constexpr int kTileCells = 4096;   // cells per own batch (RMAX = kTileCells / NT per thread)
+constexpr int kTileTarget = 2048;  // locations per tile (default tile count: n / this, <= CUs)
 
 thread_local std::string g_err;
 
@@ -158,9 +182,44 @@ SweepDev sweep_dev(nngp_ctx* c) {
   return L;
 }
 
+TileDev tile_dev(nngp_ctx* c) {
+  TileDev D;
+  D.batch = c->tb_d;
+  D.batch_ptr = c->tb_ptr_d;
+  D.cell_pk = c->cell_pk_d;
+  D.cell_val = c->cell_val_d;
+  D.n_cells = (long long)c->tl.cell_pk.size();
+  D.gcell = c->gcell_d;
+  D.gval = c->gval_d;
+  D.n_gcells = (long long)c->tl.gsrc.size();
+  D.gptr = c->gptr_d;
+  D.nb_ptr = c->nb_ptr_d;
+  D.nb = c->nb_d;
+  D.erow_ptr = c->erow_ptr_d;
+  D.erow = c->erow_d;
+  D.sinfo = c->sinfo_d;
+  D.slot_loc = c->compact_loc_d;
+  D.dr = c->dr_d;
+  D.w_slot = c->w_slot_d;
+  D.dwx = c->dwx_d;
+  D.r = c->r_d;
+  D.scal = c->scal_d;
+  D.ctl = c->ctl_d;
+  D.dbg = c->tdbg_d;
+  D.K = c->tl.K;
+  D.C = c->C;
+  D.T = c->tl.T;
+  D.n = c->n;
+  return D;
+}
+
 // sweep values of B + precision_diag of chain k from its current factor
 int refresh_sweep_values(nngp_ctx* c, int k) {
-  HIPCHK(c, launch_sell_refresh(c->st, sweep_dev(c), c->lay.nchunks, c->ent_src_d, c->ch[k].linv_d[0], k));
+  if (c->engine == 1)
+    HIPCHK(c, launch_tile_refresh(c->st, tile_dev(c), (int)c->tl.batch.size(), c->tl.NT, c->cell_src_d, c->gsrc_d,
+                                  c->ch[k].linv_d[0], k));
+  else
+    HIPCHK(c, launch_sell_refresh(c->st, sweep_dev(c), c->lay.nchunks, c->ent_src_d, c->ch[k].linv_d[0], k));
   c->linv_cur_h[k] = c->ch[k].linv_d[0];
   HIPCHK(c, hipMemcpyAsync(c->linv_cur_d, c->linv_cur_h, sizeof(double*) * c->C, hipMemcpyHostToDevice, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
@@ -257,7 +316,9 @@ void nngp_ctx_destroy(nngp_ctx* c) {
                              c->r_d, c->level_rows_d, c->obs_ptr_d, c->obs_idx_d, c->lm_d, c->y_d, c->tmp_d,
                              c->tmp2_d, c->partials_d, c->res_d, c->z_d, c->scal_d, c->dbg_d,
                              c->chunk_first_d, c->loc_rank_d, c->pairs_d, c->level_ptr_d, c->zbuf_d, c->ent_pos_d, c->start_mask_d,
-                             c->dpos_d, c->perm_d};
+                             c->dpos_d, c->perm_d, c->tb_d, c->tb_ptr_d, c->cell_pk_d, c->cell_src_d,
+                             c->cell_val_d, c->gcell_d, c->gsrc_d, c->gval_d, c->gptr_d, c->nb_ptr_d, c->nb_d,
+                             c->erow_ptr_d, c->erow_d, c->dwx_d, c->ctl_d, c->tdbg_d};
   for (int k = 0; k < kMaxChains; ++k) {
     ChainState& s = c->ch[k];
     ptrs.insert(ptrs.end(), {s.linv_d[0], s.linv_d[1], s.field_d, s.field_prop_d, s.mu_d});
@@ -267,6 +328,7 @@ void nngp_ctx_destroy(nngp_ctx* c) {
   if (c->res_h) hipHostFree(c->res_h);
   if (c->linv_cur_h) hipHostFree(c->linv_cur_h);
   if (c->stage_h) hipHostFree(c->stage_h);
+  if (c->tmo_h) hipHostFree(c->tmo_h);
   if (c->st) hipStreamDestroy(c->st);
   delete c;
 }
@@ -322,11 +384,58 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
     std::vector<int> f(obs_cnt.begin(), obs_cnt.end() - 1);
     for (int o = 0; o < n_obs; ++o) obs_idx[f[lm0[o]]++] = o;
   }
-  // lanes per chain: 3 chains use the 4-chain shape (measured faster than 21 lanes)
-  const int LW = n_chains == 1 ? 64 : (n_chains == 2 ? 32 : 16);
-  if (!build_sweep_layout(nn.data(), n, b, coloring, locs, d, LW, c->lay, err)) {
-    delete c;
-    return fail_msg(nullptr, NNGP_ERR_ARG, err);
+  // sweep engine: tiles (one persistent launch per call, r resident in LDS)
+  // when the tile layout fits a CU's LDS, else one launch per colour.
+  // NNGP_ENGINE=colors|tiles forces one; NNGP_TILES=T sets the tile count.
+  {
+    const char* eng = std::getenv("NNGP_ENGINE");
+    const std::string es = eng ? eng : "";
+    if (es != "" && es != "colors" && es != "tiles") {
+      delete c;
+      return fail_msg(nullptr, NNGP_ERR_ARG, "NNGP_ENGINE must be colors or tiles");
+    }
+    if (es != "colors") {
+      int cus = 0, lds_max = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 0;
+      if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeSharedMemPerBlockOptin, device) != hipSuccess) lds_max = 0;
+      int T = std::max(1, std::min(cus, (n + kTileTarget - 1) / kTileTarget));
+      if (const char* te = std::getenv("NNGP_TILES")) T = std::max(1, std::min(cus, std::atoi(te)));
+      std::string terr;
+      int NT = kTileNT;
+      if (const char* te = std::getenv("NNGP_TILE_NT")) NT = std::atoi(te);
+      if (NT != 256 && NT != 512 && NT != 1024) {
+        delete c;
+        return fail_msg(nullptr, NNGP_ERR_ARG, "NNGP_TILE_NT must be 256, 512 or 1024");
+      }
+      bool ok = cus > 0 && build_tile_layout(nn.data(), n, b, coloring, locs, d, T, NT, kTileCells / NT, c->tl, terr);
+      if (ok && tile_lds_bytes(c->tl.max_rows, n_chains, NT) > lds_max) {
+        ok = false;
+        terr = "tile layout needs " + std::to_string(tile_lds_bytes(c->tl.max_rows, n_chains, NT)) +
+               " B of LDS per tile (device: " + std::to_string(lds_max) + ")";
+      }
+      if (ok) {
+        c->engine = 1;
+      } else {
+        c->tl = TileLayout();
+        if (es == "tiles") { delete c; return fail_msg(nullptr, NNGP_ERR_ARG, "tile engine: " + terr); }
+      }
+    }
+  }
+  if (c->engine == 1) {
+    // the tile layout defines the device row and slot orders
+    SweepLayout& Lw = c->lay;
+    Lw.n = n; Lw.b = b; Lw.K = c->tl.K; Lw.nnz = c->tl.nnz; Lw.max_collen = c->tl.max_collen;
+    Lw.rpos = c->tl.rpos;
+    Lw.compact_loc = c->tl.compact_loc;
+    Lw.LW = 0; Lw.nchunks = 0;
+    Lw.n_entries = (long long)c->tl.cell_pk.size() + (long long)c->tl.gsrc.size();
+  } else {
+    // lanes per chain: 3 chains use the 4-chain shape (measured faster than 21 lanes)
+    const int LW = n_chains == 1 ? 64 : (n_chains == 2 ? 32 : 16);
+    if (!build_sweep_layout(nn.data(), n, b, coloring, locs, d, LW, c->lay, err)) {
+      delete c;
+      return fail_msg(nullptr, NNGP_ERR_ARG, err);
+    }
   }
   const SweepLayout& L = c->lay;
   static_assert(kPkRowBits == kRowBits && kPkPadRow == kPadRow, "packed entry format");
@@ -386,15 +495,58 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
   CK(dalloc(&c->dpos_d, n));
   CK(dalloc(&c->perm_d, n));
   CK(hipHostMalloc((void**)&c->stage_h, sizeof(double) * n, hipHostMallocDefault));
-  CK(dalloc(&c->chunk_first_d, L.chunk_first.size()));
   CK(dalloc(&c->loc_rank_d, n));
-  CK(dalloc(&c->pairs_d, (n + 1) / 2));
-  CK(dalloc(&c->zbuf_d, (size_t)2 * n * C));
-  CK(dalloc(&c->ent_pk_d, (size_t)L.n_entries));
-  CK(dalloc(&c->ent_pos_d, (size_t)L.n_entries));
-  CK(dalloc(&c->start_mask_d, L.start_mask.size()));
-  CK(dalloc(&c->ent_src_d, (size_t)L.n_entries));
-  CK(dalloc(&c->ent_val_d, (size_t)L.n_entries * C));
+  if (c->engine == 0) {
+    CK(dalloc(&c->chunk_first_d, L.chunk_first.size()));
+    CK(dalloc(&c->pairs_d, (n + 1) / 2));
+    CK(dalloc(&c->zbuf_d, (size_t)2 * n * C));
+    CK(dalloc(&c->ent_pk_d, (size_t)L.n_entries));
+    CK(dalloc(&c->ent_pos_d, (size_t)L.n_entries));
+    CK(dalloc(&c->start_mask_d, L.start_mask.size()));
+    CK(dalloc(&c->ent_src_d, (size_t)L.n_entries));
+    CK(dalloc(&c->ent_val_d, (size_t)L.n_entries * C));
+  } else {
+    const TileLayout& TL = c->tl;
+    const size_t nb = TL.batch.size(), ncell = TL.cell_pk.size(), ng = TL.gsrc.size();
+    CK(dalloc(&c->tb_d, nb));
+    CK(dalloc(&c->tb_ptr_d, TL.batch_ptr.size()));
+    CK(dalloc(&c->cell_pk_d, ncell));
+    CK(dalloc(&c->cell_src_d, ncell));
+    CK(dalloc(&c->cell_val_d, ncell * C));
+    CK(dalloc(&c->gcell_d, ng));
+    CK(dalloc(&c->gsrc_d, ng));
+    CK(dalloc(&c->gval_d, ng * C));
+    CK(dalloc(&c->gptr_d, TL.gptr.size()));
+    CK(dalloc(&c->nb_ptr_d, TL.nb_ptr.size()));
+    CK(dalloc(&c->nb_d, TL.nb.size()));
+    CK(dalloc(&c->erow_ptr_d, TL.erow_ptr.size()));
+    CK(dalloc(&c->erow_d, TL.erow.size()));
+    CK(dalloc(&c->dwx_d, (size_t)n * C * 2));
+    CK(dalloc(&c->ctl_d, 4));
+    CK(hipHostMalloc((void**)&c->tmo_h, sizeof(unsigned), hipHostMallocDefault));
+    *c->tmo_h = 0;
+    static_assert(sizeof(TileBatch) == sizeof(int4), "batch record");
+    CK(upload(c->tb_d, reinterpret_cast<const int4*>(TL.batch.data()), nb, c->st));
+    CK(upload(c->tb_ptr_d, TL.batch_ptr.data(), TL.batch_ptr.size(), c->st));
+    CK(upload(c->cell_pk_d, TL.cell_pk.data(), ncell, c->st));
+    CK(upload(c->cell_src_d, TL.cell_src.data(), ncell, c->st));
+    CK(hipMemsetAsync(c->cell_val_d, 0, sizeof(double) * std::max<size_t>(1, ncell * C), c->st));
+    CK(upload(c->gcell_d, reinterpret_cast<const int2*>(TL.gcell.data()), ng, c->st));
+    CK(upload(c->gsrc_d, TL.gsrc.data(), ng, c->st));
+    CK(hipMemsetAsync(c->gval_d, 0, sizeof(double) * std::max<size_t>(1, ng * C), c->st));
+    CK(upload(c->gptr_d, TL.gptr.data(), TL.gptr.size(), c->st));
+    CK(upload(c->nb_ptr_d, TL.nb_ptr.data(), TL.nb_ptr.size(), c->st));
+    CK(upload(c->nb_d, TL.nb.data(), TL.nb.size(), c->st));
+    CK(upload(c->erow_ptr_d, TL.erow_ptr.data(), TL.erow_ptr.size(), c->st));
+    CK(upload(c->erow_d, TL.erow.data(), TL.erow.size(), c->st));
+    CK(hipMemsetAsync(c->dwx_d, 0, sizeof(double) * (size_t)n * C * 2, c->st));
+    CK(hipMemsetAsync(c->ctl_d, 0, sizeof(unsigned) * 4, c->st));
+    if (const char* pr = std::getenv("NNGP_PROBE"))
+      if (std::atoi(pr) == 9 && (C == 1 || C == 3)) {
+        CK(dalloc(&c->tdbg_d, (size_t)TL.T * 8));
+        CK(hipMemsetAsync(c->tdbg_d, 0, sizeof(unsigned long long) * TL.T * 8, c->st));
+      }
+  }
   CK(dalloc(&c->w_slot_d, NS * C));
   CK(dalloc(&c->r_d, (size_t)n * C));
   CK(dalloc(&c->level_rows_d, n));
@@ -442,7 +594,7 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
     for (size_t x = 0; x < NS; ++x) {
       const int i = L.compact_loc[x];
       sd[x].x = obs_cnt[i + 1] - obs_cnt[i];
-      sd[x].y = L.slot_f0[x] | (L.collen[x] << 16);
+      sd[x].y = c->engine == 1 ? c->tl.slot_f0[x] : (L.slot_f0[x] | (L.collen[x] << 16));
     }
     CK(hipMemcpy(c->sinfo_d, sd.data(), sizeof(int2) * sd.size(), hipMemcpyHostToDevice));
     CK(hipMemcpy(c->compact_loc_d, L.compact_loc.data(), sizeof(int) * NS, hipMemcpyHostToDevice));
@@ -456,24 +608,28 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
     // by the colour of 2p, pairs ordered by the compact rank of 2p
     c->loc_rank.assign(n, 0);
     for (int x = 0; x < n; ++x) c->loc_rank[L.compact_loc[x]] = x;
-    std::vector<int> pairs;
-    pairs.reserve((n + 1) / 2);
-    c->pair_ptr.assign(L.K + 1, 0);
-    for (int col = 0; col < L.K; ++col) {
-      for (int x = L.color_loc_ptr[col]; x < L.color_loc_ptr[col + 1]; ++x)
-        if ((L.compact_loc[x] & 1) == 0) pairs.push_back(L.compact_loc[x] >> 1);
-      c->pair_ptr[col + 1] = (int)pairs.size();
-    }
-    CK(upload(c->chunk_first_d, L.chunk_first.data(), L.chunk_first.size(), c->st));
     CK(upload(c->loc_rank_d, c->loc_rank.data(), n, c->st));
-    CK(upload(c->pairs_d, pairs.data(), pairs.size(), c->st));
+    if (c->engine == 0) {
+      std::vector<int> pairs;
+      pairs.reserve((n + 1) / 2);
+      c->pair_ptr.assign(L.K + 1, 0);
+      for (int col = 0; col < L.K; ++col) {
+        for (int x = L.color_loc_ptr[col]; x < L.color_loc_ptr[col + 1]; ++x)
+          if ((L.compact_loc[x] & 1) == 0) pairs.push_back(L.compact_loc[x] >> 1);
+        c->pair_ptr[col + 1] = (int)pairs.size();
+      }
+      CK(upload(c->chunk_first_d, L.chunk_first.data(), L.chunk_first.size(), c->st));
+      CK(upload(c->pairs_d, pairs.data(), pairs.size(), c->st));
+    }
     CK(hipStreamSynchronize(c->st));
   }
-  CK(upload(c->ent_pk_d, L.ent_pk.data(), (size_t)L.n_entries, c->st));
-  CK(upload(c->ent_pos_d, L.ent_pos.data(), (size_t)L.n_entries, c->st));
-  CK(upload(c->start_mask_d, L.start_mask.data(), L.start_mask.size(), c->st));
-  CK(upload(c->ent_src_d, L.ent_src.data(), (size_t)L.n_entries, c->st));
-  CK(hipMemsetAsync(c->ent_val_d, 0, sizeof(double) * std::max<long long>(1, L.n_entries * C), c->st));
+  if (c->engine == 0) {
+    CK(upload(c->ent_pk_d, L.ent_pk.data(), (size_t)L.n_entries, c->st));
+    CK(upload(c->ent_pos_d, L.ent_pos.data(), (size_t)L.n_entries, c->st));
+    CK(upload(c->start_mask_d, L.start_mask.data(), L.start_mask.size(), c->st));
+    CK(upload(c->ent_src_d, L.ent_src.data(), (size_t)L.n_entries, c->st));
+    CK(hipMemsetAsync(c->ent_val_d, 0, sizeof(double) * std::max<long long>(1, L.n_entries * C), c->st));
+  }
   CK(hipMemcpyAsync(c->linv_cur_d, c->linv_cur_h, sizeof(double*) * C, hipMemcpyHostToDevice, c->st));
   CK(upload(c->level_rows_d, c->level_rows.data(), n, c->st));
   CK(upload(c->obs_ptr_d, obs_cnt.data(), (size_t)n + 1, c->st));
@@ -481,7 +637,7 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
   CK(upload(c->lm_d, lm_dev.data(), n_obs, c->st));
   CK(upload(c->y_d, observed_field, n_obs, c->st));
   if (const char* pr = std::getenv("NNGP_PROBE"))
-    if (std::atoi(pr) == 9) {
+    if (std::atoi(pr) == 9 && c->engine == 0) {
       CK(dalloc(&c->dbg_d, (size_t)L.nchunks * 8));
       CK(hipMemset(c->dbg_d, 0, sizeof(unsigned long long) * L.nchunks * 8));
     }
@@ -510,6 +666,10 @@ int nngp_ctx_info(const nngp_ctx* c, nngp_info* info) {
   info->n_chains = c->C;
   info->lanes_per_chain = c->lay.LW;
   info->n_chunks = c->lay.nchunks;
+  info->sweep_engine = c->engine;
+  info->n_tiles = c->engine == 1 ? c->tl.T : 0;
+  info->tile_rows_max = c->engine == 1 ? c->tl.max_rows : 0;
+  info->n_ghost_cells = c->engine == 1 ? (long long)c->tl.gsrc.size() : 0;
   return NNGP_OK;
 }
 
@@ -726,6 +886,15 @@ static int sweep_prepare(nngp_ctx* c, int k, double beta0, double log_scale, dou
   return NNGP_OK;
 }
 
+// the tile engine's bounded spins set a timeout word instead of hanging
+static int tile_timeout_check(nngp_ctx* c) {
+  if (c->engine == 1 && c->tmo_h && *c->tmo_h != 0) {
+    *c->tmo_h = 0;
+    return fail_msg(c, NNGP_ERR_HIP, "tile sweep: neighbour wait timed out (tiles not co-resident?)");
+  }
+  return NNGP_OK;
+}
+
 static int upload_scalars(nngp_ctx* c) {
   HIPCHK(c, hipMemcpyAsync(c->scal_d, c->scal_h, sizeof(SweepScalars) * c->C, hipMemcpyHostToDevice, c->st));
   return NNGP_OK;
@@ -750,10 +919,18 @@ static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, int mask, const double*
       HIPCHK(c, hipGetLastError());
     }
     // normals of sweep 0 (later sweeps' normals are generated inside the
-    // previous sweep's colour launches)
-    if (!z_dev) HIPCHK(c, launch_normals_compact(c->st, L, mask, 0, n, c->zbuf_d));
+    // previous sweep's colour launches; the tile engine draws them inline)
+    if (!z_dev && c->engine == 0) HIPCHK(c, launch_normals_compact(c->st, L, mask, 0, n, c->zbuf_d));
   }
-  if (parts & kColours) {
+  if ((parts & kColours) && c->engine == 1) {
+    TileLaunch a;
+    a.n_sweeps = n_sweeps;
+    a.chain_mask = mask;
+    a.z_in = z_dev;
+    HIPCHK(c, launch_sweep_tiles(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NT));
+    HIPCHK(c, hipMemcpyAsync(c->tmo_h, c->ctl_d + 1, sizeof(unsigned), hipMemcpyDeviceToHost, c->st));
+  }
+  if ((parts & kColours) && c->engine == 0) {
     const size_t zn = (size_t)n * c->C;
     for (int s = 0; s < n_sweeps; ++s) {
       for (int col = 0; col < c->lay.K; ++col) {
@@ -831,7 +1008,7 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
     HIPCHK(c, hipGraphLaunch(ex, c->st));
   }
   HIPCHK(c, hipStreamSynchronize(c->st));
-  return NNGP_OK;
+  return tile_timeout_check(c);
 }
 
 int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const double* log_scale,
@@ -847,6 +1024,17 @@ int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const doub
   if ((rc = graph_for(c, n_sweeps, (1 << c->C) - 1, &ex))) return rc;
   HIPCHK(c, hipGraphLaunch(ex, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
+  if ((rc = tile_timeout_check(c))) return rc;
+  if (c->tdbg_d) {
+    if (const char* path = std::getenv("NNGP_DBG_OUT")) {
+      std::vector<unsigned long long> h((size_t)c->tl.T * 8);
+      HIPCHK(c, hipMemcpy(h.data(), c->tdbg_d, h.size() * 8, hipMemcpyDeviceToHost));
+      if (FILE* f = std::fopen(path, "wb")) {
+        std::fwrite(h.data(), 8, h.size(), f);
+        std::fclose(f);
+      }
+    }
+  }
   if (c->dbg_d) {
     if (const char* path = std::getenv("NNGP_DBG_OUT")) {
       std::vector<unsigned long long> h((size_t)c->lay.nchunks * 8);
@@ -894,7 +1082,7 @@ int nngp_sweep_timed(nngp_ctx* c, int n_sweeps, const double* beta0, const doubl
   *ms = f;
   if (kernel_ms) *kernel_ms = g;
   for (auto& x : e) hipEventDestroy(x);
-  return NNGP_OK;
+  return tile_timeout_check(c);
 }
 
 // ---------------------------------------------------------------- MH helpers

@@ -441,6 +441,182 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
   return true;
 }
 
+// ---------------------------------------------------------------- tile layout
+bool build_tile_layout(const int* nn, int n, int b, const int* colors, const double* locs, int d, int T,
+                       int NT, int RMAX, TileLayout& L, std::string& err) {
+  L = TileLayout();
+  L.n = n; L.b = b; L.NT = NT; L.RMAX = RMAX;
+  if (NT < 64 || NT > 1024 || RMAX < 1 || (long long)NT * RMAX > (1 << 20)) { err = "tile layout: bad NT/RMAX"; return false; }
+  if (T < 1) T = 1;
+  if (T > n) T = n;
+  L.T = T;
+  int K = 0;
+  for (int i = 0; i < n; ++i) {
+    if (colors[i] < 1) { err = "coloring must be 1-based positive"; return false; }
+    K = std::max(K, colors[i]);
+  }
+  L.K = K;
+  std::vector<uint64_t> key;
+  morton_keys(locs, n, d, key);
+  std::vector<int> perm(n);  // Morton rank -> loc
+  std::iota(perm.begin(), perm.end(), 0);
+  std::sort(perm.begin(), perm.end(), [&](int a, int c) { return key[a] < key[c] || (key[a] == key[c] && a < c); });
+  L.rpos.resize(n);
+  for (int r = 0; r < n; ++r) L.rpos[perm[r]] = r;
+  // CSC of B: column i -> (row k, position u of i in row k)
+  std::vector<long long> cptr(n + 1, 0);
+  for (long long e = 0; e < (long long)n * b; ++e) {
+    const int a = nn[e];
+    if (a >= n) { err = "NNarray index out of range"; return false; }
+    if (a >= 0) cptr[a + 1]++;
+  }
+  for (int i = 0; i < n; ++i) cptr[i + 1] += cptr[i];
+  L.nnz = cptr[n];
+  std::vector<int> crow(L.nnz), cu(L.nnz);
+  {
+    std::vector<long long> f(cptr.begin(), cptr.end() - 1);
+    for (int k = 0; k < n; ++k)
+      for (int u = 0; u < b; ++u) {
+        const int a = nn[(size_t)k * b + u];
+        if (a < 0) continue;
+        const long long p = f[a]++;
+        crow[p] = k; cu[p] = u;
+      }
+  }
+  for (int i = 0; i < n; ++i) L.max_collen = std::max(L.max_collen, (int)(cptr[i + 1] - cptr[i]));
+  if (L.max_collen > NT * RMAX) { err = "tile layout: a column of B is longer than a batch"; return false; }
+  // tiles: contiguous Morton ranges with equal column work (collen + 1)
+  L.tile_row0.assign(T + 1, n);
+  {
+    long long tot = 0;
+    for (int i = 0; i < n; ++i) tot += (cptr[i + 1] - cptr[i]) + 1;
+    long long acc = 0;
+    int t = 0;
+    L.tile_row0[0] = 0;
+    for (int r = 0; r < n && t + 1 < T; ++r) {
+      const int i = perm[r];
+      acc += (cptr[i + 1] - cptr[i]) + 1;
+      // tile t ends when its share is reached, leaving >= 1 row per later tile
+      if (acc * T >= tot * (long long)(t + 1) || n - (r + 1) <= T - (t + 1)) L.tile_row0[++t] = r + 1;
+    }
+    while (t + 1 < T) { L.tile_row0[t + 1] = L.tile_row0[t] + 1; ++t; }
+    L.tile_row0[T] = n;
+  }
+  std::vector<int> tile_of(n);  // loc -> tile
+  for (int t = 0; t < T; ++t)
+    for (int r = L.tile_row0[t]; r < L.tile_row0[t + 1]; ++r) tile_of[perm[r]] = t;
+  // slot order: tile, colour, Morton
+  L.compact_loc.resize(n);
+  std::vector<int> slot_of(n);
+  std::vector<int> tc_ptr((size_t)T * K + 1, 0);  // slots of (tile, colour)
+  for (int i = 0; i < n; ++i) tc_ptr[(size_t)tile_of[i] * K + colors[i]]++;
+  for (size_t p = 0; p < (size_t)T * K; ++p) tc_ptr[p + 1] += tc_ptr[p];
+  {
+    std::vector<int> f(tc_ptr.begin(), tc_ptr.end() - 1);
+    for (int r = 0; r < n; ++r) {
+      const int i = perm[r];
+      const int x = f[(size_t)tile_of[i] * K + colors[i] - 1]++;
+      L.compact_loc[x] = i;
+      slot_of[i] = x;
+    }
+  }
+  L.slot_f0.assign(n, 0);
+  L.batch_ptr.assign((size_t)T * K + 1, 0);
+  L.gptr.assign((size_t)T * K + 1, 0);
+  L.nb_ptr.assign((size_t)T * K + 1, 0);
+  L.erow_ptr.assign(T + 1, 0);
+  std::vector<int> lr_of(n, -1);  // device row -> local row of the current tile
+  std::vector<int> rows;
+  std::vector<std::vector<int>> gh(K);  // ghost cells of the current tile by colour: (lr, x, src)
+  std::vector<int> nbmark(T, -1);
+  for (int t = 0; t < T; ++t) {
+    // local rows: own rows, then ghost rows in Morton order
+    rows.clear();
+    for (int r = L.tile_row0[t]; r < L.tile_row0[t + 1]; ++r) rows.push_back(r);
+    const size_t n_own = rows.size();
+    for (int r = L.tile_row0[t]; r < L.tile_row0[t + 1]; ++r) {
+      const int i = perm[r];
+      for (long long p = cptr[i]; p < cptr[i + 1]; ++p) {
+        const int k = crow[p];
+        if (tile_of[k] != t) rows.push_back(L.rpos[k]);
+      }
+    }
+    std::sort(rows.begin() + n_own, rows.end());
+    rows.erase(std::unique(rows.begin() + n_own, rows.end()), rows.end());
+    if (rows.size() > kTilePadRow) { err = "tile layout: too many local rows in a tile"; return false; }
+    L.max_rows = std::max(L.max_rows, (int)rows.size());
+    for (size_t q = 0; q < rows.size(); ++q) lr_of[rows[q]] = (int)q;
+    L.erow.insert(L.erow.end(), rows.begin(), rows.end());
+    L.erow_ptr[t + 1] = (int)L.erow.size();
+    // own batches, colour by colour
+    for (int c = 0; c < K; ++c) {
+      const size_t pc = (size_t)t * K + c;
+      int x = tc_ptr[pc];
+      const int xe = tc_ptr[pc + 1];
+      while (x < xe) {
+        int cells = 0, ns = 0;
+        while (x + ns < xe && ns < std::min(NT, kTileSlotsMax)) {
+          const int len = (int)(cptr[L.compact_loc[x + ns] + 1] - cptr[L.compact_loc[x + ns]]);
+          if (cells + len > NT * RMAX) break;
+          cells += len;
+          ++ns;
+        }
+        const int R = std::max(1, (cells + NT - 1) / NT);
+        TileBatch tb{(int)L.cell_pk.size(), R, ns, x};
+        if ((long long)L.cell_pk.size() + (long long)R * NT > INT32_MAX) { err = "tile layout: too many cells"; return false; }
+        L.cell_pk.resize(L.cell_pk.size() + (size_t)R * NT, kTilePadRow);
+        L.cell_src.resize(L.cell_pk.size(), -1);
+        int f = 0;
+        for (int q = 0; q < ns; ++q) {
+          const int i = L.compact_loc[x + q];
+          L.slot_f0[x + q] = (L.slot_f0[x + q] & kSlotExported) | f;
+          const long long p0 = cptr[i], p1 = cptr[i + 1];
+          for (long long p = p0; p < p1; ++p, ++f) {
+            const int k = crow[p];
+            uint32_t pk = (uint32_t)lr_of[L.rpos[k]] | ((uint32_t)q << kTileQShift);
+            if (p == p0) pk |= kCellStart;
+            if (p == p1 - 1) pk |= kCellEnd;
+            const size_t e = (size_t)tb.off + (size_t)(f % R) * NT + f / R;
+            L.cell_pk[e] = pk;
+            L.cell_src[e] = L.rpos[k] * b + cu[p];
+          }
+        }
+        L.batch.push_back(tb);
+        x += ns;
+      }
+      L.batch_ptr[pc + 1] = (int)L.batch.size();
+    }
+    // ghost cells: foreign members j of the tile's rows, by colour of j
+    for (auto& g : gh) g.clear();
+    for (size_t q = 0; q < rows.size(); ++q) {
+      const int k = perm[rows[q]];
+      for (int u = 0; u < b; ++u) {
+        const int j = nn[(size_t)k * b + u];
+        if (j < 0 || tile_of[j] == t) continue;
+        auto& g = gh[colors[j] - 1];
+        g.push_back((int)q);
+        g.push_back(slot_of[j]);
+        g.push_back(L.rpos[k] * b + u);
+        L.slot_f0[slot_of[j]] |= kSlotExported;
+      }
+    }
+    for (int c = 0; c < K; ++c) {
+      const size_t pc = (size_t)t * K + c;
+      for (size_t g = 0; g < gh[c].size(); g += 3) {
+        L.gcell.push_back(gh[c][g]);
+        L.gcell.push_back(gh[c][g + 1]);
+        L.gsrc.push_back(gh[c][g + 2]);
+        const int u = tile_of[L.compact_loc[gh[c][g + 1]]];
+        if (nbmark[u] != (int)pc) { nbmark[u] = (int)pc; L.nb.push_back(u); }
+      }
+      L.gptr[pc + 1] = (int)L.gsrc.size();
+      L.nb_ptr[pc + 1] = (int)L.nb.size();
+    }
+    for (int r : rows) lr_of[r] = -1;
+  }
+  return true;
+}
+
 void dag_levels(const int* nn, int n, int b, std::vector<int>& level_ptr, std::vector<int>& level_rows) {
   std::vector<int> lev(n, 0);
   int maxl = 0;

@@ -72,6 +72,62 @@ bool build_sweep_layout(const int* nn_rowmajor, int n, int b, const int* colors,
                         const double* locs_colmajor, int d, int lanes_per_chain, SweepLayout& L,
                         std::string& err);
 
+
+// Device layout of the tile-resident chromatic sweep (one persistent launch
+// per call; DESIGN.md "Tile-resident sweep").
+//  - tiles: T contiguous ranges of the Morton order (device rows), balanced
+//    by column work; tile t owns the locations / rows of its range;
+//  - local rows of tile t (E_t): every row of B with a member in t -- its own
+//    rows first (local row = Morton rank - tile start), then the foreign
+//    ("ghost") rows in Morton order; r of these rows lives in the tile's LDS
+//    for the whole call;
+//  - compact (slot) order: tile-major, then colour, then Morton;
+//  - own batches of (tile, colour): runs of <= 256 whole slots and <= NT*RMAX
+//    cells (the slots' columns of B, concatenated in stream order f); cell f of
+//    a batch with R = ceil(cells/NT) rows sits at entry off + (f % R)*NT + f / R
+//    (thread f / R, register f % R: coalesced loads, contiguous runs per
+//    thread).  cell_pk = local row | q << 17 | start << 30 | end << 31
+//    (q = slot inside the batch; start/end: first/last cell of a slot);
+//    padding cells carry local row kTilePadRow and no flags;
+//  - ghost cells of (tile, colour): (local row k, slot x of a foreign member j
+//    of colour c): r_k += B[k,j] dw_j once j's owner has published dw_j;
+//  - neighbours of (tile, colour): the owner tiles of those ghost slots.
+constexpr int kTileRowBits = 17;
+constexpr uint32_t kTilePadRow = (1u << kTileRowBits) - 1;
+constexpr int kTileQShift = 17;
+constexpr uint32_t kTileQMask = 0x7FF;  // q < 2048
+constexpr uint32_t kCellStart = 1u << 30;
+constexpr uint32_t kCellEnd = 1u << 31;
+constexpr int kSlotExported = 1 << 30;  // slot_f0 flag: dw of the slot is read by other tiles
+constexpr int kTileSlotsMax = 256;      // slots per own batch
+
+struct TileBatch { int off, R, nslots, slot0; };
+
+struct TileLayout {
+  int n = 0, b = 0, K = 0, T = 0, NT = 0, RMAX = 0;
+  long long nnz = 0;
+  int max_rows = 0;                  // max |E_t|
+  int max_collen = 0;
+  std::vector<int> rpos;             // n: loc -> device row (Morton rank)
+  std::vector<int> compact_loc;      // n: slot -> loc
+  std::vector<int> slot_f0;          // n: first stream cell inside its batch | kSlotExported
+  std::vector<int> tile_row0;        // T+1: device rows owned by each tile
+  std::vector<int> erow_ptr, erow;   // local rows of each tile -> device row
+  std::vector<TileBatch> batch;      // own batches, grouped by (tile, colour)
+  std::vector<int> batch_ptr;        // T*K + 1
+  std::vector<uint32_t> cell_pk;     // own cells (padded batches)
+  std::vector<int> cell_src;         // device Linv index rpos[k]*b + j, or -1 (padding)
+  std::vector<int> gcell;            // 2 per ghost cell: local row, slot of the foreign member
+  std::vector<int> gsrc;             // device Linv index of each ghost cell
+  std::vector<int> gptr;             // T*K + 1
+  std::vector<int> nb_ptr, nb;       // T*K + 1, neighbour tiles of each (tile, colour)
+};
+
+// Fails (returns false, err set) when the layout does not fit the packed
+// formats; the caller checks the LDS budget (max_rows).
+bool build_tile_layout(const int* nn_rowmajor, int n, int b, const int* colors, const double* locs_colmajor,
+                       int d, int T, int NT, int RMAX, TileLayout& L, std::string& err);
+
 // Level sets of the Vecchia DAG for the sparse triangular solve:
 // level(i) = 1 + max level(NN(i)), level 0 rows have no neighbours.
 void dag_levels(const int* nn_rowmajor, int n, int b, std::vector<int>& level_ptr,

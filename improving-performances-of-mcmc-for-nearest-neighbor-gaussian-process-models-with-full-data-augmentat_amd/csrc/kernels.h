@@ -106,6 +106,48 @@ hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, const ColorLaun
 hipError_t launch_normals_compact(hipStream_t st, const SweepDev& L, int chain_mask, int sweep_off, int n,
                                   double* z);
 
+// ---- tile-resident sweep (graph_prep.h TileLayout): one persistent launch
+// runs every sweep of a call; r of each tile's local rows stays in its LDS;
+// colour c's dw of exported slots is handed to the neighbour tiles through
+// dwx (sc1 stores / loads) behind a per-tile progress flag.
+struct TileDev {
+  const int4* batch;          // own batches {off, R, nslots, slot0}
+  const int* batch_ptr;       // T*K+1
+  const uint32_t* cell_pk;    // n_cells
+  const double* cell_val;     // C x n_cells
+  long long n_cells;
+  const int2* gcell;          // n_gcells: {local row, slot}
+  const double* gval;         // C x n_gcells
+  long long n_gcells;
+  const int* gptr;            // T*K+1
+  const int* nb_ptr;          // T*K+1
+  const int* nb;
+  const int* erow_ptr;        // T+1
+  const int* erow;            // local row -> device row
+  const int2* sinfo;          // per slot {obs_per_loc, f0 | exported}
+  const int* slot_loc;        // per slot: location (normals)
+  double2* dr;                // per slot x C {precision_diag, residuals_sum}
+  double* w_slot;             // per slot x C
+  double* dwx;                // per slot x C: 16-byte granules {dw, epoch, call id}
+  const double* r;            // device rows x C (r = B w at call start)
+  const SweepScalars* scal;   // C
+  unsigned* ctl;              // [0] call id (bumped on the device before every launch), [1] timeout word
+  unsigned long long* dbg;    // NNGP_PROBE=9: per-tile phase times (4 x u64), else null
+  int K, C, T, n;
+};
+
+struct TileLaunch {
+  int n_sweeps;
+  int chain_mask;
+  const double* z_in;         // injected normals, per sweep: slot x C (nullptr: Philox inline)
+};
+
+int tile_lds_bytes(int max_rows, int C, int NT);
+hipError_t launch_sweep_tiles(hipStream_t st, const TileDev& D, const TileLaunch& a, int max_rows, int NT);
+// chain `chain`: cell/ghost values from Linv (device order) and precision_diag
+hipError_t launch_tile_refresh(hipStream_t st, const TileDev& D, int nbatches, int NT, const int* cell_src,
+                               const int* gsrc, const double* linv, int chain);
+
 // obs reductions: mode 0 -> partial[0] += (y - f[loc] - mu + beta0)^2
 //                 mode 1 -> partial[0] += ((y-b)^2 - (y-a)^2) / (2 sd^2),
 //                           a = fnew[loc]+mu-beta0, b = f[loc]+mu-beta0

@@ -32,28 +32,56 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
   }
 }
 
-// N(0,1) pair for locations 2p, 2p+1 of global sweep `sweep`: one Philox
-// call, counter (p, sweep_lo, sweep_hi, 0x5EED), key = seed; Box-Muller on its
-// two 53-bit uniforms: r cos(theta) -> 2p, r sin(theta) -> 2p+1.
-__device__ __forceinline__ void normal_pair(uint64_t seed, uint64_t sweep, uint32_t p, double& z0, double& z1) {
-  uint32_t c[4] = {p, (uint32_t)sweep, (uint32_t)(sweep >> 32), 0x5EEDu};
+// Standard normal by inversion (R's own default, norm_rand INVERSION ->
+// qnorm): Wichura's AS241 (PPND16) at p in (0, 1).
+__device__ __forceinline__ double qnorm_as241(double p) {
+  const double q = p - 0.5;
+  double r, val;
+  if (fabs(q) <= 0.425) {
+    r = 0.180625 - q * q;
+    return q * (((((((r * 2509.0809287301226727 + 33430.575583588128105) * r + 67265.770927008700853) * r +
+                    45921.953931549871457) * r + 13731.693765509461125) * r + 1971.5909503065514427) * r +
+                  133.14166789178437745) * r + 3.387132872796366608) /
+           (((((((r * 5226.495278852545925 + 28729.085735721942674) * r + 39307.89580009271061) * r +
+                 21213.794301586595867) * r + 5394.1960214247511077) * r + 687.1870074920579083) * r +
+             42.313330701600911252) * r + 1.);
+  }
+  r = q < 0 ? p : 1.0 - p;
+  r = sqrt(-log(r));
+  if (r <= 5.) {
+    r -= 1.6;
+    val = (((((((r * 7.7454501427834140764e-4 + .0227238449892691845833) * r + .24178072517745061177) * r +
+               1.27045825245236838258) * r + 3.64784832476320460504) * r + 5.7694972214606914055) * r +
+             4.6303378461565452959) * r + 1.42343711074968357734) /
+          (((((((r * 1.05075007164441684324e-9 + 5.475938084995344946e-4) * r + .0151986665636164571966) * r +
+               .14810397642748007459) * r + .68976733498510000455) * r + 1.6763848301838038494) * r +
+             2.05319162663775882187) * r + 1.);
+  } else {
+    r -= 5.;
+    val = (((((((r * 2.01033439929228813265e-7 + 2.71155556874348757815e-5) * r + .0012426609473880784386) * r +
+               .026532189526576123093) * r + .29656057182850489123) * r + 1.7848265399172913358) * r +
+             5.4637849111641143699) * r + 6.6579046435011037772) /
+          (((((((r * 2.04426310338993978564e-15 + 1.4215117583164458887e-7) * r + 1.8463183175100546818e-5) * r +
+               7.868691311456132591e-4) * r + .0148753612908506148525) * r + .13692988092273580531) * r +
+             .59983220655588793769) * r + 1.);
+  }
+  return q < 0.0 ? -val : val;
+}
+
+// N(0,1) for location `loc` of global sweep `sweep`: one Philox4x32-10 call,
+// counter (loc, sweep_lo, sweep_hi, 0x5EED), key = seed; its first 53 bits
+// give u in (0,1); z = qnorm(u) (AS241).  Every location draws alone, so any
+// subset of locations (a colour class, a tile) generates exactly its own.
+__device__ __forceinline__ double normal_loc(uint64_t seed, uint64_t sweep, uint32_t loc) {
+  uint32_t c[4] = {loc, (uint32_t)sweep, (uint32_t)(sweep >> 32), 0x5EEDu};
   philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-  uint64_t a = ((((uint64_t)c[1]) << 32) | c[0]) >> 11;
-  uint64_t b = ((((uint64_t)c[3]) << 32) | c[2]) >> 11;
-  double u1 = ((double)a + 0.5) * 0x1.0p-53;
-  double u2 = (double)b * 0x1.0p-53;
-  const double r = sqrt(-2.0 * log(u1)), th = 6.283185307179586476925286766559 * u2;
-  z0 = r * cos(th);
-  z1 = r * sin(th);
+  const uint64_t a = ((((uint64_t)c[1]) << 32) | c[0]) >> 11;
+  return qnorm_as241(((double)a + 0.5) * 0x1.0p-53);
 }
 
 __global__ void normals_kernel(uint64_t seed, uint64_t sweep, int n, double* z) {
-  int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (2 * p >= n) return;
-  double z0, z1;
-  normal_pair(seed, sweep, (uint32_t)p, z0, z1);
-  z[2 * p] = z0;
-  if (2 * p + 1 < n) z[2 * p + 1] = z1;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) z[i] = normal_loc(seed, sweep, (uint32_t)i);
 }
 
 // ------------------------------------------------------------------ Bessel K
@@ -749,10 +777,12 @@ __device__ __forceinline__ void gen_normals(int item, const int* __restrict__ pa
   const int chain = item % C;
   if (!((chain_mask >> chain) & 1)) return;
   const int p = pairs ? pairs[item / C] : item / C;
-  double z0, z1;
-  normal_pair(scal[chain].seed, scal[chain].counter_base + sweep_off, (uint32_t)p, z0, z1);
-  __builtin_nontemporal_store(z0, z + (size_t)loc_rank[2 * p] * C + chain);
-  if (2 * p + 1 < n) __builtin_nontemporal_store(z1, z + (size_t)loc_rank[2 * p + 1] * C + chain);
+  const uint64_t sw = scal[chain].counter_base + sweep_off;
+  __builtin_nontemporal_store(normal_loc(scal[chain].seed, sw, (uint32_t)(2 * p)),
+                              z + (size_t)loc_rank[2 * p] * C + chain);
+  if (2 * p + 1 < n)
+    __builtin_nontemporal_store(normal_loc(scal[chain].seed, sw, (uint32_t)(2 * p + 1)),
+                                z + (size_t)loc_rank[2 * p + 1] * C + chain);
 }
 
 __global__ __launch_bounds__(256) void normals_compact_kernel(SweepDev L, int chain_mask, int sweep_off,
@@ -979,6 +1009,471 @@ hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, const ColorLaun
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ A1 (tiles)
+// Tile-resident chromatic sweep: ONE persistent launch per call runs every
+// sweep; workgroup t owns tile t (graph_prep.h TileLayout).  r of the tile's
+// local rows (its own rows plus the foreign rows its columns touch) lives in
+// LDS for the whole call, so the per-colour r traffic of the colour-launch
+// engine (every launch re-reads / writes back almost every line of r) is gone;
+// HBM carries only the B values, the per-slot records and the halo dw.
+// Per colour c (epoch = sweep*K + c + 1):
+//  1. own batches: cells (coalesced, non-temporal; the colour's first batch
+//     was prefetched during the previous colour's hand-off) -> products
+//     B[k,i] r_k with r_k from LDS -> running sums along each thread's
+//     contiguous cells (restart at slot starts) -> per-thread tails in LDS ->
+//     the thread holding a slot's last cell adds the tails of the threads the
+//     slot spans (thread order: deterministic) -> the slot's thread draws w_i'
+//     -> dw_i in LDS, and for a slot other tiles read, one 16-byte write-through
+//     granule {dw_i, tag} (tag = call id << 32 | epoch) -> every cell scatters
+//     r_k += B[k,i] dw_i in LDS (the rows of one colour are distinct);
+//  2. the next colour's first batch is prefetched;
+//  3. ghosts: every ghost cell (local row k, foreign slot j of colour c) reads
+//     j's granule (sc1) until its tag is this call's epoch, then adds B[k,j]
+//     dw_j to its local row.  The data is its own flag (MI355X_MICROARCH
+//     "R2" granules): no drain, no flag store, no barrier before the read.
+// Each row of B has at most one member of colour c, so steps 1 and 3 never
+// update a row twice within a colour.  j's granule is rewritten one sweep
+// later, after its owner has read granules of every tile reading j (they
+// share the row, so each is the other's neighbour at its own colour), so no
+// reader sees a later value; the call id (bumped on the device before every
+// launch) keeps granules of earlier calls from matching.  Spins are bounded: a
+// timeout sets ctl[1] and the launch drains (the host reports an error).
+constexpr uint32_t kTPad = (1u << 17) - 1;
+constexpr uint32_t kTStart = 1u << 30, kTEnd = 1u << 31;
+constexpr int kTExported = 1 << 30;
+constexpr int kTSlots = 256;       // slots per own batch (graph_prep.h kTileSlotsMax)
+constexpr int kTSpreadLds = 82 * 1024;  // LDS floor: at most one tile per CU
+
+int tile_lds_bytes(int max_rows, int C, int NT) {
+  const int rbytes = ((max_rows * C * 8 + 15) / 16) * 16;
+  return rbytes + kTSlots * C * 8 + (NT / 64) * (C * 8 + 4) + 16;
+}
+
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+__global__ void tile_call_bump_kernel(unsigned* ctl) {
+  ctl[0] += 1u;  // call id (never 0 inside a launch)
+  ctl[1] = 0u;   // timeout word
+}
+
+// registers of one own batch: this thread's cells (f = t*R + j) and its draw
+// items u = t + k*NT < nslots*C (slot q = u / C, chain u % C: per-slot
+// records of consecutive items are consecutive, the loads coalesce), and,
+// once tile_prep_items has run, each item's draw scalars
+template <int C, int NT, int RMAX>
+struct TileBatchRegs {
+  static constexpr int IMAX = (kTSlots * C + NT - 1) / NT;
+  int R, ns, x0;
+  uint32_t pk[RMAX];
+  double v[RMAX][C];
+  int2 si[IMAX];
+  int loc[IMAX];
+  double2 dr[IMAX];
+  double w[IMAX];
+  double cR[IMAX], invP[IMAX], zs[IMAX], is2[IMAX];
+};
+
+template <int C, int NT, int RMAX>
+__device__ __forceinline__ void tile_load_batch(const TileDev& D, int bi, TileBatchRegs<C, NT, RMAX>& b, int t) {
+  const int4 B = D.batch[bi];
+  b.R = B.y; b.ns = B.z; b.x0 = B.w;
+#pragma unroll
+  for (int j = 0; j < RMAX; ++j) {
+    if (j < b.R) {
+      const long long e = B.x + (long long)j * NT + t;
+      b.pk[j] = __builtin_nontemporal_load(D.cell_pk + e);
+#pragma unroll
+      for (int ch = 0; ch < C; ++ch) b.v[j][ch] = __builtin_nontemporal_load(D.cell_val + ch * D.n_cells + e);
+    } else {
+      b.pk[j] = kTPad;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < TileBatchRegs<C, NT, RMAX>::IMAX; ++k) {
+    const int u = t + k * NT;
+    if (u < b.ns * C) {
+      const int q = u / C;
+      const size_t xu = (size_t)b.x0 * C + u;  // = (x0 + q) * C + chain
+      b.si[k] = D.sinfo[b.x0 + q];
+      b.loc[k] = D.slot_loc[b.x0 + q];
+      b.dr[k] = D.dr[xu];
+      b.w[k] = D.w_slot[xu];
+    }
+  }
+}
+
+// everything of the Gibbs draw but acc: P = D/s2 + n/t2, w' = (cR - acc/s2)/P
+// + z/sqrt(P) with cR = R/t2 + D w/s2 (w of an own slot is constant until its
+// colour, so this runs a colour ahead, during the previous hand-off)
+template <int C, int NT, int RMAX>
+__device__ __forceinline__ void tile_prep_items(const TileDev& D, const TileLaunch& a, int s, TileBatchRegs<C, NT, RMAX>& b,
+                                                int t) {
+#pragma unroll
+  for (int k = 0; k < TileBatchRegs<C, NT, RMAX>::IMAX; ++k) {
+    const int u = t + k * NT;
+    if (u < b.ns * C) {
+      const int q = u / C, ch = u - q * C;
+      const SweepScalars& sc = D.scal[ch];
+      const double inv_s2 = sc.inv_s2, inv_t2 = sc.inv_t2;
+      const double z = a.z_in ? a.z_in[((size_t)s * D.n + b.x0 + q) * C + ch]
+                              : normal_loc(sc.seed, sc.counter_base + s, (uint32_t)b.loc[k]);
+      const double P = b.dr[k].x * inv_s2 + (double)b.si[k].x * inv_t2;
+      b.invP[k] = 1.0 / P;
+      b.zs[k] = z / sqrt(P);
+      b.cR[k] = inv_t2 * b.dr[k].y + inv_s2 * (b.dr[k].x * b.w[k]);
+      b.is2[k] = inv_s2;
+    }
+  }
+}
+
+// ghost cells of one chunk: local row, foreign slot, B values, received dw
+template <int C, int GMAX>
+struct TileGhostRegs {
+  int lr[GMAX], gx[GMAX];
+  double gv[GMAX][C];
+};
+
+template <int C, int NT, int GMAX>
+__device__ __forceinline__ void tile_load_ghosts(const TileDev& D, int gb, int g1, TileGhostRegs<C, GMAX>& g, int t) {
+#pragma unroll
+  for (int k = 0; k < GMAX; ++k) {
+    const int e = gb + k * NT + t;
+    g.lr[k] = -1;
+    if (e < g1) {
+      const long long raw = __builtin_nontemporal_load(reinterpret_cast<const long long*>(D.gcell) + e);
+      g.lr[k] = (int)(raw & 0xFFFFFFFFll);
+      g.gx[k] = (int)(raw >> 32);
+#pragma unroll
+      for (int ch = 0; ch < C; ++ch) g.gv[k][ch] = __builtin_nontemporal_load(D.gval + ch * D.n_gcells + e);
+    }
+  }
+}
+
+template <int C, int NT, int RMAX, int GMAX, int PROBE>
+__global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D, TileLaunch a) {
+  using BR = TileBatchRegs<C, NT, RMAX>;
+  using GR = TileGhostRegs<C, GMAX>;
+  constexpr int IMAX = BR::IMAX;
+  constexpr int NW = NT / 64;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int T = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int row0 = D.erow_ptr[T], nrows = D.erow_ptr[T + 1] - row0;
+  double* r_s = smem;
+  double* acc_s = smem + ((nrows * C + 1) / 2) * 2;   // kTSlots x C: slot totals, then dw
+  double* wsum = acc_s + kTSlots * C;                  // NW x C: segmented wave totals
+  int* wflag = reinterpret_cast<int*>(wsum + NW * C);  // NW: the wave holds a slot start
+  unsigned long long tp[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_prev = 0;
+#define TSTAMP(k)                                                       \
+  do {                                                                  \
+    if (PROBE) {                                                        \
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");       \
+      const unsigned long long now_ = __builtin_amdgcn_s_memrealtime(); \
+      if ((k) >= 0) tp[(k) < 0 ? 0 : (k)] += now_ - t_prev;             \
+      t_prev = now_;                                                    \
+    }                                                                   \
+  } while (0)
+  TSTAMP(-1);
+  for (int lr = t; lr < nrows; lr += NT) {
+    const size_t g = (size_t)D.erow[row0 + lr] * C;
+#pragma unroll
+    for (int ch = 0; ch < C; ++ch) r_s[lr * C + ch] = D.r[g + ch];
+  }
+  const unsigned call = D.ctl[0];
+  unsigned* tmo = D.ctl + 1;
+  const __amdgpu_buffer_rsrc_t gran = __builtin_amdgcn_make_buffer_rsrc(D.dwx, 0, 0x7FFFFFFF, 0x00020000);
+  BR nb;  // the next colour's first batch, loaded and prepared a colour ahead
+  const int K = D.K;
+  if (D.batch_ptr[T * K] < D.batch_ptr[T * K + 1]) {
+    tile_load_batch<C, NT, RMAX>(D, D.batch_ptr[T * K], nb, t);
+    tile_prep_items<C, NT, RMAX>(D, a, 0, nb, t);
+  }
+  __syncthreads();
+  TSTAMP(7);
+  unsigned epoch = 0;
+  bool timed_out = false;
+  for (int s = 0; s < a.n_sweeps; ++s) {
+    for (int c = 0; c < K; ++c) {
+      ++epoch;
+      const int pc = T * K + c;
+      // ---- 1. own batches
+      const int bfirst = D.batch_ptr[pc], bend = D.batch_ptr[pc + 1];
+      for (int bi = bfirst; bi < bend; ++bi) {
+        BR& b = nb;  // the prefetched first batch; further batches load in place
+        if (bi != bfirst) {
+          tile_load_batch<C, NT, RMAX>(D, bi, b, t);
+          tile_prep_items<C, NT, RMAX>(D, a, s, b, t);
+        }
+        const int R = b.R, nit = b.ns * C;
+        // products, running sums restarted at slot starts.  A slot that
+        // began in this thread is complete at its last cell (-> acc_s); the
+        // thread's first cells may continue a slot of earlier threads: its
+        // end (if here) waits for the carry of those threads.
+        double run[C], cont[C];
+        int cont_q = -1;
+        bool seen_start = false;
+#pragma unroll
+        for (int ch = 0; ch < C; ++ch) { run[ch] = 0.0; cont[ch] = 0.0; }
+#pragma unroll
+        for (int j = 0; j < RMAX; ++j) {
+          if (j < R) {
+            const uint32_t lr = b.pk[j] & kTPad;
+            const bool st = (b.pk[j] & kTStart) != 0;
+#pragma unroll
+            for (int ch = 0; ch < C; ++ch) {
+              const double p = (lr != kTPad) ? b.v[j][ch] * r_s[lr * C + ch] : 0.0;
+              run[ch] = st ? p : run[ch] + p;
+            }
+            seen_start |= st;
+            if (b.pk[j] & kTEnd) {
+              const int q = (int)((b.pk[j] >> 17) & 0x7FF);
+              if (seen_start) {
+#pragma unroll
+                for (int ch = 0; ch < C; ++ch) acc_s[q * C + ch] = run[ch];
+              } else {
+                cont_q = q;
+#pragma unroll
+                for (int ch = 0; ch < C; ++ch) cont[ch] = run[ch];
+              }
+            }
+          }
+        }
+        TSTAMP(1);
+        // segmented inclusive scan of the thread tails (restart at threads
+        // holding a slot start): in the wave by shuffles, across waves
+        // through LDS
+        double v[C];
+        int f = seen_start ? 1 : 0;
+#pragma unroll
+        for (int ch = 0; ch < C; ++ch) v[ch] = run[ch];
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          double vu[C];
+#pragma unroll
+          for (int ch = 0; ch < C; ++ch) vu[ch] = __shfl_up(v[ch], d, 64);
+          const int fu = __shfl_up(f, d, 64);
+          if (lane >= d) {
+            if (!f) {
+#pragma unroll
+              for (int ch = 0; ch < C; ++ch) v[ch] = vu[ch] + v[ch];
+            }
+            f |= fu;
+          }
+        }
+        if (lane == 63) {
+#pragma unroll
+          for (int ch = 0; ch < C; ++ch) wsum[wv * C + ch] = v[ch];
+          wflag[wv] = f;
+        }
+        __syncthreads();
+        double in[C];
+#pragma unroll
+        for (int ch = 0; ch < C; ++ch) in[ch] = 0.0;
+        for (int p = wv - 1; p >= 0; --p) {
+#pragma unroll
+          for (int ch = 0; ch < C; ++ch) in[ch] = wsum[p * C + ch] + in[ch];
+          if (wflag[p]) break;
+        }
+        double cp[C];
+#pragma unroll
+        for (int ch = 0; ch < C; ++ch) {
+          const double S = f ? v[ch] : v[ch] + in[ch];
+          const double up = __shfl_up(S, 1, 64);
+          cp[ch] = lane ? up : in[ch];
+        }
+        if (cont_q >= 0) {
+#pragma unroll
+          for (int ch = 0; ch < C; ++ch) acc_s[cont_q * C + ch] = cont[ch] + cp[ch];
+        }
+        __syncthreads();
+        TSTAMP(2);
+#pragma unroll
+        for (int k = 0; k < IMAX; ++k) {
+          const int u = t + k * NT;
+          if (u < nit) {
+            const int ch = u % C;
+            double dw = 0.0;
+            const size_t xu = (size_t)b.x0 * C + u;
+            if ((a.chain_mask >> ch) & 1) {
+              const double wn = (b.cR[k] - b.is2[k] * acc_s[u]) * b.invP[k] + b.zs[k];
+              dw = wn - b.w[k];
+              D.w_slot[xu] = wn;
+            }
+            acc_s[u] = dw;
+            if (b.si[k].y & kTExported) {
+              const unsigned long long uu = __builtin_bit_cast(unsigned long long, dw);
+              u32x4_t g;
+              g.x = (unsigned)uu; g.y = (unsigned)(uu >> 32); g.z = epoch; g.w = call;
+              __builtin_amdgcn_raw_buffer_store_b128(g, gran, (int)(xu * 16), 0, 16);
+            }
+          }
+        }
+        __syncthreads();
+        TSTAMP(3);
+#pragma unroll
+        for (int j = 0; j < RMAX; ++j) {
+          if (j < R) {
+            const uint32_t lr = b.pk[j] & kTPad;
+            if (lr != kTPad) {
+              const int q = (int)((b.pk[j] >> 17) & 0x7FF);
+#pragma unroll
+              for (int ch = 0; ch < C; ++ch) r_s[lr * C + ch] += b.v[j][ch] * acc_s[q * C + ch];
+            }
+          }
+        }
+        TSTAMP(4);
+      }
+      // ---- 2. next colour's first batch: loads, then (while neighbours
+      // publish colour c) its draw scalars; this colour's ghost cells load
+      const int g0 = D.gptr[pc], g1 = D.gptr[pc + 1];
+      GR gr;
+      {
+        const int cn = c + 1 < K ? c + 1 : 0;
+        const int sn = c + 1 < K ? s : s + 1;
+        const int pn = T * K + cn;
+        const bool more = sn < a.n_sweeps && D.batch_ptr[pn] < D.batch_ptr[pn + 1];
+        if (more) tile_load_batch<C, NT, RMAX>(D, D.batch_ptr[pn], nb, t);
+        if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
+        if (more) tile_prep_items<C, NT, RMAX>(D, a, sn, nb, t);
+      }
+      TSTAMP(5);
+      // ---- 3. ghosts: poll each granule until it carries this epoch
+      for (int gb = g0; gb < g1; gb += NT * GMAX) {
+        if (gb != g0) tile_load_ghosts<C, NT, GMAX>(D, gb, g1, gr, t);
+        double dw[GMAX][C];
+        unsigned pend = 0;
+#pragma unroll
+        for (int k = 0; k < GMAX; ++k)
+          if (gr.lr[k] >= 0) pend |= ((1u << C) - 1) << (k * C);
+        for (unsigned spins = 0; pend; ++spins) {
+#pragma unroll
+          for (int k = 0; k < GMAX; ++k)
+#pragma unroll
+            for (int ch = 0; ch < C; ++ch) {
+              const unsigned bit = 1u << (k * C + ch);
+              if (pend & bit) {
+                const u32x4_t g = __builtin_amdgcn_raw_buffer_load_b128(gran, (int)(((size_t)gr.gx[k] * C + ch) * 16), 0, 16);
+                if (g.z == epoch && g.w == call) {
+                  dw[k][ch] = __builtin_bit_cast(double, (unsigned long long)g.x | ((unsigned long long)g.y << 32));
+                  pend &= ~bit;
+                }
+              }
+            }
+          if (!pend) break;
+          if (timed_out || spins > (1u << 20)) {
+            if (!timed_out) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            timed_out = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+#pragma unroll
+        for (int k = 0; k < GMAX; ++k)
+          if (gr.lr[k] >= 0 && !timed_out)
+#pragma unroll
+            for (int ch = 0; ch < C; ++ch) r_s[gr.lr[k] * C + ch] += gr.gv[k][ch] * dw[k][ch];
+      }
+      __syncthreads();
+      TSTAMP(6);
+    }
+  }
+  if (PROBE && t == 0) {
+    unsigned long long* o = D.dbg + (size_t)T * 8;
+    for (int k = 0; k < 8; ++k) o[k] = tp[k];
+  }
+#undef TSTAMP
+}
+
+template <int C, int NT, int PROBE>
+static hipError_t launch_tiles_c(hipStream_t st, const TileDev& D, const TileLaunch& a, int lds) {
+  constexpr int RMAX = 4096 / NT;
+  auto k = sweep_tiles_kernel<C, NT, RMAX, (1024 / NT > 0 ? 1024 / NT : 1), PROBE>;
+  lds = lds < kTSpreadLds ? kTSpreadLds : lds;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(tile_call_bump_kernel, dim3(1), dim3(1), 0, st, D.ctl);
+  hipLaunchKernelGGL(k, dim3(D.T), dim3(NT), lds, st, D, a);
+  return hipGetLastError();
+}
+
+template <int NT>
+static hipError_t launch_tiles_nt(hipStream_t st, const TileDev& D, const TileLaunch& a, int lds) {
+  if (D.dbg) {
+    switch (D.C) {
+      case 1: return launch_tiles_c<1, NT, 1>(st, D, a, lds);
+      case 3: return launch_tiles_c<3, NT, 1>(st, D, a, lds);
+      default: break;
+    }
+  }
+  switch (D.C) {
+    case 1: return launch_tiles_c<1, NT, 0>(st, D, a, lds);
+    case 2: return launch_tiles_c<2, NT, 0>(st, D, a, lds);
+    case 3: return launch_tiles_c<3, NT, 0>(st, D, a, lds);
+    case 4: return launch_tiles_c<4, NT, 0>(st, D, a, lds);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_sweep_tiles(hipStream_t st, const TileDev& D, const TileLaunch& a, int max_rows, int NT) {
+  const int lds = tile_lds_bytes(max_rows, D.C, NT);
+  switch (NT) {
+    case 256: return launch_tiles_nt<256>(st, D, a, lds);
+    case 512: return launch_tiles_nt<512>(st, D, a, lds);
+    case 1024: return launch_tiles_nt<1024>(st, D, a, lds);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// B values of chain `chain` into the tile layout + precision_diag (column
+// sums of squares in stream = row order, as sell_refresh); workgroups
+// [0, nbatches) take one own batch each (NT = the layout's threads per tile,
+// cell f of the batch at off + (f % R)*NT + f / R), the rest copy ghost values
+__global__ __launch_bounds__(256) void tile_refresh_kernel(TileDev D, int nbatches, int NT,
+                                                           const int* __restrict__ cell_src,
+                                                           const int* __restrict__ gsrc,
+                                                           const double* __restrict__ linv, int chain) {
+  __shared__ double sq[4096];
+  __shared__ unsigned char endf[4096];
+  const int t = threadIdx.x;
+  if ((int)blockIdx.x >= nbatches) {
+    double* gv = const_cast<double*>(D.gval) + (size_t)chain * D.n_gcells;
+    for (long long g = (long long)(blockIdx.x - nbatches) * 256 + t; g < D.n_gcells;
+         g += (long long)(gridDim.x - nbatches) * 256)
+      gv[g] = linv[gsrc[g]];
+    return;
+  }
+  const int4 B = D.batch[blockIdx.x];
+  double* cv = const_cast<double*>(D.cell_val) + (size_t)chain * D.n_cells;
+  for (int e0 = t; e0 < B.y * NT; e0 += 256) {
+    const long long e = B.x + e0;
+    const int src = cell_src[e];
+    const double v = src >= 0 ? linv[src] : 0.0;
+    cv[e] = v;
+    const int f = (e0 % NT) * B.y + e0 / NT;  // e0 = j*NT + thread
+    sq[f] = v * v;
+    endf[f] = (D.cell_pk[e] & kTEnd) ? 1 : 0;
+  }
+  __syncthreads();
+  if (t < B.z) {
+    const int x = B.w + t;
+    const int f0 = D.sinfo[x].y & 0xFFFFF;
+    double s = 0.0;
+    for (int f = f0;; ++f) {
+      s += sq[f];
+      if (endf[f]) break;
+    }
+    D.dr[(size_t)x * D.C + chain].x = s;
+  }
+}
+
+hipError_t launch_tile_refresh(hipStream_t st, const TileDev& D, int nbatches, int NT, const int* cell_src,
+                               const int* gsrc, const double* linv, int chain) {
+  const int gx = D.n_gcells > 0 ? 256 : 0;
+  if (nbatches + gx == 0) return hipSuccess;
+  hipLaunchKernelGGL(tile_refresh_kernel, dim3(nbatches + gx), dim3(256), 0, st, D, nbatches, NT, cell_src, gsrc,
+                     linv, chain);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ A8
 __global__ __launch_bounds__(256) void obs_reduce_kernel(int mode, int n_obs, const double* __restrict__ y,
                                                          const double* __restrict__ mu, double beta0,
@@ -1144,7 +1639,7 @@ hipError_t launch_spin(hipStream_t st, double seconds) {
 }
 
 hipError_t launch_normals(hipStream_t st, uint64_t seed, uint64_t sweep, int n, double* z) {
-  int g = ((n + 1) / 2 + kBlock - 1) / kBlock;
+  int g = (n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(normals_kernel, dim3(g), dim3(kBlock), 0, st, seed, sweep, n, z);
   return hipGetLastError();
 }

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define NNGP_ABI_VERSION 2
+#define NNGP_ABI_VERSION 3
 
 typedef enum {
   NNGP_OK = 0,
@@ -91,6 +91,10 @@ typedef struct {
   int n_chains;    /* chains held by the context */
   int lanes_per_chain; /* sweep lanes of one chain in a wavefront (64/32/16) */
   int n_chunks;    /* sweep chunks (wavefront tasks per chain and sweep) */
+  int sweep_engine;  /* 0: one launch per colour, 1: tile-resident persistent sweep */
+  int n_tiles;       /* tiles (persistent workgroups) of the tile engine */
+  int tile_rows_max; /* max local rows (own + foreign) of a tile: its LDS-resident r */
+  long long n_ghost_cells; /* foreign-member cells the tiles apply after a hand-off */
 } nngp_info;
 
 /* ---------- library ---------- */

@@ -63,21 +63,52 @@ void or_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out
   out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; out[3] = c[3];
 }
 
+/* Standard normal by inversion, Wichura's AS241 (PPND16) -- the algorithm of
+ * R's qnorm, which R's default norm_rand (INVERSION) applies to a uniform. */
+double or_qnorm(double p) {
+  double q = p - 0.5, r, val;
+  if (fabs(q) <= 0.425) {
+    r = 0.180625 - q * q;
+    return q * (((((((r * 2509.0809287301226727 + 33430.575583588128105) * r + 67265.770927008700853) * r +
+                    45921.953931549871457) * r + 13731.693765509461125) * r + 1971.5909503065514427) * r +
+                  133.14166789178437745) * r + 3.387132872796366608) /
+           (((((((r * 5226.495278852545925 + 28729.085735721942674) * r + 39307.89580009271061) * r +
+                 21213.794301586595867) * r + 5394.1960214247511077) * r + 687.1870074920579083) * r +
+             42.313330701600911252) * r + 1.);
+  }
+  r = q < 0 ? p : 1.0 - p;
+  r = sqrt(-log(r));
+  if (r <= 5.) {
+    r -= 1.6;
+    val = (((((((r * 7.7454501427834140764e-4 + .0227238449892691845833) * r + .24178072517745061177) * r +
+               1.27045825245236838258) * r + 3.64784832476320460504) * r + 5.7694972214606914055) * r +
+             4.6303378461565452959) * r + 1.42343711074968357734) /
+          (((((((r * 1.05075007164441684324e-9 + 5.475938084995344946e-4) * r + .0151986665636164571966) * r +
+               .14810397642748007459) * r + .68976733498510000455) * r + 1.6763848301838038494) * r +
+             2.05319162663775882187) * r + 1.);
+  } else {
+    r -= 5.;
+    val = (((((((r * 2.01033439929228813265e-7 + 2.71155556874348757815e-5) * r + .0012426609473880784386) * r +
+               .026532189526576123093) * r + .29656057182850489123) * r + 1.7848265399172913358) * r +
+             5.4637849111641143699) * r + 6.6579046435011037772) /
+          (((((((r * 2.04426310338993978564e-15 + 1.4215117583164458887e-7) * r + 1.8463183175100546818e-5) * r +
+               7.868691311456132591e-4) * r + .0148753612908506148525) * r + .13692988092273580531) * r +
+             .59983220655588793769) * r + 1.);
+  }
+  return q < 0.0 ? -val : val;
+}
+
 /* Standard normal for location `loc` (0-based) in global sweep `sweep` with
- * 64-bit `seed`: locations 2p and 2p+1 share one Philox call, counter =
- * (p, sweep_lo, sweep_hi, 0x5EEDu), key = seed; Box-Muller on its two 53-bit
- * uniforms gives r cos(theta) to the even and r sin(theta) to the odd one. */
+ * 64-bit `seed`: one Philox call per location, counter = (loc, sweep_lo,
+ * sweep_hi, 0x5EEDu), key = seed; its first 53 bits give u in (0,1) and the
+ * normal is qnorm(u). */
 double or_normal(uint64_t seed, uint64_t sweep, uint32_t loc) {
-  uint32_t ctr[4] = {loc >> 1, (uint32_t)sweep, (uint32_t)(sweep >> 32), 0x5EEDu};
+  uint32_t ctr[4] = {loc, (uint32_t)sweep, (uint32_t)(sweep >> 32), 0x5EEDu};
   uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
   uint32_t o[4];
   or_philox4x32_10(ctr, key, o);
   uint64_t a = (((uint64_t)o[1] << 32) | o[0]) >> 11;
-  uint64_t b = (((uint64_t)o[3] << 32) | o[2]) >> 11;
-  double u1 = ((double)a + 0.5) * 0x1.0p-53;   /* (0,1) */
-  double u2 = (double)b * 0x1.0p-53;           /* [0,1) */
-  double r = sqrt(-2.0 * log(u1)), th = 6.283185307179586476925286766559 * u2;
-  return (loc & 1u) ? r * sin(th) : r * cos(th);
+  return or_qnorm(((double)a + 0.5) * 0x1.0p-53);   /* u in (0,1) */
 }
 
 void or_normals(uint64_t seed, uint64_t sweep, int n, double *z) {

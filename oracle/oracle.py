@@ -47,6 +47,8 @@ def lib():
         L.or_normal.restype = C.c_double
         L.or_normal.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32]
         L.or_normals.argtypes = [C.c_uint64, C.c_uint64, C.c_int, dp]
+        L.or_qnorm.restype = C.c_double
+        L.or_qnorm.argtypes = [C.c_double]
         L.or_bessel_k.restype = C.c_double
         L.or_bessel_k.argtypes = [C.c_double, C.c_double]
         L.or_ncovparms.restype = C.c_int
@@ -99,6 +101,10 @@ def normals(seed: int, sweep: int, n: int) -> np.ndarray:
     z = np.zeros(n)
     lib().or_normals(seed, sweep, n, z)
     return z
+
+
+def qnorm(p: float) -> float:
+    return lib().or_qnorm(float(p))
 
 
 def sweep_normals(seed: int, counter_base: int, n_sweeps: int, n: int) -> np.ndarray:

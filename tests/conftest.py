@@ -74,3 +74,23 @@ def heavy():
             cols[c] = pd.Categorical.from_codes(d[f"fac_{c}"] - 1, categories=levels)
     return {"observed_locs": d["observed_locs"], "observed_field": d["observed_field"],
             "X_locs": pd.DataFrame(cols)}
+
+
+# Sweep engines of the device context (capi.hip): "colors" = one launch per
+# colour class; "tiles" = the tile-resident persistent sweep with many small
+# tiles (NNGP_TILES=24: every small test problem has halos, neighbour
+# hand-offs and several tiles per XCD; contexts whose 24-tile layout does not
+# fit a CU's LDS fall back to colour launches, as in production);
+# "tiles-default" = the production engine choice and tile count.  GPU test modules that exercise the sweep run under all three.
+ENGINES = {"colors": {"NNGP_ENGINE": "colors"},
+           "tiles": {"NNGP_TILES": "24"},  # automatic: colours where 24 tiles exceed the LDS
+           "tiles-default": {}}
+
+
+@pytest.fixture(params=list(ENGINES))
+def engine(request, monkeypatch):
+    monkeypatch.delenv("NNGP_TILES", raising=False)
+    monkeypatch.delenv("NNGP_ENGINE", raising=False)
+    for k, v in ENGINES[request.param].items():
+        monkeypatch.setenv(k, v)
+    return request.param

@@ -24,6 +24,7 @@ def _compare(res, ref, it, has_X):
     np.testing.assert_array_equal(res["acceptance"]["covariance_acceptance_sufficient"], ref["acceptance"]["sufficient"])
 
 
+@pytest.mark.usefixtures("engine")
 def test_update_iterations_match_oracle_no_X(P, O):
     import mcmc_oracle as MO
     from nngp_amd.update_gaussian import _philox_key, _run_chain
@@ -49,6 +50,7 @@ def test_update_iterations_match_oracle_no_X(P, O):
     _compare(res, ref, iters, False)
 
 
+@pytest.mark.usefixtures("engine")
 def test_update_iterations_match_oracle_vignette_X_locs(P, O, toy):
     """Vignette toy (n = 2000, m = 5, X_locs with 2 columns => interweaving)."""
     import mcmc_oracle as MO
@@ -68,6 +70,7 @@ def test_update_iterations_match_oracle_vignette_X_locs(P, O, toy):
         c.close()
 
 
+@pytest.mark.usefixtures("engine")
 def test_lockstep_batched_chains_equal_sequential_chains(P, toy):
     """mcmc_nngp_update_Gaussian drives the 3 chains of one context in
     lockstep with batched sweeps; every record equals the chains run one

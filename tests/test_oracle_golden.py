@@ -78,15 +78,25 @@ def test_oracle_normals_are_standard(O):
     assert kstest(z, "norm").pvalue > 1e-3
 
 
-def test_oracle_normal_pairs_independent(O):
-    """Locations 2p and 2p+1 share one Philox call (cos / sin of Box-Muller):
-    the two halves must be uncorrelated, also in their squares."""
+def test_oracle_normals_independent_and_local(O):
+    """One Philox call per location (counter = location, sweep): neighbouring
+    locations and consecutive sweeps are uncorrelated, also in their squares;
+    a location's normal does not depend on n."""
     z = O.normals(7, 3, 400_000)
     a, b = z[0::2], z[1::2]
     assert abs(np.corrcoef(a, b)[0, 1]) < 0.01
     assert abs(np.corrcoef(a * a, b * b)[0, 1]) < 0.01
-    # the pair of a location does not depend on n (counter = location >> 1)
+    z4 = O.normals(7, 4, 400_000)
+    assert abs(np.corrcoef(z, z4)[0, 1]) < 0.01
     np.testing.assert_array_equal(O.normals(7, 3, 11), z[:11])
+
+
+def test_oracle_qnorm_known_values(O):
+    """AS241 inversion against scipy's ndtri (published to ~1e-16)."""
+    from scipy.special import ndtri
+    p = np.concatenate([np.linspace(1e-12, 1 - 1e-12, 2001), [2.0 ** -54, 1e-300 + 2.0 ** -53, 0.5, 0.025, 0.975]])
+    got = np.array([O.qnorm(x) for x in p])
+    np.testing.assert_allclose(got, ndtri(p), rtol=1e-14, atol=1e-15)
 
 
 @pytest.mark.parametrize("nu", [0.3, 0.5, 0.77, 1.0, 1.5, 2.2, 3.7])
