@@ -166,18 +166,19 @@ def mcmc_iterations(P, wl, covfun, cp, ctx, iters, warmup, sync):
             "ms_per_iteration": el * 1e3 / iters, "field_thinning": 1.0}
 
 
-def pmc_traffic(chains, n, m):
+def pmc_traffic(chains, n, m, kernel):
     """Per-launch HBM bytes of the sweep kernel from the committed rocprofv3
     PMC summary of the same workload (profiles/, scripts/pmc.sh: FETCH_SIZE and
     WRITE_SIZE passes, calibrated on known-byte kernels)."""
     best = None
-    for f in sorted((ROOT / "profiles").glob("r*_pmc_sweep_c*.json")):
+    for f in sorted((ROOT / "profiles").glob("r*_pmc_*.json")):
         try:
             d = json.loads(f.read_text())
         except Exception:
             continue
         w = d.get("workload", {})
-        if w.get("chains") == chains and w.get("n") == n and w.get("m") == m and d.get("traffic_bytes_per_launch"):
+        if (w.get("chains") == chains and w.get("n") == n and w.get("m") == m and kernel.startswith(d.get("kernel", "?"))
+                and d.get("traffic_bytes_per_launch")):
             best = (d["traffic_bytes_per_launch"], f.name)
     return best
 
@@ -274,38 +275,48 @@ def main():
     info = ctx.info
     wl["field0"] = ctx.get_field()
     log(f"graph prep {wl['t_graph']:.1f}s colours={info['n_colors']} nnz={info['nnz']} "
-        f"entries={info['n_entries']} chunks={info['n_chunks']} lanes/chain={info['lanes_per_chain']} "
+        f"entries={info['n_entries']} engine={info['sweep_engine']} tiles={info['n_tiles']} chunks={info['n_chunks']} "
         f"max_collen={info['max_collen']}", rank)
     elapsed, ctr = timed(ctx, args.steps, args.warmup)
 
-    # per-kernel timing (HIP events around every colour launch, on the
-    # context's own stream) -> sweep kernel time per sweep
+    # per-kernel timing with HIP events on the context's own stream: the
+    # sweep kernel's launches alone (tile engine: one persistent launch per
+    # call of n_chromatic sweeps; colour engine: one launch per colour)
     n, nnz = args.n, info["nnz"]
+    engine = info["sweep_engine"]
     # SURVEY §8(d) algorithmic bytes: 12 nnz + 40 n per chain-sweep, the 4-byte
     # row index of an entry shared by the chains of a launch
     bytes_sweep = C * (8 * nnz + 40 * n) + 4 * nnz
     roofline = None
     if not args.no_kernel_timing:
-        ksw = max(4, min(20, args.steps))
+        ksw = nc if engine == 1 else max(4, min(20, args.steps))
+        reps = 5 if engine == 1 else 1
+        kms_all = []
         try:
-            ms_tot, kms = ctx.sweep_timed(ksw, [b0] * C, [ls] * C, [lnv] * C, seeds, [ctr] * C, per_kernel=True)
+            for r in range(reps):
+                _, kms = ctx.sweep_timed(ksw, [b0] * C, [ls] * C, [lnv] * C, seeds, [ctr + r * ksw] * C,
+                                         per_kernel=True)
+                kms_all.append(kms)
+            kms = float(np.median(kms_all))
         except Exception as e:  # report, do not hide the throughput line
             log(f"per-kernel timing failed: {e}", rank)
             kms = float("nan")
-        per_sweep_ms = kms / ksw
-        achieved = bytes_sweep / (per_sweep_ms * 1e-3) / 1e9
-        launches = ksw * info["n_colors"]
-        tr = pmc_traffic(C, n, args.m)
+        launches = 1 if engine == 1 else ksw * info["n_colors"]
+        bytes_launch = bytes_sweep * ksw / launches
+        achieved = bytes_launch / (kms * 1e-3 / launches) / 1e9
+        kname = "sweep_tiles_kernel" if engine == 1 else "sweep_color_kernel"
+        tr = pmc_traffic(C, n, args.m, kname)
         roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": achieved / HBM_PEAK_GBS,
                     "traffic": tr[0] / (kms * 1e-3 / launches) / 1e9 if tr else None,
                     "traffic_unit": "GB/s (PMC bytes per launch / measured launch time)",
                     "traffic_bytes_per_launch": tr[0] if tr else None,
                     "traffic_source": f"profiles/{tr[1]}" if tr else None,
-                    "kernel": "sweep_color_kernel", "kernel_avg_us": kms * 1e3 / launches,
+                    "kernel": kname, "kernel_avg_us": kms * 1e3 / launches,
                     "algorithmic_bytes_per_sweep": bytes_sweep,
-                    "algorithmic_bytes_per_launch": bytes_sweep / info["n_colors"],
-                    "launches_per_sweep": info["n_colors"]}
+                    "algorithmic_bytes_per_launch": bytes_launch,
+                    "sweeps_per_launch": ksw / launches,
+                    "launches_per_sweep": launches / ksw}
     mcmc = None
     if args.mcmc_iters > 0:
         sync = (lambda: torch.cuda.synchronize(local_rank)) if torch.cuda.is_available() else (lambda: None)
@@ -328,6 +339,9 @@ def main():
                                    f"{C} chains per GPU swept together (value = chain-sweeps/s)"),
                       "n": n, "m": args.m, "n_colors": info["n_colors"], "nnz": nnz, "chains_per_gpu": C,
                       "n_entries": info["n_entries"], "n_chromatic_per_call": nc,
+                      "sweep_engine": "tiles" if info["sweep_engine"] == 1 else "colours",
+                      "n_tiles": info["n_tiles"], "tile_rows_max": info["tile_rows_max"],
+                      "n_ghost_cells": info["n_ghost_cells"],
                       "single_chain": single,
                       "parallelism": f"chains {C} per GPU x {world} GPUs (independent)"},
            "roofline": roofline, "cpu_baseline": cpu, "secondary": mcmc}

@@ -120,7 +120,6 @@ struct nngp_ctx {
 namespace {
 
 constexpr int kTileNT = 512;       // threads per tile workgroup (NNGP_TILE_NT: 256, 512, 1024)
-constexpr int kTileCells = 4096;   // cells per own batch (RMAX = kTileCells / NT per thread)
 constexpr int kTileTarget = 2048;  // locations per tile (default tile count: n / this, <= CUs)
 
 thread_local std::string g_err;
@@ -407,10 +406,11 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
         delete c;
         return fail_msg(nullptr, NNGP_ERR_ARG, "NNGP_TILE_NT must be 256, 512 or 1024");
       }
-      bool ok = cus > 0 && build_tile_layout(nn.data(), n, b, coloring, locs, d, T, NT, kTileCells / NT, c->tl, terr);
-      if (ok && tile_lds_bytes(c->tl.max_rows, n_chains, NT) > lds_max) {
+      bool ok = cus > 0 && build_tile_layout(nn.data(), n, b, coloring, locs, d, T, NT, tile_rmax(n_chains, NT), c->tl, terr);
+      const int need = ok ? tile_lds_bytes(c->tl.max_rows, n_chains, NT, c->tl.K, c->tl.max_batches) : 0;
+      if (ok && need > lds_max) {
         ok = false;
-        terr = "tile layout needs " + std::to_string(tile_lds_bytes(c->tl.max_rows, n_chains, NT)) +
+        terr = "tile layout needs " + std::to_string(need) +
                " B of LDS per tile (device: " + std::to_string(lds_max) + ")";
       }
       if (ok) {
@@ -927,7 +927,9 @@ static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, int mask, const double*
     a.n_sweeps = n_sweeps;
     a.chain_mask = mask;
     a.z_in = z_dev;
-    HIPCHK(c, launch_sweep_tiles(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NT));
+    a.exp = 0;
+    if (const char* e = std::getenv("NNGP_TILE_EXP")) a.exp = std::atoi(e);
+    HIPCHK(c, launch_sweep_tiles(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NT, c->tl.max_batches));
     HIPCHK(c, hipMemcpyAsync(c->tmo_h, c->ctl_d + 1, sizeof(unsigned), hipMemcpyDeviceToHost, c->st));
   }
   if ((parts & kColours) && c->engine == 0) {

@@ -586,6 +586,7 @@ bool build_tile_layout(const int* nn, int n, int b, const int* colors, const dou
       }
       L.batch_ptr[pc + 1] = (int)L.batch.size();
     }
+    L.max_batches = std::max(L.max_batches, L.batch_ptr[(size_t)t * K + K] - L.batch_ptr[(size_t)t * K]);
     // ghost cells: foreign members j of the tile's rows, by colour of j
     for (auto& g : gh) g.clear();
     for (size_t q = 0; q < rows.size(); ++q) {

@@ -107,6 +107,7 @@ struct TileLayout {
   int n = 0, b = 0, K = 0, T = 0, NT = 0, RMAX = 0;
   long long nnz = 0;
   int max_rows = 0;                  // max |E_t|
+  int max_batches = 0;               // max own batches of a tile
   int max_collen = 0;
   std::vector<int> rpos;             // n: loc -> device row (Morton rank)
   std::vector<int> compact_loc;      // n: slot -> loc

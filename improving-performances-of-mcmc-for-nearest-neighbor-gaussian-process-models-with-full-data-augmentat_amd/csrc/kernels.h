@@ -140,10 +140,18 @@ struct TileLaunch {
   int n_sweeps;
   int chain_mask;
   const double* z_in;         // injected normals, per sweep: slot x C (nullptr: Philox inline)
+  int exp;                    // timing experiments (NNGP_TILE_EXP; 0 in production)
 };
 
-int tile_lds_bytes(int max_rows, int C, int NT);
-hipError_t launch_sweep_tiles(hipStream_t st, const TileDev& D, const TileLaunch& a, int max_rows, int NT);
+int tile_lds_bytes(int max_rows, int C, int NT, int K, int max_batches);
+// cells per thread of an own batch (the layout's RMAX): two batches of C
+// chains stay in registers (C >= 3: fewer cells per batch)
+// double-buffered batch registers (the next colour's loads in flight during
+// this colour's work) where two batches fit in registers
+constexpr int tile_double_buffer(int C) { return C <= 2 ? 1 : 0; }
+constexpr int tile_rmax(int C, int NT) { return 4096 / NT; }
+hipError_t launch_sweep_tiles(hipStream_t st, const TileDev& D, const TileLaunch& a, int max_rows, int NT,
+                              int max_batches);
 // chain `chain`: cell/ghost values from Linv (device order) and precision_diag
 hipError_t launch_tile_refresh(hipStream_t st, const TileDev& D, int nbatches, int NT, const int* cell_src,
                                const int* gsrc, const double* linv, int chain);

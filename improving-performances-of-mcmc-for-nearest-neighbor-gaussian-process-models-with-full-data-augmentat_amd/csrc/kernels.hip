@@ -1044,9 +1044,10 @@ constexpr int kTExported = 1 << 30;
 constexpr int kTSlots = 256;       // slots per own batch (graph_prep.h kTileSlotsMax)
 constexpr int kTSpreadLds = 82 * 1024;  // LDS floor: at most one tile per CU
 
-int tile_lds_bytes(int max_rows, int C, int NT) {
+int tile_lds_bytes(int max_rows, int C, int NT, int K, int max_batches) {
   const int rbytes = ((max_rows * C * 8 + 15) / 16) * 16;
-  return rbytes + kTSlots * C * 8 + (NT / 64) * (C * 8 + 4) + 16;
+  return rbytes + kTSlots * C * 8 + (NT / 64) * C * 8 + 4 * C * 8 + max_batches * 16 + 2 * (K + 1) * 4 +
+         (NT / 64) * 4 + 64;
 }
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
@@ -1058,24 +1059,22 @@ __global__ void tile_call_bump_kernel(unsigned* ctl) {
 
 // registers of one own batch: this thread's cells (f = t*R + j) and its draw
 // items u = t + k*NT < nslots*C (slot q = u / C, chain u % C: per-slot
-// records of consecutive items are consecutive, the loads coalesce), and,
-// once tile_prep_items has run, each item's draw scalars
+// records of consecutive items are consecutive, the loads coalesce).  Item
+// fields hold the raw records after tile_load_batch and the draw scalars
+// after tile_prep_items (in place: two batches stay in registers).
 template <int C, int NT, int RMAX>
 struct TileBatchRegs {
   static constexpr int IMAX = (kTSlots * C + NT - 1) / NT;
   int R, ns, x0;
   uint32_t pk[RMAX];
   double v[RMAX][C];
-  int2 si[IMAX];
-  int loc[IMAX];
-  double2 dr[IMAX];
-  double w[IMAX];
-  double cR[IMAX], invP[IMAX], zs[IMAX], is2[IMAX];
+  int nobs[IMAX], flag[IMAX], loc[IMAX];
+  double a0[IMAX], a1[IMAX];  // raw: precision_diag, residuals_sum; prepped: cR, 1/P
+  double w[IMAX], zs[IMAX];   // w; prepped: z / sqrt(P)
 };
 
 template <int C, int NT, int RMAX>
-__device__ __forceinline__ void tile_load_batch(const TileDev& D, int bi, TileBatchRegs<C, NT, RMAX>& b, int t) {
-  const int4 B = D.batch[bi];
+__device__ __forceinline__ void tile_load_batch(const TileDev& D, const int4 B, TileBatchRegs<C, NT, RMAX>& b, int t) {
   b.R = B.y; b.ns = B.z; b.x0 = B.w;
 #pragma unroll
   for (int j = 0; j < RMAX; ++j) {
@@ -1094,9 +1093,13 @@ __device__ __forceinline__ void tile_load_batch(const TileDev& D, int bi, TileBa
     if (u < b.ns * C) {
       const int q = u / C;
       const size_t xu = (size_t)b.x0 * C + u;  // = (x0 + q) * C + chain
-      b.si[k] = D.sinfo[b.x0 + q];
+      const int2 si = D.sinfo[b.x0 + q];
+      b.nobs[k] = si.x;
+      b.flag[k] = si.y;
       b.loc[k] = D.slot_loc[b.x0 + q];
-      b.dr[k] = D.dr[xu];
+      const double2 dr = D.dr[xu];
+      b.a0[k] = dr.x;
+      b.a1[k] = dr.y;
       b.w[k] = D.w_slot[xu];
     }
   }
@@ -1106,27 +1109,28 @@ __device__ __forceinline__ void tile_load_batch(const TileDev& D, int bi, TileBa
 // + z/sqrt(P) with cR = R/t2 + D w/s2 (w of an own slot is constant until its
 // colour, so this runs a colour ahead, during the previous hand-off)
 template <int C, int NT, int RMAX>
-__device__ __forceinline__ void tile_prep_items(const TileDev& D, const TileLaunch& a, int s, TileBatchRegs<C, NT, RMAX>& b,
-                                                int t) {
+__device__ __forceinline__ void tile_prep_items(const TileDev& D, const TileLaunch& a, const double* sc_s,
+                                                const unsigned long long* seed_s, int s,
+                                                TileBatchRegs<C, NT, RMAX>& b, int t) {
 #pragma unroll
   for (int k = 0; k < TileBatchRegs<C, NT, RMAX>::IMAX; ++k) {
     const int u = t + k * NT;
     if (u < b.ns * C) {
       const int q = u / C, ch = u - q * C;
-      const SweepScalars& sc = D.scal[ch];
-      const double inv_s2 = sc.inv_s2, inv_t2 = sc.inv_t2;
-      const double z = a.z_in ? a.z_in[((size_t)s * D.n + b.x0 + q) * C + ch]
-                              : normal_loc(sc.seed, sc.counter_base + s, (uint32_t)b.loc[k]);
-      const double P = b.dr[k].x * inv_s2 + (double)b.si[k].x * inv_t2;
-      b.invP[k] = 1.0 / P;
+      const double inv_s2 = sc_s[2 * ch], inv_t2 = sc_s[2 * ch + 1];
+      double z = 0.0;
+      if (a.z_in) z = a.z_in[((size_t)s * D.n + b.x0 + q) * C + ch];
+      else if (!(a.exp & 1)) z = normal_loc(seed_s[2 * ch], seed_s[2 * ch + 1] + s, (uint32_t)b.loc[k]);
+      const double P = b.a0[k] * inv_s2 + (double)b.nobs[k] * inv_t2;
+      const double cR = inv_t2 * b.a1[k] + inv_s2 * (b.a0[k] * b.w[k]);
+      b.a0[k] = cR;
+      b.a1[k] = 1.0 / P;
       b.zs[k] = z / sqrt(P);
-      b.cR[k] = inv_t2 * b.dr[k].y + inv_s2 * (b.dr[k].x * b.w[k]);
-      b.is2[k] = inv_s2;
     }
   }
 }
 
-// ghost cells of one chunk: local row, foreign slot, B values, received dw
+// ghost cells of one chunk: local row, foreign slot, B values
 template <int C, int GMAX>
 struct TileGhostRegs {
   int lr[GMAX], gx[GMAX];
@@ -1149,244 +1153,315 @@ __device__ __forceinline__ void tile_load_ghosts(const TileDev& D, int gb, int g
   }
 }
 
-template <int C, int NT, int RMAX, int GMAX, int PROBE>
+// per-workgroup state of the persistent sweep
+struct TileState {
+  double* r_s;
+  double* acc_s;
+  double* wsum;
+  double* sc_s;   // C x {inv_s2, inv_t2}
+  unsigned long long* seed_s;  // C x {seed, counter_base}
+  int4* batch_s;  // this tile's own batches
+  int* bptr_s;    // K+1: batches of colour c = batch_s[bptr_s[c] .. bptr_s[c+1])
+  int* gptr_s;    // K+1: ghost cells of colour c (global indices)
+  int* wflag;
+  __amdgpu_buffer_rsrc_t gran;
+  unsigned call;
+  unsigned* tmo;
+  bool timed_out;
+  int T, t, lane, wv, K, nph;
+  unsigned long long tp[8], t_prev;
+};
+
+#define TSTAMP(S, k)                                                      \
+  do {                                                                    \
+    if (PROBE) {                                                          \
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");         \
+      const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();   \
+      if ((k) >= 0) (S).tp[(k) < 0 ? 0 : (k)] += now_ - (S).t_prev;       \
+      (S).t_prev = now_;                                                  \
+    }                                                                     \
+  } while (0)
+
+// one own batch of colour c (epoch): products -> slot totals -> draws ->
+// scatter.  LDS and registers only, plus the draws' stores: no global load
+// (a load here would wait behind the next batch's prefetch, vmcnt is in order)
+template <int C, int NT, int RMAX, int PROBE>
+__device__ __forceinline__ void tile_own_batch(const TileDev& D, const TileLaunch& a, TileState& S,
+                                               TileBatchRegs<C, NT, RMAX>& b, unsigned epoch) {
+  constexpr int IMAX = TileBatchRegs<C, NT, RMAX>::IMAX;
+  const int t = S.t, lane = S.lane, wv = S.wv;
+  double* r_s = S.r_s;
+  double* acc_s = S.acc_s;
+  const int R = b.R, nit = b.ns * C;
+  // products, running sums restarted at slot starts.  A slot that began in
+  // this thread is complete at its last cell (-> acc_s); the thread's first
+  // cells may continue a slot of earlier threads: its end (if here) waits for
+  // the carry of those threads.
+  double run[C], cont[C];
+  int cont_q = -1;
+  bool seen_start = false;
+#pragma unroll
+  for (int ch = 0; ch < C; ++ch) { run[ch] = 0.0; cont[ch] = 0.0; }
+#pragma unroll
+  for (int j = 0; j < RMAX; ++j) {
+    if (j < R) {
+      const uint32_t lr = b.pk[j] & kTPad;
+      const bool st = (b.pk[j] & kTStart) != 0;
+#pragma unroll
+      for (int ch = 0; ch < C; ++ch) {
+        const double p = (lr != kTPad) ? b.v[j][ch] * r_s[lr * C + ch] : 0.0;
+        run[ch] = st ? p : run[ch] + p;
+      }
+      seen_start |= st;
+      if (b.pk[j] & kTEnd) {
+        const int q = (int)((b.pk[j] >> 17) & 0x7FF);
+        if (seen_start) {
+#pragma unroll
+          for (int ch = 0; ch < C; ++ch) acc_s[q * C + ch] = run[ch];
+        } else {
+          cont_q = q;
+#pragma unroll
+          for (int ch = 0; ch < C; ++ch) cont[ch] = run[ch];
+        }
+      }
+    }
+  }
+  TSTAMP(S, 1);
+  // segmented inclusive scan of the thread tails (restart at threads holding
+  // a slot start): in the wave by shuffles, across waves through LDS
+  double v[C];
+  int f = seen_start ? 1 : 0;
+#pragma unroll
+  for (int ch = 0; ch < C; ++ch) v[ch] = run[ch];
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    double vu[C];
+#pragma unroll
+    for (int ch = 0; ch < C; ++ch) vu[ch] = __shfl_up(v[ch], d, 64);
+    const int fu = __shfl_up(f, d, 64);
+    if (lane >= d) {
+      if (!f) {
+#pragma unroll
+        for (int ch = 0; ch < C; ++ch) v[ch] = vu[ch] + v[ch];
+      }
+      f |= fu;
+    }
+  }
+  if (lane == 63) {
+#pragma unroll
+    for (int ch = 0; ch < C; ++ch) S.wsum[wv * C + ch] = v[ch];
+    S.wflag[wv] = f;
+  }
+  __syncthreads();
+  double in[C];
+#pragma unroll
+  for (int ch = 0; ch < C; ++ch) in[ch] = 0.0;
+  for (int p = wv - 1; p >= 0; --p) {
+#pragma unroll
+    for (int ch = 0; ch < C; ++ch) in[ch] = S.wsum[p * C + ch] + in[ch];
+    if (S.wflag[p]) break;
+  }
+#pragma unroll
+  for (int ch = 0; ch < C; ++ch) {
+    const double Sv = f ? v[ch] : v[ch] + in[ch];
+    const double up = __shfl_up(Sv, 1, 64);
+    const double cp = lane ? up : in[ch];
+    if (cont_q >= 0) acc_s[cont_q * C + ch] = cont[ch] + cp;
+  }
+  __syncthreads();
+  TSTAMP(S, 2);
+#pragma unroll
+  for (int k = 0; k < IMAX; ++k) {
+    const int u = t + k * NT;
+    if (u < nit) {
+      const int ch = u % C;
+      double dw = 0.0;
+      const size_t xu = (size_t)b.x0 * C + u;
+      if ((a.chain_mask >> ch) & 1) {
+        const double wn = (b.a0[k] - S.sc_s[2 * ch] * acc_s[u]) * b.a1[k] + b.zs[k];
+        dw = wn - b.w[k];
+        D.w_slot[xu] = wn;
+      }
+      acc_s[u] = dw;
+      if (b.flag[k] & kTExported) {
+        const unsigned long long uu = __builtin_bit_cast(unsigned long long, dw);
+        u32x4_t g;
+        g.x = (unsigned)uu; g.y = (unsigned)(uu >> 32); g.z = epoch; g.w = S.call;
+        __builtin_amdgcn_raw_buffer_store_b128(g, S.gran, (int)(xu * 16), 0, 16);
+      }
+    }
+  }
+  __syncthreads();
+  TSTAMP(S, 3);
+#pragma unroll
+  for (int j = 0; j < RMAX; ++j) {
+    if (j < R) {
+      const uint32_t lr = b.pk[j] & kTPad;
+      if (lr != kTPad) {
+        const int q = (int)((b.pk[j] >> 17) & 0x7FF);
+#pragma unroll
+        for (int ch = 0; ch < C; ++ch) r_s[lr * C + ch] += b.v[j][ch] * acc_s[q * C + ch];
+      }
+    }
+  }
+  TSTAMP(S, 4);
+}
+
+// one colour phase ph = sweep*K + c with `cur` holding its prepared first
+// batch; the next phase's first batch is loaded into `nxt` at the start (its
+// HBM stream overlaps this colour's work) and prepared during the hand-off
+template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE>
+__device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a, TileState& S, int ph,
+                                           TileBatchRegs<C, NT, RMAX>& cur, TileBatchRegs<C, NT, RMAX>& nxt,
+                                           TileGhostRegs<C, GMAX>& gr, TileGhostRegs<C, GMAX>& grn) {
+  const int K = S.K, t = S.t;
+  const int s = ph / K, c = ph - s * K;
+  const unsigned epoch = (unsigned)ph + 1;
+  const int phn = ph + 1;
+  const int cn = phn % K, sn = phn / K;
+  const bool has_next = phn < S.nph;
+  const bool more = has_next && S.bptr_s[cn] < S.bptr_s[cn + 1];
+  const int bfirst = S.bptr_s[c], bend = S.bptr_s[c + 1];
+  const int g0 = S.gptr_s[c], g1 = S.gptr_s[c + 1];
+  const int gn0 = S.gptr_s[cn], gn1 = S.gptr_s[cn + 1];
+  if (DB) {
+    // the next colour's first batch and first ghost chunk: their HBM stream
+    // overlaps this colour's work (two register sets)
+    if (more) tile_load_batch<C, NT, RMAX>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
+    if (has_next && gn1 > gn0) tile_load_ghosts<C, NT, GMAX>(D, gn0, gn1, grn, t);
+  }
+  // ---- 1. own batches
+  for (int bi = bfirst; bi < bend; ++bi) {
+    if (bi != bfirst) {  // rare: a colour with more than one batch in this tile
+      tile_load_batch<C, NT, RMAX>(D, S.batch_s[bi], cur, t);
+      tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, s, cur, t);
+    }
+    tile_own_batch<C, NT, RMAX, PROBE>(D, a, S, cur, epoch);
+  }
+  if (!DB) {
+    // one register set: load the next batch now; this colour's ghosts too
+    if (more) tile_load_batch<C, NT, RMAX>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
+    if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
+  }
+  // ---- 2. the next batch is prepared while the neighbours publish colour c
+  if (more) tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, sn, nxt, t);
+  TSTAMP(S, 5);
+  // ---- 3. ghosts: poll each granule until it carries this epoch
+  for (int gb = g0; gb < g1; gb += NT * GMAX) {
+    if (gb != g0) tile_load_ghosts<C, NT, GMAX>(D, gb, g1, gr, t);
+    double dw[GMAX][C];
+    unsigned pend = 0;
+#pragma unroll
+    for (int k = 0; k < GMAX; ++k)
+      if (gr.lr[k] >= 0) pend |= ((1u << C) - 1) << (k * C);
+    if (a.exp & 2) pend = 0;
+    for (unsigned spins = 0; pend; ++spins) {
+#pragma unroll
+      for (int k = 0; k < GMAX; ++k)
+#pragma unroll
+        for (int ch = 0; ch < C; ++ch) {
+          const unsigned bit = 1u << (k * C + ch);
+          if (pend & bit) {
+            const u32x4_t g = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gr.gx[k] * C + ch) * 16), 0, 16);
+            if (g.z == epoch && g.w == S.call) {
+              dw[k][ch] = __builtin_bit_cast(double, (unsigned long long)g.x | ((unsigned long long)g.y << 32));
+              pend &= ~bit;
+            }
+          }
+        }
+      if (!pend) break;
+      if (S.timed_out || spins > (1u << 20)) {
+        if (!S.timed_out) __hip_atomic_store(S.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        S.timed_out = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int k = 0; k < GMAX; ++k)
+      if (gr.lr[k] >= 0 && !S.timed_out && !(a.exp & 2))
+#pragma unroll
+        for (int ch = 0; ch < C; ++ch) S.r_s[gr.lr[k] * C + ch] += gr.gv[k][ch] * dw[k][ch];
+  }
+  __syncthreads();
+  TSTAMP(S, 6);
+}
+
+template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE>
 __global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D, TileLaunch a) {
   using BR = TileBatchRegs<C, NT, RMAX>;
-  using GR = TileGhostRegs<C, GMAX>;
-  constexpr int IMAX = BR::IMAX;
   constexpr int NW = NT / 64;
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int T = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  TileState S;
+  S.T = blockIdx.x; S.t = threadIdx.x; S.lane = S.t & 63; S.wv = S.t >> 6; S.K = D.K;
+  S.nph = a.n_sweeps * D.K;
+  S.timed_out = false;
+  for (int k = 0; k < 8; ++k) S.tp[k] = 0;
+  S.t_prev = 0;
+  const int T = S.T, t = S.t, K = D.K;
   const int row0 = D.erow_ptr[T], nrows = D.erow_ptr[T + 1] - row0;
-  double* r_s = smem;
-  double* acc_s = smem + ((nrows * C + 1) / 2) * 2;   // kTSlots x C: slot totals, then dw
-  double* wsum = acc_s + kTSlots * C;                  // NW x C: segmented wave totals
-  int* wflag = reinterpret_cast<int*>(wsum + NW * C);  // NW: the wave holds a slot start
-  unsigned long long tp[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_prev = 0;
-#define TSTAMP(k)                                                       \
-  do {                                                                  \
-    if (PROBE) {                                                        \
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");       \
-      const unsigned long long now_ = __builtin_amdgcn_s_memrealtime(); \
-      if ((k) >= 0) tp[(k) < 0 ? 0 : (k)] += now_ - t_prev;             \
-      t_prev = now_;                                                    \
-    }                                                                   \
-  } while (0)
-  TSTAMP(-1);
+  const int b_lo = D.batch_ptr[T * K], nbt = D.batch_ptr[T * K + K] - b_lo;
+  S.r_s = smem;
+  S.acc_s = smem + ((nrows * C + 1) / 2) * 2;   // kTSlots x C: slot totals, then dw
+  S.wsum = S.acc_s + kTSlots * C;                // NW x C: segmented wave totals
+  S.sc_s = S.wsum + NW * C;                      // C x {inv_s2, inv_t2}
+  S.seed_s = reinterpret_cast<unsigned long long*>(S.sc_s + 2 * C);
+  S.batch_s = reinterpret_cast<int4*>(S.seed_s + 2 * C);
+  S.bptr_s = reinterpret_cast<int*>(S.batch_s + nbt);
+  S.gptr_s = S.bptr_s + K + 1;
+  S.wflag = S.gptr_s + K + 1;                    // NW: the wave holds a slot start
+  TSTAMP(S, -1);
   for (int lr = t; lr < nrows; lr += NT) {
     const size_t g = (size_t)D.erow[row0 + lr] * C;
 #pragma unroll
-    for (int ch = 0; ch < C; ++ch) r_s[lr * C + ch] = D.r[g + ch];
+    for (int ch = 0; ch < C; ++ch) S.r_s[lr * C + ch] = D.r[g + ch];
   }
-  const unsigned call = D.ctl[0];
-  unsigned* tmo = D.ctl + 1;
-  const __amdgpu_buffer_rsrc_t gran = __builtin_amdgcn_make_buffer_rsrc(D.dwx, 0, 0x7FFFFFFF, 0x00020000);
-  BR nb;  // the next colour's first batch, loaded and prepared a colour ahead
-  const int K = D.K;
-  if (D.batch_ptr[T * K] < D.batch_ptr[T * K + 1]) {
-    tile_load_batch<C, NT, RMAX>(D, D.batch_ptr[T * K], nb, t);
-    tile_prep_items<C, NT, RMAX>(D, a, 0, nb, t);
+  // per-tile metadata in LDS: no dependent scalar loads in the phase loop
+  for (int i = t; i < nbt; i += NT) S.batch_s[i] = D.batch[b_lo + i];
+  for (int i = t; i <= K; i += NT) {
+    S.bptr_s[i] = D.batch_ptr[T * K + i] - b_lo;
+    S.gptr_s[i] = D.gptr[T * K + i];
   }
+  if (t < C) {
+    S.sc_s[2 * t] = D.scal[t].inv_s2;
+    S.sc_s[2 * t + 1] = D.scal[t].inv_t2;
+    S.seed_s[2 * t] = D.scal[t].seed;
+    S.seed_s[2 * t + 1] = D.scal[t].counter_base;
+  }
+  S.call = D.ctl[0];
+  S.tmo = D.ctl + 1;
+  S.gran = __builtin_amdgcn_make_buffer_rsrc(D.dwx, 0, 0x7FFFFFFF, 0x00020000);
   __syncthreads();
-  TSTAMP(7);
-  unsigned epoch = 0;
-  bool timed_out = false;
-  for (int s = 0; s < a.n_sweeps; ++s) {
-    for (int c = 0; c < K; ++c) {
-      ++epoch;
-      const int pc = T * K + c;
-      // ---- 1. own batches
-      const int bfirst = D.batch_ptr[pc], bend = D.batch_ptr[pc + 1];
-      for (int bi = bfirst; bi < bend; ++bi) {
-        BR& b = nb;  // the prefetched first batch; further batches load in place
-        if (bi != bfirst) {
-          tile_load_batch<C, NT, RMAX>(D, bi, b, t);
-          tile_prep_items<C, NT, RMAX>(D, a, s, b, t);
-        }
-        const int R = b.R, nit = b.ns * C;
-        // products, running sums restarted at slot starts.  A slot that
-        // began in this thread is complete at its last cell (-> acc_s); the
-        // thread's first cells may continue a slot of earlier threads: its
-        // end (if here) waits for the carry of those threads.
-        double run[C], cont[C];
-        int cont_q = -1;
-        bool seen_start = false;
-#pragma unroll
-        for (int ch = 0; ch < C; ++ch) { run[ch] = 0.0; cont[ch] = 0.0; }
-#pragma unroll
-        for (int j = 0; j < RMAX; ++j) {
-          if (j < R) {
-            const uint32_t lr = b.pk[j] & kTPad;
-            const bool st = (b.pk[j] & kTStart) != 0;
-#pragma unroll
-            for (int ch = 0; ch < C; ++ch) {
-              const double p = (lr != kTPad) ? b.v[j][ch] * r_s[lr * C + ch] : 0.0;
-              run[ch] = st ? p : run[ch] + p;
-            }
-            seen_start |= st;
-            if (b.pk[j] & kTEnd) {
-              const int q = (int)((b.pk[j] >> 17) & 0x7FF);
-              if (seen_start) {
-#pragma unroll
-                for (int ch = 0; ch < C; ++ch) acc_s[q * C + ch] = run[ch];
-              } else {
-                cont_q = q;
-#pragma unroll
-                for (int ch = 0; ch < C; ++ch) cont[ch] = run[ch];
-              }
-            }
-          }
-        }
-        TSTAMP(1);
-        // segmented inclusive scan of the thread tails (restart at threads
-        // holding a slot start): in the wave by shuffles, across waves
-        // through LDS
-        double v[C];
-        int f = seen_start ? 1 : 0;
-#pragma unroll
-        for (int ch = 0; ch < C; ++ch) v[ch] = run[ch];
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          double vu[C];
-#pragma unroll
-          for (int ch = 0; ch < C; ++ch) vu[ch] = __shfl_up(v[ch], d, 64);
-          const int fu = __shfl_up(f, d, 64);
-          if (lane >= d) {
-            if (!f) {
-#pragma unroll
-              for (int ch = 0; ch < C; ++ch) v[ch] = vu[ch] + v[ch];
-            }
-            f |= fu;
-          }
-        }
-        if (lane == 63) {
-#pragma unroll
-          for (int ch = 0; ch < C; ++ch) wsum[wv * C + ch] = v[ch];
-          wflag[wv] = f;
-        }
-        __syncthreads();
-        double in[C];
-#pragma unroll
-        for (int ch = 0; ch < C; ++ch) in[ch] = 0.0;
-        for (int p = wv - 1; p >= 0; --p) {
-#pragma unroll
-          for (int ch = 0; ch < C; ++ch) in[ch] = wsum[p * C + ch] + in[ch];
-          if (wflag[p]) break;
-        }
-        double cp[C];
-#pragma unroll
-        for (int ch = 0; ch < C; ++ch) {
-          const double S = f ? v[ch] : v[ch] + in[ch];
-          const double up = __shfl_up(S, 1, 64);
-          cp[ch] = lane ? up : in[ch];
-        }
-        if (cont_q >= 0) {
-#pragma unroll
-          for (int ch = 0; ch < C; ++ch) acc_s[cont_q * C + ch] = cont[ch] + cp[ch];
-        }
-        __syncthreads();
-        TSTAMP(2);
-#pragma unroll
-        for (int k = 0; k < IMAX; ++k) {
-          const int u = t + k * NT;
-          if (u < nit) {
-            const int ch = u % C;
-            double dw = 0.0;
-            const size_t xu = (size_t)b.x0 * C + u;
-            if ((a.chain_mask >> ch) & 1) {
-              const double wn = (b.cR[k] - b.is2[k] * acc_s[u]) * b.invP[k] + b.zs[k];
-              dw = wn - b.w[k];
-              D.w_slot[xu] = wn;
-            }
-            acc_s[u] = dw;
-            if (b.si[k].y & kTExported) {
-              const unsigned long long uu = __builtin_bit_cast(unsigned long long, dw);
-              u32x4_t g;
-              g.x = (unsigned)uu; g.y = (unsigned)(uu >> 32); g.z = epoch; g.w = call;
-              __builtin_amdgcn_raw_buffer_store_b128(g, gran, (int)(xu * 16), 0, 16);
-            }
-          }
-        }
-        __syncthreads();
-        TSTAMP(3);
-#pragma unroll
-        for (int j = 0; j < RMAX; ++j) {
-          if (j < R) {
-            const uint32_t lr = b.pk[j] & kTPad;
-            if (lr != kTPad) {
-              const int q = (int)((b.pk[j] >> 17) & 0x7FF);
-#pragma unroll
-              for (int ch = 0; ch < C; ++ch) r_s[lr * C + ch] += b.v[j][ch] * acc_s[q * C + ch];
-            }
-          }
-        }
-        TSTAMP(4);
-      }
-      // ---- 2. next colour's first batch: loads, then (while neighbours
-      // publish colour c) its draw scalars; this colour's ghost cells load
-      const int g0 = D.gptr[pc], g1 = D.gptr[pc + 1];
-      GR gr;
-      {
-        const int cn = c + 1 < K ? c + 1 : 0;
-        const int sn = c + 1 < K ? s : s + 1;
-        const int pn = T * K + cn;
-        const bool more = sn < a.n_sweeps && D.batch_ptr[pn] < D.batch_ptr[pn + 1];
-        if (more) tile_load_batch<C, NT, RMAX>(D, D.batch_ptr[pn], nb, t);
-        if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
-        if (more) tile_prep_items<C, NT, RMAX>(D, a, sn, nb, t);
-      }
-      TSTAMP(5);
-      // ---- 3. ghosts: poll each granule until it carries this epoch
-      for (int gb = g0; gb < g1; gb += NT * GMAX) {
-        if (gb != g0) tile_load_ghosts<C, NT, GMAX>(D, gb, g1, gr, t);
-        double dw[GMAX][C];
-        unsigned pend = 0;
-#pragma unroll
-        for (int k = 0; k < GMAX; ++k)
-          if (gr.lr[k] >= 0) pend |= ((1u << C) - 1) << (k * C);
-        for (unsigned spins = 0; pend; ++spins) {
-#pragma unroll
-          for (int k = 0; k < GMAX; ++k)
-#pragma unroll
-            for (int ch = 0; ch < C; ++ch) {
-              const unsigned bit = 1u << (k * C + ch);
-              if (pend & bit) {
-                const u32x4_t g = __builtin_amdgcn_raw_buffer_load_b128(gran, (int)(((size_t)gr.gx[k] * C + ch) * 16), 0, 16);
-                if (g.z == epoch && g.w == call) {
-                  dw[k][ch] = __builtin_bit_cast(double, (unsigned long long)g.x | ((unsigned long long)g.y << 32));
-                  pend &= ~bit;
-                }
-              }
-            }
-          if (!pend) break;
-          if (timed_out || spins > (1u << 20)) {
-            if (!timed_out) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            timed_out = true;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-#pragma unroll
-        for (int k = 0; k < GMAX; ++k)
-          if (gr.lr[k] >= 0 && !timed_out)
-#pragma unroll
-            for (int ch = 0; ch < C; ++ch) r_s[gr.lr[k] * C + ch] += gr.gv[k][ch] * dw[k][ch];
-      }
-      __syncthreads();
-      TSTAMP(6);
+  BR A, B;  // batch register sets: the current colour's and (DB) the next one's
+  TileGhostRegs<C, GMAX> GA, GB;
+  if (S.nph > 0 && S.bptr_s[0] < S.bptr_s[1]) {
+    tile_load_batch<C, NT, RMAX>(D, S.batch_s[S.bptr_s[0]], A, t);
+    tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, 0, A, t);
+  }
+  if (DB && S.nph > 0 && S.gptr_s[0] < S.gptr_s[1]) tile_load_ghosts<C, NT, GMAX>(D, S.gptr_s[0], S.gptr_s[1], GA, t);
+  __syncthreads();
+  TSTAMP(S, 7);
+  if (DB) {
+    for (int ph = 0; ph < S.nph; ph += 2) {
+      tile_phase<C, NT, RMAX, GMAX, DB, PROBE>(D, a, S, ph, A, B, GA, GB);
+      if (ph + 1 < S.nph) tile_phase<C, NT, RMAX, GMAX, DB, PROBE>(D, a, S, ph + 1, B, A, GB, GA);
     }
+  } else {
+    for (int ph = 0; ph < S.nph; ++ph) tile_phase<C, NT, RMAX, GMAX, DB, PROBE>(D, a, S, ph, A, A, GA, GA);
   }
   if (PROBE && t == 0) {
     unsigned long long* o = D.dbg + (size_t)T * 8;
-    for (int k = 0; k < 8; ++k) o[k] = tp[k];
+    for (int k = 0; k < 8; ++k) o[k] = S.tp[k];
   }
-#undef TSTAMP
 }
+#undef TSTAMP
 
 template <int C, int NT, int PROBE>
 static hipError_t launch_tiles_c(hipStream_t st, const TileDev& D, const TileLaunch& a, int lds) {
-  constexpr int RMAX = 4096 / NT;
-  auto k = sweep_tiles_kernel<C, NT, RMAX, (1024 / NT > 0 ? 1024 / NT : 1), PROBE>;
+  constexpr int RMAX = tile_rmax(C, NT);
+  constexpr int DB = tile_double_buffer(C);
+  constexpr int GMAX = (DB && C >= 3) ? (512 / NT > 0 ? 512 / NT : 1) : (1024 / NT > 0 ? 1024 / NT : 1);
+  auto k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE>;
   lds = lds < kTSpreadLds ? kTSpreadLds : lds;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return e;
@@ -1413,8 +1488,9 @@ static hipError_t launch_tiles_nt(hipStream_t st, const TileDev& D, const TileLa
   }
 }
 
-hipError_t launch_sweep_tiles(hipStream_t st, const TileDev& D, const TileLaunch& a, int max_rows, int NT) {
-  const int lds = tile_lds_bytes(max_rows, D.C, NT);
+hipError_t launch_sweep_tiles(hipStream_t st, const TileDev& D, const TileLaunch& a, int max_rows, int NT,
+                              int max_batches) {
+  const int lds = tile_lds_bytes(max_rows, D.C, NT, D.K, max_batches);
   switch (NT) {
     case 256: return launch_tiles_nt<256>(st, D, a, lds);
     case 512: return launch_tiles_nt<512>(st, D, a, lds);
@@ -1441,7 +1517,7 @@ __global__ __launch_bounds__(256) void tile_refresh_kernel(TileDev D, int nbatch
       gv[g] = linv[gsrc[g]];
     return;
   }
-  const int4 B = D.batch[blockIdx.x];
+  const int4 B = D.batch[blockIdx.x];  // refresh kernel: one batch per workgroup
   double* cv = const_cast<double*>(D.cell_val) + (size_t)chain * D.n_cells;
   for (int e0 = t; e0 < B.y * NT; e0 += 256) {
     const long long e = B.x + e0;
