@@ -19,6 +19,7 @@ ap.add_argument("root")
 ap.add_argument("pattern")
 ap.add_argument("--json")
 ap.add_argument("--chains", type=int, default=3)
+ap.add_argument("--sweeps-per-dispatch", type=float, default=None)
 a = ap.parse_args()
 
 KNOWN = 512 << 20
@@ -54,5 +55,6 @@ if a.json:
     json.dump({"kernel": a.pattern, "chains": a.chains, "per_dispatch": sweep, "dispatches": counts,
                "calibration_counter_over_true": cal, "read_correction": f_read, "write_correction": f_write,
                "traffic_bytes_per_launch": traffic,
+               "sweeps_per_dispatch": a.sweeps_per_dispatch,
                "workload": {"n": 1000000, "m": 15, "covfun": "matern15_isotropic", "chains": a.chains}},
               open(a.json, "w"), indent=1)
