@@ -1333,6 +1333,7 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
   // ---- 1. own batches
   for (int bi = bfirst; bi < bend; ++bi) {
     if (bi != bfirst) {  // rare: a colour with more than one batch in this tile
+      __syncthreads();   // acc_s is indexed by slot-in-batch: every wave is done with the last batch
       tile_load_batch<C, NT, RMAX>(D, S.batch_s[bi], cur, t);
       tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, s, cur, t);
     }

@@ -79,6 +79,10 @@ int main(int argc, char** argv) {
   for (auto& v : z) v = N01(g);
   const double inv_s2[4] = {0.7, 1.3, 0.9, 1.1}, inv_t2[4] = {2.0, 0.5, 1.0, 4.0};
   // ---- reference: serial local-form sweep in colour order
+  std::vector<std::vector<std::pair<int, int>>> colB(n);  // column i -> (row k, position u)
+  for (int k = 0; k < n; ++k)
+    for (int u = 0; u < b; ++u)
+      if (nn[(size_t)k * b + u] >= 0) colB[nn[(size_t)k * b + u]].push_back({k, u});
   std::vector<std::vector<double>> wr = w0;
   for (int ch = 0; ch < C; ++ch)
     for (int s = 0; s < sweeps; ++s) {
@@ -93,9 +97,7 @@ int main(int argc, char** argv) {
         for (int i = 0; i < n; ++i) {
           if (col[i] != c) continue;
           double acc = 0.0;
-          for (int k = 0; k < n; ++k)  // slow but plain: column i of B
-            for (int u = 0; u < b; ++u)
-              if (nn[(size_t)k * b + u] == i) acc += linv[ch][(size_t)L.rpos[k] * b + u] * r[k];
+          for (const auto& ku : colB[i]) acc += linv[ch][(size_t)L.rpos[ku.first] * b + ku.second] * r[ku.first];
           acc -= Dg[ch][i] * wr[ch][i];
           const double P = Dg[ch][i] * inv_s2[ch] + nobs[i] * inv_t2[ch];
           const double wn = (Rs[ch][i] * inv_t2[ch] - acc * inv_s2[ch]) / P + z[((size_t)s * n + i) * C + ch] / std::sqrt(P);

@@ -146,7 +146,8 @@ def tile_check_exe(tmp_path_factory):
 
 @pytest.mark.parametrize("n,m,tiles,chains,seed,nt,rmax", [
     (1500, 10, 16, 2, 1, 256, 16), (800, 5, 7, 3, 2, 64, 4), (300, 8, 1, 1, 3, 256, 16),
-    (2000, 15, 40, 4, 4, 128, 2), (1200, 12, 256, 1, 5, 256, 16), (5, 2, 8, 2, 6, 64, 1)])
+    (2000, 15, 40, 4, 4, 128, 2), (1200, 12, 256, 1, 5, 256, 16), (5, 2, 8, 2, 6, 64, 1),
+    (200000, 15, 24, 1, 21, 512, 8)])
 def test_tile_sweep_emulation(tile_check_exe, n, m, tiles, chains, seed, nt, rmax):
     """C++ emulation of the tile-resident sweep kernel step by step on the
     tile layout (own batches, thread runs and tails, slot totals, published
