@@ -927,8 +927,6 @@ static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, int mask, const double*
     a.n_sweeps = n_sweeps;
     a.chain_mask = mask;
     a.z_in = z_dev;
-    a.exp = 0;
-    if (const char* e = std::getenv("NNGP_TILE_EXP")) a.exp = std::atoi(e);
     HIPCHK(c, launch_sweep_tiles(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NT, c->tl.max_batches));
     HIPCHK(c, hipMemcpyAsync(c->tmo_h, c->ctl_d + 1, sizeof(unsigned), hipMemcpyDeviceToHost, c->st));
   }

@@ -140,7 +140,6 @@ struct TileLaunch {
   int n_sweeps;
   int chain_mask;
   const double* z_in;         // injected normals, per sweep: slot x C (nullptr: Philox inline)
-  int exp;                    // timing experiments (NNGP_TILE_EXP; 0 in production)
 };
 
 int tile_lds_bytes(int max_rows, int C, int NT, int K, int max_batches);

@@ -1120,7 +1120,7 @@ __device__ __forceinline__ void tile_prep_items(const TileDev& D, const TileLaun
       const double inv_s2 = sc_s[2 * ch], inv_t2 = sc_s[2 * ch + 1];
       double z = 0.0;
       if (a.z_in) z = a.z_in[((size_t)s * D.n + b.x0 + q) * C + ch];
-      else if (!(a.exp & 1)) z = normal_loc(seed_s[2 * ch], seed_s[2 * ch + 1] + s, (uint32_t)b.loc[k]);
+      else z = normal_loc(seed_s[2 * ch], seed_s[2 * ch + 1] + s, (uint32_t)b.loc[k]);
       const double P = b.a0[k] * inv_s2 + (double)b.nobs[k] * inv_t2;
       const double cR = inv_t2 * b.a1[k] + inv_s2 * (b.a0[k] * b.w[k]);
       b.a0[k] = cR;
@@ -1355,7 +1355,6 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
 #pragma unroll
     for (int k = 0; k < GMAX; ++k)
       if (gr.lr[k] >= 0) pend |= ((1u << C) - 1) << (k * C);
-    if (a.exp & 2) pend = 0;
     for (unsigned spins = 0; pend; ++spins) {
 #pragma unroll
       for (int k = 0; k < GMAX; ++k)
@@ -1380,7 +1379,7 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
     }
 #pragma unroll
     for (int k = 0; k < GMAX; ++k)
-      if (gr.lr[k] >= 0 && !S.timed_out && !(a.exp & 2))
+      if (gr.lr[k] >= 0 && !S.timed_out)
 #pragma unroll
         for (int ch = 0; ch < C; ++ch) S.r_s[gr.lr[k] * C + ch] += gr.gv[k][ch] * dw[k][ch];
   }
