@@ -8,6 +8,7 @@ reference's R functions.
 from ._lib import COVFUNS, NNGPError, lib  # noqa: F401  (fails loudly without libnngp.so)
 from .graph import find_ordered_nn, naive_greedy_coloring, order_maxmin, sparse_chol_indices  # noqa: F401
 from .context import ChainContext  # noqa: F401
+from .shard import ShardContext, init_shard_comm, sweep_chains_group  # noqa: F401
 from .initialize import mcmc_nngp_initialize  # noqa: F401
 from .update_gaussian import mcmc_nngp_update_Gaussian, ll_compressed_sparse_chol  # noqa: F401
 from .run import mcmc_nngp_run  # noqa: F401

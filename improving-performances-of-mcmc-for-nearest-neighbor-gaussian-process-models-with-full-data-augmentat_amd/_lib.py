@@ -33,7 +33,9 @@ ABI_SYMBOLS = (
     "nngp_field_response_ratio",
     "nngp_accept_field", "nngp_beta0_stats", "nngp_sum_squared_residuals", "nngp_spmv",
     "nngp_tri_solve", "nngp_sweep_timed", "nngp_device_normals",
+    "nngp_ctx_create_shard", "nngp_shard_unique_id", "nngp_shard_comm_init", "nngp_sweep_chains_group",
 )
+SHARD_ID_BYTES = 128  # NNGP_SHARD_ID_BYTES
 
 
 class NNGPError(RuntimeError):
@@ -48,7 +50,9 @@ class Info(C.Structure):
                 ("n_entries", C.c_longlong), ("max_collen", C.c_int), ("device", C.c_int),
                 ("n_chains", C.c_int), ("lanes_per_chain", C.c_int), ("n_chunks", C.c_int),
                 ("sweep_engine", C.c_int), ("n_tiles", C.c_int), ("tile_rows_max", C.c_int),
-                ("n_ghost_cells", C.c_longlong)]
+                ("n_ghost_cells", C.c_longlong), ("n_ranks", C.c_int), ("rank", C.c_int),
+                ("shard_owned", C.c_longlong), ("shard_needed_rows", C.c_longlong),
+                ("shard_exchange_slots", C.c_longlong)]
 
 
 _dp = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
@@ -100,6 +104,11 @@ def _load():
     L.nngp_sweep_timed.argtypes = [_vp, C.c_int, _dp, _dp, _dp, _up, _up,
                                    C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.nngp_device_normals.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_int, _dp]
+    L.nngp_ctx_create_shard.argtypes = [_dp, C.c_int, C.c_int, _ip, C.c_int, _ip, _ip, _dp, C.c_int,
+                                        C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_vp)]
+    L.nngp_shard_unique_id.argtypes = [C.c_char_p, C.c_int]
+    L.nngp_shard_comm_init.argtypes = [_vp, C.c_char_p, C.c_int]
+    L.nngp_sweep_chains_group.argtypes = [C.POINTER(_vp), C.c_int, C.c_int, _dp, _dp, _dp, _up, _up]
     return L
 
 

@@ -24,7 +24,7 @@ class ChainContext:
     chain (``select``; chain 0 by default)."""
 
     def __init__(self, locs, NNarray, coloring, locs_match, observed_field, device: int = -1,
-                 n_chains: int = 1):
+                 n_chains: int = 1, _shard=None):
         locs = np.asarray(locs, np.float64)
         if locs.ndim == 1:
             locs = locs[:, None]
@@ -35,9 +35,12 @@ class ChainContext:
         self.n_obs = len(observed_field)
         self.n_chains = int(n_chains)
         h = C.c_void_p()
-        check(lib.nngp_ctx_create(colmajor(locs, np.float64), n, d, colmajor(NNarray, np.int32), b,
-                                  i32(coloring), i32(locs_match), f64(observed_field), self.n_obs,
-                                  self.n_chains, int(device), C.byref(h)))
+        args = (colmajor(locs, np.float64), n, d, colmajor(NNarray, np.int32), b, i32(coloring), i32(locs_match),
+                f64(observed_field), self.n_obs, self.n_chains, int(device))
+        if _shard is None:
+            check(lib.nngp_ctx_create(*args, C.byref(h)))
+        else:
+            check(lib.nngp_ctx_create_shard(*args, int(_shard[0]), int(_shard[1]), C.byref(h)))
         self._h = h
         self._sel = 0
 

@@ -2,6 +2,7 @@
 // One nngp_ctx per group of <= 4 MCMC chains: device buffers, the sweep layout planned on the
 // host (graph_prep.cpp), one HIP stream, and cached hipGraphs of the sweep.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <climits>
@@ -113,6 +114,19 @@ struct nngp_ctx {
   unsigned* ctl_d = nullptr;      // [0] call id, [1] timeout word
   unsigned* tmo_h = nullptr;      // pinned copy of the timeout word after each launch
   unsigned long long* tdbg_d = nullptr;  // NNGP_PROBE=9: per-tile phase times
+  // colour-sharded sweep (nngp_ctx_create_shard; graph_prep.h ShardPlan):
+  // this context is rank sp.rank of sp.G; it sweeps its own chunks of every
+  // colour and exchanges {dw, w_new} of the colour's slots through xbuf_d
+  // (RCCL all-gather, or device copies between the contexts of a group)
+  bool shard = false;
+  ShardPlan sp;
+  int* sg_row_d = nullptr;        // ghost cells: device row
+  int* sg_recv_d = nullptr;       //              exchange index
+  int* sg_src_d = nullptr;        //              Linv index
+  double* sg_val_d = nullptr;     //              B value, C x cells
+  double2* xbuf_d = nullptr;      // exchange regions of all colours: slot x C
+  int* sp_pairs_d = nullptr;      // normal pairs of the rank
+  ncclComm_t comm = nullptr;
   std::map<long long, hipGraphExec_t> graphs;  // key: n_sweeps << 8 | chain mask
   std::vector<hipGraph_t> graph_objs;
 };
@@ -219,6 +233,10 @@ int refresh_sweep_values(nngp_ctx* c, int k) {
                                   c->ch[k].linv_d[0], k));
   else
     HIPCHK(c, launch_sell_refresh(c->st, sweep_dev(c), c->lay.nchunks, c->ent_src_d, c->ch[k].linv_d[0], k));
+  if (c->shard && !c->sp.grow.empty()) {
+    const int ng = (int)c->sp.grow.size();
+    HIPCHK(c, launch_permute_gather(c->st, ng, c->sg_src_d, c->ch[k].linv_d[0], c->sg_val_d + (size_t)k * ng));
+  }
   c->linv_cur_h[k] = c->ch[k].linv_d[0];
   HIPCHK(c, hipMemcpyAsync(c->linv_cur_d, c->linv_cur_h, sizeof(double*) * c->C, hipMemcpyHostToDevice, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
@@ -317,7 +335,9 @@ void nngp_ctx_destroy(nngp_ctx* c) {
                              c->chunk_first_d, c->loc_rank_d, c->pairs_d, c->level_ptr_d, c->zbuf_d, c->ent_pos_d, c->start_mask_d,
                              c->dpos_d, c->perm_d, c->tb_d, c->tb_ptr_d, c->cell_pk_d, c->cell_src_d,
                              c->cell_val_d, c->gcell_d, c->gsrc_d, c->gval_d, c->gptr_d, c->nb_ptr_d, c->nb_d,
-                             c->erow_ptr_d, c->erow_d, c->dwx_d, c->ctl_d, c->tdbg_d};
+                             c->erow_ptr_d, c->erow_d, c->dwx_d, c->ctl_d, c->tdbg_d, c->sg_row_d,
+                             c->sg_recv_d, c->sg_src_d, c->sg_val_d, c->xbuf_d, c->sp_pairs_d};
+  if (c->comm) ncclCommDestroy(c->comm);
   for (int k = 0; k < kMaxChains; ++k) {
     ChainState& s = c->ch[k];
     ptrs.insert(ptrs.end(), {s.linv_d[0], s.linv_d[1], s.field_d, s.field_prop_d, s.mu_d});
@@ -334,9 +354,10 @@ void nngp_ctx_destroy(nngp_ctx* c) {
 
 const char* nngp_ctx_last_error(const nngp_ctx* c) { return c ? c->err.c_str() : g_err.c_str(); }
 
-int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b, const int* coloring,
-                    const int* locs_match, const double* observed_field, int n_obs, int n_chains,
-                    int device, nngp_ctx** out) {
+// shard_G > 0: a rank of the colour-sharded sweep (colour-launch engine)
+static int ctx_create(const double* locs, int n, int d, const int* NNarray, int b, const int* coloring,
+                      const int* locs_match, const double* observed_field, int n_obs, int n_chains,
+                      int device, int shard_G, int shard_rank, nngp_ctx** out) {
   if (!out) return fail_msg(nullptr, NNGP_ERR_ARG, "ctx_create: out == NULL");
   *out = nullptr;
   if (!locs || !NNarray || !coloring || !locs_match || !observed_field || n < 1 || d < 1 || d > 4 ||
@@ -393,7 +414,7 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
       delete c;
       return fail_msg(nullptr, NNGP_ERR_ARG, "NNGP_ENGINE must be colors or tiles");
     }
-    if (es != "colors") {
+    if (es != "colors" && shard_G == 0) {
       int cus = 0, lds_max = 0;
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 0;
       if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeSharedMemPerBlockOptin, device) != hipSuccess) lds_max = 0;
@@ -435,6 +456,13 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
     if (!build_sweep_layout(nn.data(), n, b, coloring, locs, d, LW, c->lay, err)) {
       delete c;
       return fail_msg(nullptr, NNGP_ERR_ARG, err);
+    }
+    if (shard_G > 0) {
+      if (!build_shard_plan(nn.data(), n, b, coloring, c->lay, shard_G, shard_rank, c->sp, err)) {
+        delete c;
+        return fail_msg(nullptr, NNGP_ERR_ARG, err);
+      }
+      c->shard = true;
     }
   }
   const SweepLayout& L = c->lay;
@@ -630,6 +658,22 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
     CK(upload(c->ent_src_d, L.ent_src.data(), (size_t)L.n_entries, c->st));
     CK(hipMemsetAsync(c->ent_val_d, 0, sizeof(double) * std::max<long long>(1, L.n_entries * C), c->st));
   }
+  if (c->shard) {
+    const ShardPlan& SP = c->sp;
+    const size_t ng = SP.grow.size();
+    CK(dalloc(&c->sg_row_d, ng));
+    CK(dalloc(&c->sg_recv_d, ng));
+    CK(dalloc(&c->sg_src_d, ng));
+    CK(dalloc(&c->sg_val_d, ng * C));
+    CK(dalloc(&c->xbuf_d, (size_t)SP.xoff[SP.K] * C));
+    CK(dalloc(&c->sp_pairs_d, SP.pairs.size()));
+    CK(upload(c->sg_row_d, SP.grow.data(), ng, c->st));
+    CK(upload(c->sg_recv_d, SP.grecv.data(), ng, c->st));
+    CK(upload(c->sg_src_d, SP.gsrc.data(), ng, c->st));
+    CK(hipMemsetAsync(c->sg_val_d, 0, sizeof(double) * std::max<size_t>(1, ng * C), c->st));
+    CK(hipMemsetAsync(c->xbuf_d, 0, sizeof(double2) * std::max<size_t>(1, (size_t)SP.xoff[SP.K] * C), c->st));
+    CK(upload(c->sp_pairs_d, SP.pairs.data(), SP.pairs.size(), c->st));
+  }
   CK(hipMemcpyAsync(c->linv_cur_d, c->linv_cur_h, sizeof(double*) * C, hipMemcpyHostToDevice, c->st));
   CK(upload(c->level_rows_d, c->level_rows.data(), n, c->st));
   CK(upload(c->obs_ptr_d, obs_cnt.data(), (size_t)n + 1, c->st));
@@ -645,6 +689,24 @@ int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b,
 #undef CK
   *out = c;
   return NNGP_OK;
+}
+
+int nngp_ctx_create(const double* locs, int n, int d, const int* NNarray, int b, const int* coloring,
+                    const int* locs_match, const double* observed_field, int n_obs, int n_chains,
+                    int device, nngp_ctx** out) {
+  return ctx_create(locs, n, d, NNarray, b, coloring, locs_match, observed_field, n_obs, n_chains, device, 0, 0,
+                    out);
+}
+
+int nngp_ctx_create_shard(const double* locs, int n, int d, const int* NNarray, int b, const int* coloring,
+                          const int* locs_match, const double* observed_field, int n_obs, int n_chains,
+                          int device, int n_ranks, int rank, nngp_ctx** out) {
+  if (n_ranks < 1 || n_ranks > kMaxRanks || rank < 0 || rank >= n_ranks) {
+    if (out) *out = nullptr;
+    return fail_msg(nullptr, NNGP_ERR_ARG, "ctx_create_shard: need 1 <= n_ranks <= 64 and 0 <= rank < n_ranks");
+  }
+  return ctx_create(locs, n, d, NNarray, b, coloring, locs_match, observed_field, n_obs, n_chains, device,
+                    n_ranks, rank, out);
 }
 
 int nngp_set_chain(nngp_ctx* c, int chain) {
@@ -669,7 +731,12 @@ int nngp_ctx_info(const nngp_ctx* c, nngp_info* info) {
   info->sweep_engine = c->engine;
   info->n_tiles = c->engine == 1 ? c->tl.T : 0;
   info->tile_rows_max = c->engine == 1 ? c->tl.max_rows : 0;
-  info->n_ghost_cells = c->engine == 1 ? (long long)c->tl.gsrc.size() : 0;
+  info->n_ghost_cells = c->engine == 1 ? (long long)c->tl.gsrc.size() : (long long)c->sp.grow.size();
+  info->n_ranks = c->shard ? c->sp.G : 0;
+  info->rank = c->shard ? c->sp.rank : 0;
+  info->shard_owned = c->shard ? c->sp.owned : 0;
+  info->shard_needed_rows = c->shard ? c->sp.needed_rows : 0;
+  info->shard_exchange_slots = c->shard ? c->sp.xoff[c->sp.K] : 0;
   return NNGP_OK;
 }
 
@@ -975,6 +1042,8 @@ static int graph_for(nngp_ctx* c, int n_sweeps, int mask, hipGraphExec_t* out, i
   return NNGP_OK;
 }
 
+static int shard_call(nngp_ctx* c, int n_sweeps, int mask);
+
 int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double lnv, uint64_t seed,
                uint64_t counter_base, const double* z) {
   if (!c || n_sweeps < 0) return NNGP_ERR_ARG;
@@ -984,6 +1053,10 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
   const int k = c->cur, mask = 1 << k;
   if ((rc = sweep_prepare(c, k, beta0, log_scale, lnv, seed, counter_base))) return rc;
   if ((rc = upload_scalars(c))) return rc;
+  if (c->shard) {
+    if (z) return fail_msg(c, NNGP_ERR_ARG, "sweep: injected normals are not supported on shard contexts");
+    return shard_call(c, n_sweeps, mask);
+  }
   if (z) {
     // injected normals -> compact order, chain-interleaved
     const size_t need = (size_t)n_sweeps * c->C * c->n;
@@ -1020,6 +1093,7 @@ int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const doub
   for (int k = 0; k < c->C; ++k)
     if ((rc = sweep_prepare(c, k, beta0[k], log_scale[k], lnv[k], seed[k], counter_base[k]))) return rc;
   if ((rc = upload_scalars(c))) return rc;
+  if (c->shard) return shard_call(c, n_sweeps, (1 << c->C) - 1);
   hipGraphExec_t ex;
   if ((rc = graph_for(c, n_sweeps, (1 << c->C) - 1, &ex))) return rc;
   HIPCHK(c, hipGraphLaunch(ex, c->st));
@@ -1049,10 +1123,194 @@ int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const doub
   return NNGP_OK;
 }
 
+// ---------------------------------------------------------------- sharded sweep
+// A call of the colour-sharded sweep on rank sp.rank: the
+// prologue/epilogue of the single-rank call (every rank keeps a full replica
+// of w, so r = B w and field = w + beta0 need no exchange), and per colour:
+//   own    -- the rank's chunks of the colour; the kernel also writes {dw, w_new}
+//             of its slots into the rank's segment of the colour's exchange region;
+//   xchg   -- all-gather of the region (RCCL, in place) or, in a group of
+//             contexts in one process, device copies of the other segments;
+//   ghosts -- r_k += B[k,j] dw_j for the foreign members j of the colour in
+//             rows the rank's columns touch; w replica of foreign slots = w_new.
+static int enqueue_shard_own(nngp_ctx* c, int s, int col, int mask, int n_sweeps) {
+  const ShardPlan& P = c->sp;
+  const int G = P.G, rk = P.rank;
+  const size_t zn = (size_t)c->n * c->C;
+  ColorLaunch a;
+  a.chunk0 = P.cb[(size_t)col * (G + 1) + rk];
+  a.nch = P.cb[(size_t)col * (G + 1) + rk + 1] - a.chunk0;
+  a.chain_mask = mask;
+  a.sweep_local = s;
+  a.z_cur = c->zbuf_d + (size_t)(s & 1) * zn;
+  a.z_next = s + 1 < n_sweeps ? c->zbuf_d + (size_t)((s + 1) & 1) * zn : nullptr;
+  a.pairs = c->sp_pairs_d + P.pair_ptr[col];
+  a.npairs = P.pair_ptr[col + 1] - P.pair_ptr[col];
+  a.n = c->n;
+  a.xsend = c->xbuf_d + (size_t)(P.xoff[col] + (long long)rk * P.cnt[col]) * c->C;
+  a.xs0 = P.seg0[(size_t)col * (G + 1) + rk];
+  HIPCHK(c, launch_sweep_color(c->st, sweep_dev(c), a));
+  return NNGP_OK;
+}
+
+static int enqueue_shard_ghosts(nngp_ctx* c, int col, int mask) {
+  const ShardPlan& P = c->sp;
+  ShardGhostLaunch g;
+  g.grow = c->sg_row_d;
+  g.grecv = c->sg_recv_d;
+  g.gval = c->sg_val_d;
+  g.ng_total = (long long)P.grow.size();
+  g.g0 = P.gptr[col];
+  g.ng = P.gptr[col + 1] - g.g0;
+  g.xbuf = c->xbuf_d + (size_t)P.xoff[col] * c->C;
+  g.G = P.G;
+  g.rank = P.rank;
+  g.cnt = P.cnt[col];
+  for (int h = 0; h <= P.G; ++h) g.seg0[h] = P.seg0[(size_t)col * (P.G + 1) + h];
+  g.chain_mask = mask;
+  HIPCHK(c, launch_shard_ghosts(c->st, sweep_dev(c), g));
+  return NNGP_OK;
+}
+
+static int enqueue_shard_allgather(nngp_ctx* c, int col) {
+  const ShardPlan& P = c->sp;
+  if (P.G == 1) return NNGP_OK;
+  const size_t cnt = (size_t)P.cnt[col] * c->C * 2;  // doubles per rank
+  double* base = reinterpret_cast<double*>(c->xbuf_d + (size_t)P.xoff[col] * c->C);
+  ncclResult_t e = ncclAllGather(base + (size_t)P.rank * cnt, base, cnt, ncclDouble, c->comm, c->st);
+  if (e != ncclSuccess) return fail_msg(c, NNGP_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(e));
+  return NNGP_OK;
+}
+
+static int shard_call(nngp_ctx* c, int n_sweeps, int mask) {
+  if (c->sp.G > 1 && !c->comm)
+    return fail_msg(c, NNGP_ERR_STATE, "sharded sweep: no communicator (nngp_shard_comm_init) -- or use nngp_sweep_chains_group");
+  int rc;
+  if ((rc = enqueue_sweep_body(c, n_sweeps, mask, nullptr, kPrologue))) return rc;
+  for (int s = 0; s < n_sweeps; ++s)
+    for (int col = 0; col < c->sp.K; ++col) {
+      if ((rc = enqueue_shard_own(c, s, col, mask, n_sweeps))) return rc;
+      if ((rc = enqueue_shard_allgather(c, col))) return rc;
+      if ((rc = enqueue_shard_ghosts(c, col, mask))) return rc;
+    }
+  if ((rc = enqueue_sweep_body(c, n_sweeps, mask, nullptr, kEpilogue))) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  return NNGP_OK;
+}
+
+int nngp_shard_unique_id(unsigned char* id, int len) {
+  if (!id || len < (int)sizeof(ncclUniqueId))
+    return fail_msg(nullptr, NNGP_ERR_ARG, "shard_unique_id: need a buffer of NNGP_SHARD_ID_BYTES");
+  ncclUniqueId u;
+  ncclResult_t e = ncclGetUniqueId(&u);
+  if (e != ncclSuccess) return fail_msg(nullptr, NNGP_ERR_COMM, std::string("ncclGetUniqueId: ") + ncclGetErrorString(e));
+  std::memcpy(id, &u, sizeof u);
+  return NNGP_OK;
+}
+
+int nngp_shard_comm_init(nngp_ctx* c, const unsigned char* id, int len) {
+  if (!c || !id || len < (int)sizeof(ncclUniqueId)) return NNGP_ERR_ARG;
+  if (!c->shard) return fail_msg(c, NNGP_ERR_STATE, "shard_comm_init: not a shard context (nngp_ctx_create_shard)");
+  if (c->comm) return fail_msg(c, NNGP_ERR_STATE, "shard_comm_init: communicator already initialised");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof u);
+  ncclResult_t e = ncclCommInitRank(&c->comm, c->sp.G, u, c->sp.rank);
+  if (e != ncclSuccess) {
+    c->comm = nullptr;
+    return fail_msg(c, NNGP_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(e));
+  }
+  return NNGP_OK;
+}
+
+int nngp_sweep_chains_group(nngp_ctx** ctxs, int G, int n_sweeps, const double* beta0, const double* log_scale,
+                            const double* lnv, const uint64_t* seed, const uint64_t* counter_base) {
+  if (!ctxs || G < 1 || n_sweeps < 0 || !beta0 || !log_scale || !lnv || !seed || !counter_base) return NNGP_ERR_ARG;
+  for (int g = 0; g < G; ++g) {
+    nngp_ctx* c = ctxs[g];
+    if (!c || !c->shard || c->sp.G != G || c->sp.rank != g || c->n != ctxs[0]->n || c->C != ctxs[0]->C ||
+        c->sp.K != ctxs[0]->sp.K)
+      return fail_msg(c, NNGP_ERR_ARG, "sweep_chains_group: ctxs[g] must be rank g of a G-rank shard of one graph");
+  }
+  if (n_sweeps == 0) return NNGP_OK;
+  int rc;
+  const int mask = (1 << ctxs[0]->C) - 1;
+  for (int g = 0; g < G; ++g) {
+    nngp_ctx* c = ctxs[g];
+    if ((rc = set_device(c))) return rc;
+    for (int k = 0; k < c->C; ++k)
+      if ((rc = sweep_prepare(c, k, beta0[k], log_scale[k], lnv[k], seed[k], counter_base[k]))) return rc;
+    if ((rc = upload_scalars(c))) return rc;
+    if ((rc = enqueue_sweep_body(c, n_sweeps, mask, nullptr, kPrologue))) return rc;
+  }
+  // ev_own[g]: rank g's segment of the colour is written; ev_done[g]: rank g
+  // has copied the others' segments (nobody rewrites a segment before every
+  // rank has read it)
+  std::vector<hipEvent_t> ev_own(G), ev_done(G);
+  auto cleanup = [&] {
+    for (auto e : ev_own) if (e) hipEventDestroy(e);
+    for (auto e : ev_done) if (e) hipEventDestroy(e);
+  };
+  for (int g = 0; g < G; ++g) {
+    set_device(ctxs[g]);
+    if (hipEventCreateWithFlags(&ev_own[g], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ev_done[g], hipEventDisableTiming) != hipSuccess) {
+      cleanup();
+      return fail_msg(ctxs[g], NNGP_ERR_HIP, "sweep_chains_group: hipEventCreate");
+    }
+  }
+#define GCHK(c, x)                                                   \
+  do {                                                               \
+    hipError_t e_ = (x);                                             \
+    if (e_ != hipSuccess) { cleanup(); return fail_hip((c), e_, #x); } \
+  } while (0)
+  const ShardPlan& P0 = ctxs[0]->sp;
+  for (int s = 0; s < n_sweeps; ++s)
+    for (int col = 0; col < P0.K; ++col) {
+      for (int g = 0; g < G; ++g) {
+        nngp_ctx* c = ctxs[g];
+        set_device(c);
+        if (s + col > 0)
+          for (int h = 0; h < G; ++h) GCHK(c, hipStreamWaitEvent(c->st, ev_done[h], 0));
+        if ((rc = enqueue_shard_own(c, s, col, mask, n_sweeps))) { cleanup(); return rc; }
+        GCHK(c, hipEventRecord(ev_own[g], c->st));
+      }
+      const size_t seg = (size_t)P0.cnt[col] * ctxs[0]->C;
+      for (int g = 0; g < G; ++g) {
+        nngp_ctx* c = ctxs[g];
+        set_device(c);
+        for (int h = 0; h < G; ++h) {
+          if (h == g) continue;
+          GCHK(c, hipStreamWaitEvent(c->st, ev_own[h], 0));
+          const size_t off = (size_t)P0.xoff[col] * c->C + (size_t)h * seg;
+          GCHK(c, hipMemcpyAsync(c->xbuf_d + off, ctxs[h]->xbuf_d + off, seg * sizeof(double2), hipMemcpyDefault,
+                                 c->st));
+        }
+        GCHK(c, hipEventRecord(ev_done[g], c->st));
+        if ((rc = enqueue_shard_ghosts(c, col, mask))) { cleanup(); return rc; }
+      }
+    }
+#undef GCHK
+  for (int g = 0; g < G; ++g) {
+    nngp_ctx* c = ctxs[g];
+    set_device(c);
+    if ((rc = enqueue_sweep_body(c, n_sweeps, mask, nullptr, kEpilogue))) { cleanup(); return rc; }
+  }
+  for (int g = 0; g < G; ++g) {
+    set_device(ctxs[g]);
+    hipError_t e = hipStreamSynchronize(ctxs[g]->st);
+    if (e != hipSuccess) { cleanup(); return fail_hip(ctxs[g], e, "hipStreamSynchronize"); }
+  }
+  cleanup();
+  return NNGP_OK;
+}
+
 int nngp_sweep_timed(nngp_ctx* c, int n_sweeps, const double* beta0, const double* log_scale,
                      const double* lnv, const uint64_t* seed, const uint64_t* counter_base, double* ms,
                      double* kernel_ms) {
   if (!c || n_sweeps < 1 || !ms || !beta0 || !log_scale || !lnv || !seed || !counter_base) return NNGP_ERR_ARG;
+  if (c->shard) return fail_msg(c, NNGP_ERR_STATE, "sweep_timed: not available on shard contexts");
   int rc;
   if ((rc = set_device(c))) return rc;
   for (int k = 0; k < c->C; ++k)

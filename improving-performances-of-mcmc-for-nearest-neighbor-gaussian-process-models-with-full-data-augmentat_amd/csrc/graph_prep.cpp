@@ -618,6 +618,90 @@ bool build_tile_layout(const int* nn, int n, int b, const int* colors, const dou
   return true;
 }
 
+// ---------------------------------------------------------------- shard plan
+bool build_shard_plan(const int* nn, int n, int b, const int* colors, const SweepLayout& L, int G, int rank,
+                      ShardPlan& P, std::string& err) {
+  P = ShardPlan();
+  if (G < 1 || G > kMaxRanks || rank < 0 || rank >= G) { err = "shard plan: need 1 <= G <= 64, 0 <= rank < G"; return false; }
+  if (L.nchunks == 0 || (int)L.compact_loc.size() != n) { err = "shard plan: needs the colour-launch layout"; return false; }
+  const int K = L.K;
+  P.G = G; P.rank = rank; P.K = K;
+  // chunk -> rank by the Morton rank of its first slot (monotone inside a colour)
+  P.cb.assign((size_t)K * (G + 1), 0);
+  P.seg0.assign((size_t)K * (G + 1), 0);
+  P.cnt.assign(K, 0);
+  P.xoff.assign(K + 1, 0);
+  std::vector<int> owner(n, 0);  // compact slot -> rank
+  for (int c = 0; c < K; ++c) {
+    const int ch0 = L.color_chunk_ptr[c], ch1 = L.color_chunk_ptr[c + 1];
+    int* cb = &P.cb[(size_t)c * (G + 1)];
+    int* sg = &P.seg0[(size_t)c * (G + 1)];
+    int ch = ch0;
+    for (int g = 0; g < G; ++g) {
+      cb[g] = ch;
+      const long long hi = (long long)(g + 1) * n / G;  // Morton ranks of rank g: [g*n/G, hi)
+      while (ch < ch1 && (g == G - 1 || L.rpos[L.compact_loc[L.chunk_first[ch]]] < hi)) ++ch;
+    }
+    cb[G] = ch1;
+    for (int g = 0; g <= G; ++g) sg[g] = L.chunk_first[cb[g]];
+    for (int g = 0; g < G; ++g) {
+      P.cnt[c] = std::max(P.cnt[c], sg[g + 1] - sg[g]);
+      for (int x = sg[g]; x < sg[g + 1]; ++x) owner[x] = g;
+    }
+    P.cnt[c] = std::max(P.cnt[c], 1);
+    P.xoff[c + 1] = P.xoff[c] + (long long)G * P.cnt[c];
+    P.owned += sg[rank + 1] - sg[rank];
+  }
+  std::vector<int> loc_rank(n), col_of(n);
+  for (int x = 0; x < n; ++x) loc_rank[L.compact_loc[x]] = x;
+  for (int c = 0; c < K; ++c)
+    for (int x = L.color_loc_ptr[c]; x < L.color_loc_ptr[c + 1]; ++x) col_of[x] = c;
+  // ghost cells: rows (Morton order) with an owned member; their foreign members
+  std::vector<int> perm(n);
+  for (int i = 0; i < n; ++i) perm[L.rpos[i]] = i;
+  std::vector<std::vector<int>> gh(K);  // per colour: triples (row, src, recv)
+  for (int r = 0; r < n; ++r) {
+    const int k = perm[r];
+    bool need = false;
+    for (int t = 0; t < b && !need; ++t) {
+      const int j = nn[(size_t)k * b + t];
+      need = j >= 0 && owner[loc_rank[j]] == rank;
+    }
+    if (!need) continue;
+    ++P.needed_rows;
+    for (int t = 0; t < b; ++t) {
+      const int j = nn[(size_t)k * b + t];
+      if (j < 0) continue;
+      const int x = loc_rank[j], h = owner[x];
+      if (h == rank) continue;
+      const int c = col_of[x];
+      if (colors[j] - 1 != c) { err = "shard plan: colouring and layout disagree"; return false; }
+      gh[c].insert(gh[c].end(), {r, r * b + t, h * P.cnt[c] + (x - P.seg0[(size_t)c * (G + 1) + h])});
+    }
+  }
+  P.gptr.assign(K + 1, 0);
+  for (int c = 0; c < K; ++c) {
+    for (size_t g = 0; g < gh[c].size(); g += 3) {
+      P.grow.push_back(gh[c][g]);
+      P.gsrc.push_back(gh[c][g + 1]);
+      P.grecv.push_back(gh[c][g + 2]);
+    }
+    P.gptr[c + 1] = (int)P.grow.size();
+  }
+  // normal pairs with an owned member, in the order of the full layout
+  P.pair_ptr.assign(K + 1, 0);
+  for (int c = 0; c < K; ++c) {
+    for (int x = L.color_loc_ptr[c]; x < L.color_loc_ptr[c + 1]; ++x) {
+      const int i = L.compact_loc[x];
+      if (i & 1) continue;
+      const bool mine = owner[x] == rank || (i + 1 < n && owner[loc_rank[i + 1]] == rank);
+      if (mine) P.pairs.push_back(i >> 1);
+    }
+    P.pair_ptr[c + 1] = (int)P.pairs.size();
+  }
+  return true;
+}
+
 void dag_levels(const int* nn, int n, int b, std::vector<int>& level_ptr, std::vector<int>& level_rows) {
   std::vector<int> lev(n, 0);
   int maxl = 0;

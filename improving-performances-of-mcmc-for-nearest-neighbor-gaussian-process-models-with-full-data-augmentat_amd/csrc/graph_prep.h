@@ -129,6 +129,44 @@ struct TileLayout {
 bool build_tile_layout(const int* nn_rowmajor, int n, int b, const int* colors, const double* locs_colmajor,
                        int d, int T, int NT, int RMAX, TileLayout& L, std::string& err);
 
+// Colour-sharded sweep over G ranks on top of a
+// SweepLayout (every rank builds the same layout from the same inputs):
+//  - rank g owns, in every colour c, the chunks whose first slot has a Morton
+//    rank in [g*n/G, (g+1)*n/G): a contiguous chunk range, hence a contiguous
+//    compact range [seg0[c][g], seg0[c][g+1]) of the colour's slots -- the
+//    same spatial block of the domain in every colour;
+//  - exchange region of colour c: G x cnt[c] slots (cnt = the largest rank
+//    segment of the colour), slot units; rank g's segment starts at g*cnt[c];
+//    after colour c every rank holds {dw, w_new} of every slot of the colour
+//    (one all-gather);
+//  - ghost cells of colour c: (device row k, Linv index of B[k,j], exchange
+//    index of j) for every row k the rank's own columns touch (any colour) and
+//    every foreign member j of colour c of that row: r_k += B[k,j] dw_j.  A
+//    row has at most one member per colour, so own and ghost updates of a
+//    colour never touch the same row;
+//  - pairs of colour c: normal pairs (2p, 2p+1) generated by the colour of 2p
+//    with at least one member owned by the rank.
+constexpr int kMaxRanks = 64;
+
+struct ShardPlan {
+  int G = 1, rank = 0, K = 0;
+  std::vector<int> cb;          // K x (G+1): chunk boundaries of the ranks inside each colour
+  std::vector<int> seg0;        // K x (G+1): compact boundaries of the ranks inside each colour
+  std::vector<int> cnt;         // K: all-gather count of each colour (slots per rank, padded)
+  std::vector<long long> xoff;  // K+1: exchange region of each colour (slot units)
+  std::vector<int> gptr;        // K+1: ghost cells of each colour
+  std::vector<int> grow;        // device row of each ghost cell
+  std::vector<int> gsrc;        // device Linv index (row-major n x b) of B[k, j]
+  std::vector<int> grecv;       // exchange index of j (slot units, relative to xoff[c])
+  std::vector<int> pair_ptr;    // K+1
+  std::vector<int> pairs;       // normal pairs of the rank, grouped by the colour of 2p
+  long long owned = 0;          // slots owned by the rank
+  long long needed_rows = 0;    // rows of B the rank's columns touch
+};
+
+bool build_shard_plan(const int* nn_rowmajor, int n, int b, const int* colors, const SweepLayout& L, int G,
+                      int rank, ShardPlan& P, std::string& err);
+
 // Level sets of the Vecchia DAG for the sparse triangular solve:
 // level(i) = 1 + max level(NN(i)), level 0 rows have no neighbours.
 void dag_levels(const int* nn_rowmajor, int n, int b, std::vector<int>& level_ptr,

@@ -59,7 +59,25 @@ struct ColorLaunch {
   const int* pairs;           // pair ids whose normals this colour generates
   int npairs;
   int n;
+  double2* xsend = nullptr;   // sharded sweep: {dw, w_new} of compact slot x at xsend[(x - xs0)*C + chain]
+  int xs0 = 0;                //   (nullptr: single rank)
 };
+
+// colour-sharded sweep (graph_prep.h ShardPlan): after the exchange of colour
+// c, apply the ghost cells r[row] += B[k,j] dw_j and the replica updates
+// w_slot[x] = w_new of the foreign slots of the colour, for the chains in mask
+struct ShardGhostLaunch {
+  const int* grow;            // ghost cells of the colour (g0 .. g0+ng)
+  const int* grecv;
+  const double* gval;         // C x ng_total, chain-planar
+  long long ng_total;
+  int g0, ng;
+  const double2* xbuf;        // exchange region of the colour: slot*C + chain
+  int G, rank, cnt;
+  int seg0[65];               // compact boundaries of the ranks inside the colour
+  int chain_mask;
+};
+hipError_t launch_shard_ghosts(hipStream_t st, const SweepDev& L, const ShardGhostLaunch& a);
 
 // coordinate transform into the isotropic unit-range space (per covfun)
 hipError_t launch_scale_coords(hipStream_t st, int covfun, const double* cp, int ncp,

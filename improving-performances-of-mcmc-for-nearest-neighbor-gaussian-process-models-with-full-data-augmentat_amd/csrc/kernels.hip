@@ -970,8 +970,11 @@ __global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, ColorLaunc
         acc += cells[l1 * kCellStride + fe % kSweepRows];
       }
       const double wn = (cR[u] - inv_s2 * acc) * invP[u] + zs[u];
-      dws[t] = wn - w[u];
+      const double dw = wn - w[u];
+      dws[t] = dw;
       __builtin_nontemporal_store(wn, L.w_slot + ((size_t)x0 + t) * C + chain);
+      // sharded sweep: publish {dw, w_new} into this rank's exchange segment
+      if (a.xsend) a.xsend[((size_t)x0 + t - a.xs0) * C + chain] = make_double2(dw, wn);
     }
   }
   wave_lds_sync();
@@ -979,7 +982,8 @@ __global__ __launch_bounds__(256) void sweep_color_kernel(SweepDev L, ColorLaunc
 #pragma unroll
   for (int j = 0; j < kSweepRows; ++j) {
     const int p = pk[j] & kPkPadRow;
-    if (p != kPkPadRow) r[(size_t)p * C + chain] = rv[j] + v[j] * dws[q[j]];
+    // explicit fma: the ghost cells of the sharded sweep round identically
+    if (p != kPkPadRow) r[(size_t)p * C + chain] = __builtin_fma(v[j], dws[q[j]], rv[j]);
   }
   STAMP(5);
   if (PROBE == 9 && l == 0 && chain == 0) {
@@ -1006,6 +1010,42 @@ hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, const ColorLaun
     case 16: hipLaunchKernelGGL((sweep_color_kernel<16>), dim3(gs + gz), dim3(kBlock), 0, st, L, a); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ A1 (sharded)
+// After colour c's exchange: workgroups [0, gb) apply the ghost cells (one
+// thread per (cell, chain): r[row] += B[k,j] dw_j; rows are distinct inside a
+// colour, so no atomics), workgroups [gb, ...) copy w_new of the other ranks'
+// slots into the w replica.  Both read the exchange region only.
+__global__ __launch_bounds__(256) void shard_ghost_kernel(SweepDev L, ShardGhostLaunch a, int gb) {
+  const int C = L.C;
+  if ((int)blockIdx.x < gb) {
+    const long long it = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (it >= (long long)a.ng * C) return;
+    const int e = a.g0 + (int)(it / C), chain = (int)(it % C);
+    if (!((a.chain_mask >> chain) & 1)) return;
+    const double v = __builtin_nontemporal_load(a.gval + (size_t)chain * a.ng_total + e);
+    const double dw = a.xbuf[(size_t)__builtin_nontemporal_load(a.grecv + e) * C + chain].x;
+    double* rp = L.r + (size_t)__builtin_nontemporal_load(a.grow + e) * C + chain;
+    *rp = __builtin_fma(v, dw, *rp);
+    return;
+  }
+  const long long it = (long long)(blockIdx.x - gb) * 256 + threadIdx.x;
+  if (it >= (long long)a.G * a.cnt * C) return;
+  const int s = (int)(it / C), chain = (int)(it % C);
+  const int h = s / a.cnt, off = s % a.cnt;
+  if (h == a.rank || !((a.chain_mask >> chain) & 1)) return;
+  const int x = a.seg0[h] + off;
+  if (x >= a.seg0[h + 1]) return;
+  L.w_slot[(size_t)x * C + chain] = a.xbuf[(size_t)s * C + chain].y;
+}
+
+hipError_t launch_shard_ghosts(hipStream_t st, const SweepDev& L, const ShardGhostLaunch& a) {
+  const int gb = (int)(((long long)a.ng * L.C + 255) / 256);
+  const int wb = a.G > 1 ? (int)(((long long)a.G * a.cnt * L.C + 255) / 256) : 0;
+  if (gb + wb == 0) return hipSuccess;
+  hipLaunchKernelGGL(shard_ghost_kernel, dim3(gb + wb), dim3(kBlock), 0, st, L, a, gb);
   return hipGetLastError();
 }
 

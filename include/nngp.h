@@ -49,7 +49,8 @@
 extern "C" {
 #endif
 
-#define NNGP_ABI_VERSION 3
+#define NNGP_ABI_VERSION 4
+#define NNGP_SHARD_ID_BYTES 128 /* RCCL unique id */
 
 typedef enum {
   NNGP_OK = 0,
@@ -94,7 +95,12 @@ typedef struct {
   int sweep_engine;  /* 0: one launch per colour, 1: tile-resident persistent sweep */
   int n_tiles;       /* tiles (persistent workgroups) of the tile engine */
   int tile_rows_max; /* max local rows (own + foreign) of a tile: its LDS-resident r */
-  long long n_ghost_cells; /* foreign-member cells the tiles apply after a hand-off */
+  long long n_ghost_cells; /* foreign-member cells the tiles (or shard ranks) apply after a hand-off */
+  int n_ranks;       /* shard contexts: ranks of the colour-sharded sweep (0: not sharded) */
+  int rank;          /* shard contexts: this context's rank */
+  long long shard_owned;          /* locations swept by this rank */
+  long long shard_needed_rows;    /* rows of B its columns touch (its r halo included) */
+  long long shard_exchange_slots; /* slots of all colours' exchange regions (padded) */
 } nngp_info;
 
 /* ---------- library ---------- */
@@ -182,6 +188,32 @@ int nngp_sum_squared_residuals(nngp_ctx* ctx, double beta0, double* ssr);
 int nngp_spmv(nngp_ctx* ctx, int which, const double* X, int ncols, double* Y);
 /* x = B^{-1} u (host buffers, length n) */
 int nngp_tri_solve(nngp_ctx* ctx, int which, const double* u, double* x);
+
+/* ---------- colour-sharded sweep (multi-GPU) ----------
+ * The chromatic sweep of ONE set of chains split over n_ranks contexts (one
+ * per GPU, one process per GPU): rank g sweeps its spatial block of every
+ * colour class, and after each colour the ranks all-gather {dw, w_new} of the
+ * colour's locations (RCCL over xGMI) and apply the updates that cross their
+ * block boundary.  Results are bitwise identical to n_ranks = 1.  A shard
+ * context supports every entry point above (factor, loglik, field, ... are
+ * computed redundantly on every rank) except nngp_sweep with injected
+ * normals and nngp_sweep_timed; nngp_sweep / nngp_sweep_chains run the sharded
+ * sweep (n_ranks > 1: after nngp_shard_comm_init).  Replaces the per-colour
+ * masked update of update_Gaussian.R:261-275 across devices. */
+int nngp_ctx_create_shard(const double* locs, int n, int d, const int* NNarray, int b,
+                          const int* coloring, const int* locs_match,
+                          const double* observed_field, int n_obs, int n_chains, int device,
+                          int n_ranks, int rank, nngp_ctx** out);
+/* rank 0 creates the id (len >= NNGP_SHARD_ID_BYTES) and sends it to the
+ * other ranks out of band (e.g. torch.distributed broadcast) */
+int nngp_shard_unique_id(unsigned char* id, int len);
+/* collective over the n_ranks contexts: RCCL communicator of the shard */
+int nngp_shard_comm_init(nngp_ctx* ctx, const unsigned char* id, int len);
+/* all n_ranks shard contexts in ONE process (ctxs[g] = rank g; any devices):
+ * nngp_sweep_chains with the exchange done by device copies between them */
+int nngp_sweep_chains_group(nngp_ctx** ctxs, int n_ranks, int n_sweeps, const double* beta0,
+                            const double* log_scale, const double* log_noise_variance,
+                            const uint64_t* seed, const uint64_t* counter_base);
 
 /* ---------- measurement ---------- */
 /* nngp_sweep_chains bracketed by HIP events on the context's stream;

@@ -20,7 +20,7 @@ def test_header_symbols_exported(P):
     lib = C.CDLL(str(_lib.LIB_PATH))
     for s in sorted(declared):
         assert hasattr(lib, s), s
-    assert P.lib.nngp_abi_version() == 3
+    assert P.lib.nngp_abi_version() == 4
 
 
 def test_library_has_gfx950_code_object():
@@ -159,4 +159,23 @@ def test_tile_sweep_emulation(tile_check_exe, n, m, tiles, chains, seed, nt, rma
 
     out = subprocess.run([str(tile_check_exe), str(n), str(m), str(tiles), str(chains), str(seed), str(nt),
                           str(rmax)], capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
+
+
+@pytest.mark.parametrize("n,m,G,sweeps,seed", [(3000, 10, 2, 2, 1), (5000, 15, 3, 2, 2), (2000, 5, 8, 2, 3),
+                                               (50, 3, 4, 1, 4), (1, 0, 2, 1, 5), (20000, 15, 8, 1, 6),
+                                               (4000, 12, 1, 2, 7)])
+def test_shard_plan_emulation(tmp_path, n, m, G, sweeps, seed):
+    """C++ emulation of the colour-sharded sweep on its plan (graph_prep.cpp
+    build_shard_plan): G ranks with their own r and w replicas, own chunks,
+    exchange regions, ghost cells and replica updates reproduce the
+    single-rank sweep bitwise after every colour; the ranks' segments
+    partition every colour; normal pairs cover every owned location."""
+    import subprocess
+
+    csrc = next(ROOT.glob("*_amd")) / "csrc"
+    exe = tmp_path / "shard_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", str(csrc), str(ROOT / "tests/cpp/shard_check.cpp"),
+                    str(csrc / "graph_prep.cpp"), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe), str(n), str(m), str(G), str(sweeps), str(seed)], capture_output=True, text=True)
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr

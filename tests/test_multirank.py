@@ -56,3 +56,36 @@ def test_rank_workloads_differ():
     """Each rank draws its own synthetic field and chain seeds (bench.main)."""
     src = (ROOT / "bench.py").read_text()
     assert "seed=1000 + rank" in src and "77 + 10 * rank + k" in src
+
+
+def _bcast_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path.insert(0, str(ROOT))
+    import _pkgload
+
+    P = _pkgload.load()
+    import nngp_amd.shard as S
+
+    # the RCCL id needs a GPU; the bootstrap logic is what runs here
+    S.shard_unique_id = lambda: bytes(range(128)) if rank == 0 else bytes(128)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    q.put((rank, S.broadcast_unique_id(dist)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_shard_unique_id_broadcast_two_ranks():
+    """The colour-sharded path's communicator bootstrap: rank 0's RCCL id
+    reaches every rank over a gloo group (bench.py --shard)."""
+    world, port = 2, 29500 + os.getpid() % 1000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bcast_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert out[0] == out[1] == bytes(range(128))
