@@ -106,6 +106,8 @@ struct nngp_ctx {
   int* gsrc_d = nullptr;
   double* gval_d = nullptr;       // C x ghost cells
   int* gptr_d = nullptr;
+  int* gslot_d = nullptr;
+  int* gslot_ptr_d = nullptr;
   int* nb_ptr_d = nullptr;
   int* nb_d = nullptr;
   int* erow_ptr_d = nullptr;
@@ -206,6 +208,9 @@ TileDev tile_dev(nngp_ctx* c) {
   D.gval = c->gval_d;
   D.n_gcells = (long long)c->tl.gsrc.size();
   D.gptr = c->gptr_d;
+  D.gslot = c->gslot_d;
+  D.gslot_ptr = c->gslot_ptr_d;
+  D.max_gslots = c->tl.max_gslots;
   D.nb_ptr = c->nb_ptr_d;
   D.nb = c->nb_d;
   D.erow_ptr = c->erow_ptr_d;
@@ -334,7 +339,7 @@ void nngp_ctx_destroy(nngp_ctx* c) {
                              c->tmp2_d, c->partials_d, c->res_d, c->z_d, c->scal_d, c->dbg_d,
                              c->chunk_first_d, c->loc_rank_d, c->pairs_d, c->level_ptr_d, c->zbuf_d, c->ent_pos_d, c->start_mask_d,
                              c->dpos_d, c->perm_d, c->tb_d, c->tb_ptr_d, c->cell_pk_d, c->cell_src_d,
-                             c->cell_val_d, c->gcell_d, c->gsrc_d, c->gval_d, c->gptr_d, c->nb_ptr_d, c->nb_d,
+                             c->cell_val_d, c->gcell_d, c->gsrc_d, c->gval_d, c->gptr_d, c->gslot_d, c->gslot_ptr_d, c->nb_ptr_d, c->nb_d,
                              c->erow_ptr_d, c->erow_d, c->dwx_d, c->ctl_d, c->tdbg_d, c->sg_row_d,
                              c->sg_recv_d, c->sg_src_d, c->sg_val_d, c->xbuf_d, c->sp_pairs_d};
   if (c->comm) ncclCommDestroy(c->comm);
@@ -428,7 +433,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
         return fail_msg(nullptr, NNGP_ERR_ARG, "NNGP_TILE_NT must be 256, 512 or 1024");
       }
       bool ok = cus > 0 && build_tile_layout(nn.data(), n, b, coloring, locs, d, T, NT, tile_rmax(n_chains, NT), c->tl, terr);
-      const int need = ok ? tile_lds_bytes(c->tl.max_rows, n_chains, NT, c->tl.K, c->tl.max_batches) : 0;
+      const int need = ok ? tile_lds_bytes(c->tl.max_rows, n_chains, NT, c->tl.K, c->tl.max_batches, c->tl.max_gslots) : 0;
       if (ok && need > lds_max) {
         ok = false;
         terr = "tile layout needs " + std::to_string(need) +
@@ -545,6 +550,10 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     CK(dalloc(&c->gsrc_d, ng));
     CK(dalloc(&c->gval_d, ng * C));
     CK(dalloc(&c->gptr_d, TL.gptr.size()));
+    CK(dalloc(&c->gslot_d, TL.gslot.size()));
+    CK(dalloc(&c->gslot_ptr_d, TL.gslot_ptr.size()));
+    CK(upload(c->gslot_d, TL.gslot.data(), TL.gslot.size(), c->st));
+    CK(upload(c->gslot_ptr_d, TL.gslot_ptr.data(), TL.gslot_ptr.size(), c->st));
     CK(dalloc(&c->nb_ptr_d, TL.nb_ptr.size()));
     CK(dalloc(&c->nb_d, TL.nb.size()));
     CK(dalloc(&c->erow_ptr_d, TL.erow_ptr.size()));
@@ -994,7 +1003,8 @@ static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, int mask, const double*
     a.n_sweeps = n_sweeps;
     a.chain_mask = mask;
     a.z_in = z_dev;
-    HIPCHK(c, launch_sweep_tiles(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NT, c->tl.max_batches));
+    HIPCHK(c, launch_sweep_tiles(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NT, c->tl.max_batches,
+                                  c->tl.max_gslots));
     HIPCHK(c, hipMemcpyAsync(c->tmo_h, c->ctl_d + 1, sizeof(unsigned), hipMemcpyDeviceToHost, c->st));
   }
   if ((parts & kColours) && c->engine == 0) {

@@ -523,6 +523,8 @@ bool build_tile_layout(const int* nn, int n, int b, const int* colors, const dou
   L.slot_f0.assign(n, 0);
   L.batch_ptr.assign((size_t)T * K + 1, 0);
   L.gptr.assign((size_t)T * K + 1, 0);
+  L.gslot_ptr.assign((size_t)T * K + 1, 0);
+  std::vector<int> gidx(n, -1);  // slot -> index in the current (tile, colour)'s foreign slots
   L.nb_ptr.assign((size_t)T * K + 1, 0);
   L.erow_ptr.assign(T + 1, 0);
   std::vector<int> lr_of(n, -1);  // device row -> local row of the current tile
@@ -603,13 +605,19 @@ bool build_tile_layout(const int* nn, int n, int b, const int* colors, const dou
     }
     for (int c = 0; c < K; ++c) {
       const size_t pc = (size_t)t * K + c;
+      const int gs0 = (int)L.gslot.size();
       for (size_t g = 0; g < gh[c].size(); g += 3) {
+        const int x = gh[c][g + 1];
+        if (gidx[x] < 0) { gidx[x] = (int)L.gslot.size() - gs0; L.gslot.push_back(x); }
         L.gcell.push_back(gh[c][g]);
-        L.gcell.push_back(gh[c][g + 1]);
+        L.gcell.push_back(gidx[x]);
         L.gsrc.push_back(gh[c][g + 2]);
-        const int u = tile_of[L.compact_loc[gh[c][g + 1]]];
+        const int u = tile_of[L.compact_loc[x]];
         if (nbmark[u] != (int)pc) { nbmark[u] = (int)pc; L.nb.push_back(u); }
       }
+      for (size_t q = gs0; q < L.gslot.size(); ++q) gidx[L.gslot[q]] = -1;
+      L.gslot_ptr[pc + 1] = (int)L.gslot.size();
+      L.max_gslots = std::max(L.max_gslots, (int)L.gslot.size() - gs0);
       L.gptr[pc + 1] = (int)L.gsrc.size();
       L.nb_ptr[pc + 1] = (int)L.nb.size();
     }

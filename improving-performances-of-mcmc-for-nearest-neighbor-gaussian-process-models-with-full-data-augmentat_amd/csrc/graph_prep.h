@@ -89,8 +89,10 @@ bool build_sweep_layout(const int* nn_rowmajor, int n, int b, const int* colors,
 //    thread).  cell_pk = local row | q << 17 | start << 30 | end << 31
 //    (q = slot inside the batch; start/end: first/last cell of a slot);
 //    padding cells carry local row kTilePadRow and no flags;
-//  - ghost cells of (tile, colour): (local row k, slot x of a foreign member j
-//    of colour c): r_k += B[k,j] dw_j once j's owner has published dw_j;
+//  - foreign slots of (tile, colour): the distinct foreign members j of colour
+//    c of the tile's local rows (the tile reads each one's published dw_j once);
+//  - ghost cells of (tile, colour): (local row k, index of j in the foreign
+//    slots of (tile, colour)): r_k += B[k,j] dw_j once j's owner has published dw_j;
 //  - neighbours of (tile, colour): the owner tiles of those ghost slots.
 constexpr int kTileRowBits = 17;
 constexpr uint32_t kTilePadRow = (1u << kTileRowBits) - 1;
@@ -118,9 +120,12 @@ struct TileLayout {
   std::vector<int> batch_ptr;        // T*K + 1
   std::vector<uint32_t> cell_pk;     // own cells (padded batches)
   std::vector<int> cell_src;         // device Linv index rpos[k]*b + j, or -1 (padding)
-  std::vector<int> gcell;            // 2 per ghost cell: local row, slot of the foreign member
+  std::vector<int> gcell;            // 2 per ghost cell: local row, index of its foreign slot
   std::vector<int> gsrc;             // device Linv index of each ghost cell
   std::vector<int> gptr;             // T*K + 1
+  std::vector<int> gslot;            // foreign slots (slot index) of each (tile, colour)
+  std::vector<int> gslot_ptr;        // T*K + 1
+  int max_gslots = 0;                // max foreign slots of a (tile, colour)
   std::vector<int> nb_ptr, nb;       // T*K + 1, neighbour tiles of each (tile, colour)
 };
 

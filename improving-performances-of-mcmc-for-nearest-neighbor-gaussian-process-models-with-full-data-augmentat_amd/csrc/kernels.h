@@ -134,10 +134,12 @@ struct TileDev {
   const uint32_t* cell_pk;    // n_cells
   const double* cell_val;     // C x n_cells
   long long n_cells;
-  const int2* gcell;          // n_gcells: {local row, slot}
+  const int2* gcell;          // n_gcells: {local row, index of its foreign slot in the (tile, colour)}
   const double* gval;         // C x n_gcells
   long long n_gcells;
   const int* gptr;            // T*K+1
+  const int* gslot;           // foreign slots of each (tile, colour): slot index
+  const int* gslot_ptr;       // T*K+1
   const int* nb_ptr;          // T*K+1
   const int* nb;
   const int* erow_ptr;        // T+1
@@ -152,6 +154,7 @@ struct TileDev {
   unsigned* ctl;              // [0] call id (bumped on the device before every launch), [1] timeout word
   unsigned long long* dbg;    // NNGP_PROBE=9: per-tile phase times (4 x u64), else null
   int K, C, T, n;
+  int max_gslots;             // max foreign slots of a (tile, colour): LDS of their dw
 };
 
 struct TileLaunch {
@@ -160,7 +163,7 @@ struct TileLaunch {
   const double* z_in;         // injected normals, per sweep: slot x C (nullptr: Philox inline)
 };
 
-int tile_lds_bytes(int max_rows, int C, int NT, int K, int max_batches);
+int tile_lds_bytes(int max_rows, int C, int NT, int K, int max_batches, int max_gslots);
 // cells per thread of an own batch (the layout's RMAX): two batches of C
 // chains stay in registers (C >= 3: fewer cells per batch)
 // double-buffered batch registers (the next colour's loads in flight during
@@ -168,7 +171,7 @@ int tile_lds_bytes(int max_rows, int C, int NT, int K, int max_batches);
 constexpr int tile_double_buffer(int C) { return C <= 2 ? 1 : 0; }
 constexpr int tile_rmax(int C, int NT) { return 4096 / NT; }
 hipError_t launch_sweep_tiles(hipStream_t st, const TileDev& D, const TileLaunch& a, int max_rows, int NT,
-                              int max_batches);
+                              int max_batches, int max_gslots);
 // chain `chain`: cell/ghost values from Linv (device order) and precision_diag
 hipError_t launch_tile_refresh(hipStream_t st, const TileDev& D, int nbatches, int NT, const int* cell_src,
                                const int* gsrc, const double* linv, int chain);

@@ -1084,10 +1084,10 @@ constexpr int kTExported = 1 << 30;
 constexpr int kTSlots = 256;       // slots per own batch (graph_prep.h kTileSlotsMax)
 constexpr int kTSpreadLds = 82 * 1024;  // LDS floor: at most one tile per CU
 
-int tile_lds_bytes(int max_rows, int C, int NT, int K, int max_batches) {
+int tile_lds_bytes(int max_rows, int C, int NT, int K, int max_batches, int max_gslots) {
   const int rbytes = ((max_rows * C * 8 + 15) / 16) * 16;
-  return rbytes + kTSlots * C * 8 + (NT / 64) * C * 8 + 4 * C * 8 + max_batches * 16 + 2 * (K + 1) * 4 +
-         (NT / 64) * 4 + 64;
+  return rbytes + kTSlots * C * 8 + (NT / 64) * C * 8 + 4 * C * 8 + ((max_gslots * C + 1) / 2) * 16 +
+         max_batches * 16 + 3 * (K + 1) * 4 + (NT / 64) * 4 + 64;
 }
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
@@ -1203,6 +1203,8 @@ struct TileState {
   int4* batch_s;  // this tile's own batches
   int* bptr_s;    // K+1: batches of colour c = batch_s[bptr_s[c] .. bptr_s[c+1])
   int* gptr_s;    // K+1: ghost cells of colour c (global indices)
+  int* gsp_s;     // K+1: foreign slots of colour c (global indices into gslot)
+  double* gdw_s;  // foreign slots x C: their dw of the current colour
   int* wflag;
   __amdgpu_buffer_rsrc_t gran;
   unsigned call;
@@ -1364,6 +1366,10 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
   const int bfirst = S.bptr_s[c], bend = S.bptr_s[c + 1];
   const int g0 = S.gptr_s[c], g1 = S.gptr_s[c + 1];
   const int gn0 = S.gptr_s[cn], gn1 = S.gptr_s[cn + 1];
+  // this colour's foreign slots (one granule per slot and chain): the first
+  // NT items' slot indices load now, behind the own work
+  const int gs0 = S.gsp_s[c], nfi = (S.gsp_s[c + 1] - gs0) * C;
+  const int gsl_pref = t < nfi ? D.gslot[gs0 + t / C] : 0;
   if (DB) {
     // the next colour's first batch and first ghost chunk: their HBM stream
     // overlaps this colour's work (two register sets)
@@ -1387,41 +1393,40 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
   // ---- 2. the next batch is prepared while the neighbours publish colour c
   if (more) tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, sn, nxt, t);
   TSTAMP(S, 5);
-  // ---- 3. ghosts: poll each granule until it carries this epoch
+  // ---- 3. hand-off: poll the granule of each (foreign slot, chain) of this
+  // colour until it carries this epoch -> gdw_s; then every ghost cell adds
+  // B[k,j] dw_j to its local row (a slot read by several rows of the tile is
+  // fetched once)
+  for (int u0 = 0; u0 < nfi; u0 += NT) {
+    const int u = u0 + t;
+    if (u < nfi) {
+      const int x = u0 == 0 ? gsl_pref : D.gslot[gs0 + u / C];
+      const int ch = u % C;
+      double dw = 0.0;
+      for (unsigned spins = 0;; ++spins) {
+        const u32x4_t g = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)x * C + ch) * 16), 0, 16);
+        if (g.z == epoch && g.w == S.call) {
+          dw = __builtin_bit_cast(double, (unsigned long long)g.x | ((unsigned long long)g.y << 32));
+          break;
+        }
+        if (S.timed_out || spins > (1u << 20)) {
+          if (!S.timed_out) __hip_atomic_store(S.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          S.timed_out = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      S.gdw_s[u] = dw;
+    }
+  }
+  __syncthreads();
   for (int gb = g0; gb < g1; gb += NT * GMAX) {
     if (gb != g0) tile_load_ghosts<C, NT, GMAX>(D, gb, g1, gr, t);
-    double dw[GMAX][C];
-    unsigned pend = 0;
 #pragma unroll
     for (int k = 0; k < GMAX; ++k)
-      if (gr.lr[k] >= 0) pend |= ((1u << C) - 1) << (k * C);
-    for (unsigned spins = 0; pend; ++spins) {
+      if (gr.lr[k] >= 0)
 #pragma unroll
-      for (int k = 0; k < GMAX; ++k)
-#pragma unroll
-        for (int ch = 0; ch < C; ++ch) {
-          const unsigned bit = 1u << (k * C + ch);
-          if (pend & bit) {
-            const u32x4_t g = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gr.gx[k] * C + ch) * 16), 0, 16);
-            if (g.z == epoch && g.w == S.call) {
-              dw[k][ch] = __builtin_bit_cast(double, (unsigned long long)g.x | ((unsigned long long)g.y << 32));
-              pend &= ~bit;
-            }
-          }
-        }
-      if (!pend) break;
-      if (S.timed_out || spins > (1u << 20)) {
-        if (!S.timed_out) __hip_atomic_store(S.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        S.timed_out = true;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-#pragma unroll
-    for (int k = 0; k < GMAX; ++k)
-      if (gr.lr[k] >= 0 && !S.timed_out)
-#pragma unroll
-        for (int ch = 0; ch < C; ++ch) S.r_s[gr.lr[k] * C + ch] += gr.gv[k][ch] * dw[k][ch];
+        for (int ch = 0; ch < C; ++ch) S.r_s[gr.lr[k] * C + ch] += gr.gv[k][ch] * S.gdw_s[gr.gx[k] * C + ch];
   }
   __syncthreads();
   TSTAMP(S, 6);
@@ -1446,10 +1451,12 @@ __global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D, TileLaunch a
   S.wsum = S.acc_s + kTSlots * C;                // NW x C: segmented wave totals
   S.sc_s = S.wsum + NW * C;                      // C x {inv_s2, inv_t2}
   S.seed_s = reinterpret_cast<unsigned long long*>(S.sc_s + 2 * C);
-  S.batch_s = reinterpret_cast<int4*>(S.seed_s + 2 * C);
+  S.gdw_s = reinterpret_cast<double*>(S.seed_s + 2 * C);  // max foreign slots x C (even count)
+  S.batch_s = reinterpret_cast<int4*>(S.gdw_s + ((D.max_gslots * C + 1) / 2) * 2);
   S.bptr_s = reinterpret_cast<int*>(S.batch_s + nbt);
   S.gptr_s = S.bptr_s + K + 1;
-  S.wflag = S.gptr_s + K + 1;                    // NW: the wave holds a slot start
+  S.gsp_s = S.gptr_s + K + 1;
+  S.wflag = S.gsp_s + K + 1;                     // NW: the wave holds a slot start
   TSTAMP(S, -1);
   for (int lr = t; lr < nrows; lr += NT) {
     const size_t g = (size_t)D.erow[row0 + lr] * C;
@@ -1461,6 +1468,7 @@ __global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D, TileLaunch a
   for (int i = t; i <= K; i += NT) {
     S.bptr_s[i] = D.batch_ptr[T * K + i] - b_lo;
     S.gptr_s[i] = D.gptr[T * K + i];
+    S.gsp_s[i] = D.gslot_ptr[T * K + i];
   }
   if (t < C) {
     S.sc_s[2 * t] = D.scal[t].inv_s2;
@@ -1529,8 +1537,8 @@ static hipError_t launch_tiles_nt(hipStream_t st, const TileDev& D, const TileLa
 }
 
 hipError_t launch_sweep_tiles(hipStream_t st, const TileDev& D, const TileLaunch& a, int max_rows, int NT,
-                              int max_batches) {
-  const int lds = tile_lds_bytes(max_rows, D.C, NT, D.K, max_batches);
+                              int max_batches, int max_gslots) {
+  const int lds = tile_lds_bytes(max_rows, D.C, NT, D.K, max_batches, max_gslots);
   switch (NT) {
     case 256: return launch_tiles_nt<256>(st, D, a, lds);
     case 512: return launch_tiles_nt<512>(st, D, a, lds);

@@ -241,7 +241,9 @@ int main(int argc, char** argv) {
         const int pc = t * K + c;
         std::set<int> nbs(L.nb.begin() + L.nb_ptr[pc], L.nb.begin() + L.nb_ptr[pc + 1]);
         for (int gi = L.gptr[pc]; gi < L.gptr[pc + 1]; ++gi) {
-          const int lr = L.gcell[2 * gi], x = L.gcell[2 * gi + 1];
+          const int lr = L.gcell[2 * gi], gx = L.gcell[2 * gi + 1];
+          REQUIRE(gx >= 0 && gx < L.gslot_ptr[pc + 1] - L.gslot_ptr[pc] && gx < L.max_gslots);
+          const int x = L.gslot[L.gslot_ptr[pc] + gx];
           REQUIRE(L.slot_f0[x] & kSlotExported);
           REQUIRE(col[L.compact_loc[x]] == c + 1);
           // the owner of x is a listed neighbour
