@@ -562,8 +562,13 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     CK(dalloc(&c->ctl_d, 4));
     CK(hipHostMalloc((void**)&c->tmo_h, sizeof(unsigned), hipHostMallocDefault));
     *c->tmo_h = 0;
-    static_assert(sizeof(TileBatch) == sizeof(int4), "batch record");
-    CK(upload(c->tb_d, reinterpret_cast<const int4*>(TL.batch.data()), nb, c->st));
+    // device batch record {off, R | nthr << 16, nslots, slot0}
+    std::vector<int4> tb(nb);
+    for (size_t q = 0; q < nb; ++q) {
+      const TileBatch& B = TL.batch[q];
+      tb[q] = make_int4(B.off, B.R | (B.nthr << 16), B.nslots, B.slot0);
+    }
+    CK(hipMemcpy(c->tb_d, tb.data(), sizeof(int4) * nb, hipMemcpyHostToDevice));
     CK(upload(c->tb_ptr_d, TL.batch_ptr.data(), TL.batch_ptr.size(), c->st));
     CK(upload(c->cell_pk_d, TL.cell_pk.data(), ncell, c->st));
     CK(upload(c->cell_src_d, TL.cell_src.data(), ncell, c->st));

@@ -564,7 +564,7 @@ bool build_tile_layout(const int* nn, int n, int b, const int* colors, const dou
           ++ns;
         }
         const int R = std::max(1, (cells + NT - 1) / NT);
-        TileBatch tb{(int)L.cell_pk.size(), R, ns, x};
+        TileBatch tb{(int)L.cell_pk.size(), R, ns, x, (cells + R - 1) / R};
         if ((long long)L.cell_pk.size() + (long long)R * NT > INT32_MAX) { err = "tile layout: too many cells"; return false; }
         L.cell_pk.resize(L.cell_pk.size() + (size_t)R * NT, kTilePadRow);
         L.cell_src.resize(L.cell_pk.size(), -1);

@@ -103,7 +103,8 @@ constexpr uint32_t kCellEnd = 1u << 31;
 constexpr int kSlotExported = 1 << 30;  // slot_f0 flag: dw of the slot is read by other tiles
 constexpr int kTileSlotsMax = 256;      // slots per own batch
 
-struct TileBatch { int off, R, nslots, slot0; };
+// nthr = ceil(cells / R): threads holding cells (the others hold padding only)
+struct TileBatch { int off, R, nslots, slot0, nthr; };
 
 struct TileLayout {
   int n = 0, b = 0, K = 0, T = 0, NT = 0, RMAX = 0;

@@ -1115,10 +1115,11 @@ struct TileBatchRegs {
 
 template <int C, int NT, int RMAX>
 __device__ __forceinline__ void tile_load_batch(const TileDev& D, const int4 B, TileBatchRegs<C, NT, RMAX>& b, int t) {
-  b.R = B.y; b.ns = B.z; b.x0 = B.w;
+  b.R = B.y & 0xFFFF; b.ns = B.z; b.x0 = B.w;
+  const bool live = t < (B.y >> 16);  // threads past nthr hold padding only: no load
 #pragma unroll
   for (int j = 0; j < RMAX; ++j) {
-    if (j < b.R) {
+    if (j < b.R && live) {
       const long long e = B.x + (long long)j * NT + t;
       b.pk[j] = __builtin_nontemporal_load(D.cell_pk + e);
 #pragma unroll
@@ -1567,12 +1568,13 @@ __global__ __launch_bounds__(256) void tile_refresh_kernel(TileDev D, int nbatch
   }
   const int4 B = D.batch[blockIdx.x];  // refresh kernel: one batch per workgroup
   double* cv = const_cast<double*>(D.cell_val) + (size_t)chain * D.n_cells;
-  for (int e0 = t; e0 < B.y * NT; e0 += 256) {
+  const int R = B.y & 0xFFFF;
+  for (int e0 = t; e0 < R * NT; e0 += 256) {
     const long long e = B.x + e0;
     const int src = cell_src[e];
     const double v = src >= 0 ? linv[src] : 0.0;
     cv[e] = v;
-    const int f = (e0 % NT) * B.y + e0 / NT;  // e0 = j*NT + thread
+    const int f = (e0 % NT) * R + e0 / NT;  // e0 = j*NT + thread
     sq[f] = v * v;
     endf[f] = (D.cell_pk[e] & kTEnd) ? 1 : 0;
   }

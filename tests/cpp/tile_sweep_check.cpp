@@ -180,6 +180,10 @@ int main(int argc, char** argv) {
         for (int bi = L.batch_ptr[pc]; bi < L.batch_ptr[pc + 1]; ++bi) {
           const TileBatch B = L.batch[bi];
           REQUIRE(B.nslots <= NT && B.R <= RMAX);
+          // threads past nthr hold padding only (the kernel skips their loads)
+          REQUIRE(B.nthr >= 1 && B.nthr <= NT);
+          for (int j = 0; j < B.R; ++j)
+            for (int th = B.nthr; th < NT; ++th) REQUIRE(L.cell_pk[(size_t)B.off + (size_t)j * NT + th] == kTilePadRow);
           std::vector<double> pr((size_t)NT * RMAX * C), tails((size_t)NT * C), acc_s((size_t)NT * C, 0.0);
           std::vector<int> f0(NT, 0);
           for (int th = 0; th < B.nslots; ++th) f0[th] = L.slot_f0[B.slot0 + th] & 0xFFFFF;
