@@ -1225,6 +1225,30 @@ struct TileState {
     }                                                                     \
   } while (0)
 
+// DPP move of a double (both halves; lanes without a source read +0.0)
+template <int CTRL, int RM, bool BC>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, x);
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, RM, 0xF, BC);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, RM, 0xF, BC);
+  return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32));
+}
+
+// one step of a segmented inclusive scan (flag f = "a segment starts here or
+// in an earlier lane of my partial"): (f_e, v_e) (+) (f, v) = (f_e | f, f ? v : v_e + v)
+template <int CTRL, int RM, bool BC, int C>
+__device__ __forceinline__ void seg_scan_step(double (&v)[C], int& f) {
+  double e[C];
+#pragma unroll
+  for (int ch = 0; ch < C; ++ch) e[ch] = dpp_f64<CTRL, RM, BC>(v[ch]);
+  const int fe = __builtin_amdgcn_update_dpp(0, f, CTRL, RM, 0xF, BC);
+  if (!f) {
+#pragma unroll
+    for (int ch = 0; ch < C; ++ch) v[ch] = e[ch] + v[ch];
+  }
+  f |= fe;
+}
+
 // one own batch of colour c (epoch): products -> slot totals -> draws ->
 // scatter.  LDS and registers only, plus the draws' stores: no global load
 // (a load here would wait behind the next batch's prefetch, vmcnt is in order)
@@ -1272,24 +1296,18 @@ __device__ __forceinline__ void tile_own_batch(const TileDev& D, const TileLaunc
   TSTAMP(S, 1);
   // segmented inclusive scan of the thread tails (restart at threads holding
   // a slot start): in the wave by shuffles, across waves through LDS
+  // (DPP: row shifts 1, 2, 4, 8 inside each row of 16 lanes, then the row
+  // broadcasts 15 and 31 -- no LDS round trips)
   double v[C];
   int f = seen_start ? 1 : 0;
 #pragma unroll
   for (int ch = 0; ch < C; ++ch) v[ch] = run[ch];
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    double vu[C];
-#pragma unroll
-    for (int ch = 0; ch < C; ++ch) vu[ch] = __shfl_up(v[ch], d, 64);
-    const int fu = __shfl_up(f, d, 64);
-    if (lane >= d) {
-      if (!f) {
-#pragma unroll
-        for (int ch = 0; ch < C; ++ch) v[ch] = vu[ch] + v[ch];
-      }
-      f |= fu;
-    }
-  }
+  seg_scan_step<0x111, 0xF, true, C>(v, f);  // row_shr:1
+  seg_scan_step<0x112, 0xF, true, C>(v, f);  // row_shr:2
+  seg_scan_step<0x114, 0xF, true, C>(v, f);  // row_shr:4
+  seg_scan_step<0x118, 0xF, true, C>(v, f);  // row_shr:8
+  seg_scan_step<0x142, 0xA, false, C>(v, f); // row_bcast:15 -> rows 1, 3
+  seg_scan_step<0x143, 0xC, false, C>(v, f); // row_bcast:31 -> rows 2, 3
   if (lane == 63) {
 #pragma unroll
     for (int ch = 0; ch < C; ++ch) S.wsum[wv * C + ch] = v[ch];
@@ -1307,7 +1325,7 @@ __device__ __forceinline__ void tile_own_batch(const TileDev& D, const TileLaunc
 #pragma unroll
   for (int ch = 0; ch < C; ++ch) {
     const double Sv = f ? v[ch] : v[ch] + in[ch];
-    const double up = __shfl_up(Sv, 1, 64);
+    const double up = dpp_f64<0x138, 0xF, true>(Sv);  // wave_shr:1
     const double cp = lane ? up : in[ch];
     if (cont_q >= 0) acc_s[cont_q * C + ch] = cont[ch] + cp;
   }
