@@ -34,6 +34,7 @@ ABI_SYMBOLS = (
     "nngp_accept_field", "nngp_beta0_stats", "nngp_sum_squared_residuals", "nngp_spmv",
     "nngp_tri_solve", "nngp_sweep_timed", "nngp_device_normals",
     "nngp_ctx_create_shard", "nngp_shard_unique_id", "nngp_shard_comm_init", "nngp_sweep_chains_group",
+    "nngp_records_reserve", "nngp_record_field", "nngp_get_records",
 )
 SHARD_ID_BYTES = 128  # NNGP_SHARD_ID_BYTES
 
@@ -109,6 +110,9 @@ def _load():
     L.nngp_shard_unique_id.argtypes = [C.c_char_p, C.c_int]
     L.nngp_shard_comm_init.argtypes = [_vp, C.c_char_p, C.c_int]
     L.nngp_sweep_chains_group.argtypes = [C.POINTER(_vp), C.c_int, C.c_int, _dp, _dp, _dp, _up, _up]
+    L.nngp_records_reserve.argtypes = [_vp, C.c_int]
+    L.nngp_record_field.argtypes = [_vp, C.c_int]
+    L.nngp_get_records.argtypes = [_vp, C.c_int, C.c_int, _dp]
     return L
 
 

@@ -110,6 +110,19 @@ class ChainContext:
         self._chk(lib.nngp_get_field(self._h, out))
         return out
 
+    # ------------------------------------------------------------ records
+    def records_reserve(self, n_rows: int) -> None:
+        """Device buffer of n_rows recorded fields for the selected chain."""
+        self._chk(lib.nngp_records_reserve(self._h, int(n_rows)))
+
+    def record_field(self, row: int) -> None:
+        self._chk(lib.nngp_record_field(self._h, int(row)))
+
+    def get_records(self, row0: int, n_rows: int) -> np.ndarray:
+        out = np.zeros(int(n_rows) * self.n)
+        self._chk(lib.nngp_get_records(self._h, int(row0), int(n_rows), out))
+        return out.reshape(int(n_rows), self.n)
+
     def set_mu(self, mu, beta0: float) -> None:
         """mu = None means mu == beta_0 for every observation (no X)."""
         self._mu_keep = None if mu is None else f64(mu)

@@ -35,6 +35,8 @@ struct ChainState {
   double* field_d = nullptr;
   double* field_prop_d = nullptr;
   double* mu_d = nullptr;
+  double* rec_d = nullptr;  // on-device field records: rec_rows x n, location order
+  int rec_rows = 0;
   bool have_factor[2] = {false, false};
   bool have_field = false, have_mu = false, mu_is_const = true;
   double mu_beta0 = 0.0;
@@ -345,7 +347,7 @@ void nngp_ctx_destroy(nngp_ctx* c) {
   if (c->comm) ncclCommDestroy(c->comm);
   for (int k = 0; k < kMaxChains; ++k) {
     ChainState& s = c->ch[k];
-    ptrs.insert(ptrs.end(), {s.linv_d[0], s.linv_d[1], s.field_d, s.field_prop_d, s.mu_d});
+    ptrs.insert(ptrs.end(), {s.linv_d[0], s.linv_d[1], s.field_d, s.field_prop_d, s.mu_d, s.rec_d});
   }
   for (void* p : ptrs) if (p) hipFree(p);
   if (c->scal_h) hipHostFree(c->scal_h);
@@ -909,6 +911,53 @@ int nngp_get_field(nngp_ctx* c, double* field) {
   int rc;
   if ((rc = set_device(c))) return rc;
   return download_field(c, S.field_d, field);
+}
+
+// ---------------------------------------------------------------- records
+int nngp_records_reserve(nngp_ctx* c, int n_rows) {
+  if (!c || n_rows < 0) return NNGP_ERR_ARG;
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  ChainState& S = c->ch[c->cur];
+  if (n_rows == S.rec_rows && (S.rec_d || n_rows == 0)) return NNGP_OK;
+  if (S.rec_d) {
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    hipFree(S.rec_d);
+  }
+  S.rec_d = nullptr;
+  S.rec_rows = 0;
+  if (n_rows == 0) return NNGP_OK;
+  if (dalloc(&S.rec_d, (size_t)n_rows * c->n) != hipSuccess) {
+    hipGetLastError();
+    S.rec_d = nullptr;
+    return fail_msg(c, NNGP_ERR_NOMEM, "records_reserve: device allocation failed");
+  }
+  S.rec_rows = n_rows;
+  return NNGP_OK;
+}
+
+int nngp_record_field(nngp_ctx* c, int row) {
+  if (!c) return NNGP_ERR_ARG;
+  ChainState& S = c->ch[c->cur];
+  if (!S.rec_d || row < 0 || row >= S.rec_rows) return fail_msg(c, NNGP_ERR_ARG, "record_field: row out of the reserved records");
+  if (!S.have_field) return fail_msg(c, NNGP_ERR_STATE, "record_field: no field");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  // device row order -> location order, stays on the device (no host sync)
+  HIPCHK(c, launch_permute_gather(c->st, c->n, c->dpos_d, S.field_d, S.rec_d + (size_t)row * c->n));
+  return NNGP_OK;
+}
+
+int nngp_get_records(nngp_ctx* c, int row0, int n_rows, double* out) {
+  if (!c || !out || n_rows < 0) return NNGP_ERR_ARG;
+  ChainState& S = c->ch[c->cur];
+  if (row0 < 0 || row0 + n_rows > S.rec_rows) return fail_msg(c, NNGP_ERR_ARG, "get_records: rows out of the reserved records");
+  if (n_rows == 0) return NNGP_OK;
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  HIPCHK(c, hipMemcpy(out, S.rec_d + (size_t)row0 * c->n, sizeof(double) * (size_t)n_rows * c->n, hipMemcpyDeviceToHost));
+  return NNGP_OK;
 }
 
 int nngp_set_mu(nngp_ctx* c, const double* mu, double beta0) {

@@ -37,6 +37,7 @@ from __future__ import annotations
 
 import numpy as np
 
+from ._lib import NNGPError
 from .context import ChainContext, make_chain_views
 from .model import covparms
 
@@ -87,6 +88,15 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
         rec["beta"] = np.zeros((n_iterations_update, X["X"].shape[1]))
     acc_suf = np.zeros(n_iterations_update)
     acc_anc = np.zeros(n_iterations_update)
+    # recorded fields stay on the device until the end of the call
+    # (records$field, :56,311); host copies per iteration if HBM is short
+    n_rec = rec["field"].shape[0]
+    dev_rec = n_rec > 0
+    if dev_rec:
+        try:
+            ctx.records_reserve(n_rec)
+        except NNGPError:
+            dev_rec = False
 
     # Vecchia factor of the current state (:67-74)
     ctx.factor(0, covfun, covparms(sp_names, params["shape"]))
@@ -208,8 +218,14 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
         rec["log_scale"][it - 1] = params["log_scale"]
         rec["shape"][it - 1] = params["shape"]
         if round(it * field_thinning) == it * field_thinning:
-            rec["field"][int(it * field_thinning) - 1] = ctx.get_field()
+            if dev_rec:
+                ctx.record_field(int(it * field_thinning) - 1)
+            else:
+                rec["field"][int(it * field_thinning) - 1] = ctx.get_field()
 
+    if dev_rec:
+        rec["field"] = ctx.get_records(0, n_rec)
+        ctx.records_reserve(0)
     params["field"] = ctx.get_field()
     return {"state": {"params": params, "transition_kernels": tk}, "records": rec,
             "acceptance": {"covariance_acceptance_sufficient": acc_suf,

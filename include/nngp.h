@@ -36,6 +36,7 @@
  *   nngp_field_response_ratio  dnorm ratio, update_Gaussian.R:129-131
  *   nngp_beta0_stats ......... beta_0 Gibbs block, update_Gaussian.R:221-222
  *   nngp_sum_squared_residuals update_Gaussian.R:281
+ *   nngp_record_field ........ records$field[i, ] = field, update_Gaussian.R:305-311
  *   nngp_spmv / nngp_tri_solve sparse_chol %*% X (update_Gaussian.R:79,147) /
  *                              Matrix::solve (initialize.R:208, predict.R:46)
  */
@@ -49,7 +50,7 @@
 extern "C" {
 #endif
 
-#define NNGP_ABI_VERSION 4
+#define NNGP_ABI_VERSION 5
 #define NNGP_SHARD_ID_BYTES 128 /* RCCL unique id */
 
 typedef enum {
@@ -148,6 +149,15 @@ int nngp_get_field(nngp_ctx* ctx, double* field);
 /* mu (length n_obs): beta_0 + X beta; recomputes residuals_sum (A7).
  * mu == NULL means mu = beta0 for every observation. */
 int nngp_set_mu(nngp_ctx* ctx, const double* mu, double beta0);
+
+/* On-device field records (records$field, update_Gaussian.R:56,305-311 with
+ * field_thinning): the selected chain's device buffer of n_rows
+ * x n (location order); record_field copies the current field into row `row`
+ * without a host round trip; get_records copies rows [row0, row0+n_rows) out
+ * (row-major n_rows x n).  reserve(0) frees the buffer. */
+int nngp_records_reserve(nngp_ctx* ctx, int n_rows);
+int nngp_record_field(nngp_ctx* ctx, int row);
+int nngp_get_records(nngp_ctx* ctx, int row0, int n_rows, double* out);
 
 /* Vecchia log-likelihood (A6) of z = field - beta0 under factor `which` */
 int nngp_loglik(nngp_ctx* ctx, int which, double beta0, double log_scale, double* ll);

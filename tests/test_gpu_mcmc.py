@@ -138,3 +138,45 @@ def test_vignette_posterior_summaries(P, printed, toy):
         assert abs(mean - printed["fixed_effects"][theirs][0]) < 0.6 * sd + 0.6 * fe[ours][4], (ours, mean)
     for c in L["_contexts"]:
         c.close()
+
+
+def test_device_records_of_the_field(P):
+    """On-device records (records$field, update_Gaussian.R:305-311): rows hold
+    the field at record time in location order; reserve(0) frees; rows
+    outside the reservation are refused."""
+    locs, NN, col, lm, y = make_problem(P, 900, 6, seed=12)
+    rng = np.random.default_rng(0)
+    fields = [rng.normal(size=900) for _ in range(3)]
+    with P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=2) as ctx:
+        ctx.select(1)
+        ctx.records_reserve(3)
+        for r, f in enumerate(fields):
+            ctx.set_field(f)
+            ctx.record_field(r)
+        np.testing.assert_array_equal(ctx.get_records(0, 3), np.stack(fields))
+        np.testing.assert_array_equal(ctx.get_records(1, 1)[0], fields[1])
+        with pytest.raises(P.NNGPError):
+            ctx.record_field(3)
+        with pytest.raises(P.NNGPError):
+            ctx.select(0).record_field(0)  # chain 0 has no reservation
+        ctx.select(1).records_reserve(0)
+        with pytest.raises(P.NNGPError):
+            ctx.get_records(0, 1)
+
+
+def test_update_records_field_thinning(P, toy):
+    """records$field rows with field_thinning = 0.5: iterations 2, 4, ...; the
+    last row is the final state's field."""
+    from nngp_amd.update_gaussian import mcmc_nngp_update_Gaussian
+
+    L = P.mcmc_nngp_initialize(toy["locs"], toy["observed_field"], X_locs=toy["X"],
+                               stationary_covfun="exponential_isotropic", m=5, n_chains=1, seed=3)
+    out = mcmc_nngp_update_Gaussian(L["locs"], L["X"], L["observed_field"], L["space_time_model"],
+                                    L["vecchia_approx"], L["states"], 6, field_thinning=0.5, n_chromatic=2,
+                                    contexts=L["_contexts"], seed=1)
+    rec = out["chain_1"]["records"]["field"]
+    assert rec.shape == (3, L["vecchia_approx"]["n_locs"])
+    np.testing.assert_array_equal(rec[-1], out["chain_1"]["state"]["params"]["field"])
+    assert np.all(np.abs(rec).sum(axis=1) > 0)
+    for c in L["_contexts"]:
+        c.close()
