@@ -1656,46 +1656,52 @@ int launch_obs_reduce(hipStream_t st, int mode, int n_obs, const double* y, cons
 // Sparse triangular solve B x = u for up to 4 chains at once (same DAG, per
 // chain factor): work item = (row of the level, chain slot kk); u and x are
 // chain-strided (element d*stride + kidx[kk]).  One chain: stride 1.
-// b <= BMAX (ctx_create caps b at 32): the row's neighbour indices, then its
-// gathers, are all issued before the first use -- two memory round trips per
-// row instead of 2(b-1) -- and subtracted in neighbour order.
+// b <= BMAX (ctx_create caps b at 32).
+// 16 lanes per (row, chain) -- one DPP row: lane l takes neighbours j = l and
+// l + 16 (b <= 32), so a row's NNarray / Linv entries load as one or two
+// coalesced lines instead of b scattered ones; the products reduce by DPP
+// row shifts and lane 15 of the row writes x_i = (u_i - sum_j B[i,j] x_j) / B[i,i].
+// Every lane of a 16-lane row runs the same path (`active` is row-uniform).
 template <int BMAX>
-__device__ __forceinline__ void tri_row(const TriArgs& a, int i, int kk, const int* __restrict__ nn, int b,
-                                        const double* __restrict__ u, double* __restrict__ x) {
-  const double* lr = a.linv[kk] + (size_t)i * b;
-  const int* nr = nn + (size_t)i * b;
-  const int k = a.kidx[kk], S = a.stride;
-  double s = u[(size_t)i * S + k];
-  int idx[BMAX];
-  double xv[BMAX], lv[BMAX];
+__device__ __forceinline__ void tri_row16(const TriArgs& a, int i, int kk, int l, bool active,
+                                          const int* __restrict__ nn, int b, const double* __restrict__ u,
+                                          double* __restrict__ x) {
+  double p = 0.0;
+  const int k = active ? a.kidx[kk] : 0, S = a.stride;
+  const double* lr = active ? a.linv[kk] + (size_t)i * b : nullptr;
+  if (active) {
+    const int* nr = nn + (size_t)i * b;
 #pragma unroll
-  for (int j = 1; j < BMAX; ++j) idx[j] = j < b ? __builtin_nontemporal_load(nr + j) : -1;
-#pragma unroll
-  for (int j = 1; j < BMAX; ++j) {
-    xv[j] = idx[j] >= 0 ? x[(size_t)idx[j] * S + k] : 0.0;
-    lv[j] = idx[j] >= 0 ? lr[j] : 0.0;
+    for (int j = l; j < BMAX; j += 16) {
+      if (j >= 1 && j < b) {
+        const int idx = __builtin_nontemporal_load(nr + j);
+        if (idx >= 0) p = __builtin_fma(__builtin_nontemporal_load(lr + j), x[(size_t)idx * S + k], p);
+      }
+    }
   }
-#pragma unroll
-  for (int j = 1; j < BMAX; ++j)
-    if (idx[j] >= 0) s -= lv[j] * xv[j];
-  x[(size_t)i * S + k] = s / lr[0];
+  p += dpp_f64<0x111, 0xF, true>(p);  // row_shr:1
+  p += dpp_f64<0x112, 0xF, true>(p);  // row_shr:2
+  p += dpp_f64<0x114, 0xF, true>(p);  // row_shr:4
+  p += dpp_f64<0x118, 0xF, true>(p);  // row_shr:8 -> lane 15 holds the row sum
+  if (active && l == 15) x[(size_t)i * S + k] = (u[(size_t)i * S + k] - p) / lr[0];
 }
 
 template <int BMAX>
-__global__ void tri_level_kernel(TriArgs a, const int* __restrict__ rows, int nrows,
-                                 const int* __restrict__ nn, int b, const double* __restrict__ u,
-                                 double* __restrict__ x) {
-  int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nrows * a.nc) return;
-  tri_row<BMAX>(a, rows[t / a.nc], t % a.nc, nn, b, u, x);
+__global__ __launch_bounds__(256) void tri_level_kernel(TriArgs a, const int* __restrict__ rows, int nrows,
+                                                        const int* __restrict__ nn, int b,
+                                                        const double* __restrict__ u, double* __restrict__ x) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long item = t >> 4;
+  const bool active = item < (long long)nrows * a.nc;
+  const int i = active ? rows[item / a.nc] : 0;
+  tri_row16<BMAX>(a, i, active ? (int)(item % a.nc) : 0, (int)(t & 15), active, nn, b, u, x);
 }
 
 hipError_t launch_tri_level(hipStream_t st, const TriArgs& a, const int* rows, int nrows, const int* nn, int b,
                             const double* u, double* x) {
-  int g = (nrows * a.nc + kBlock - 1) / kBlock;
-  if (b <= 8)
-    hipLaunchKernelGGL(tri_level_kernel<8>, dim3(g), dim3(kBlock), 0, st, a, rows, nrows, nn, b, u, x);
-  else if (b <= 16)
+  const long long threads = (long long)nrows * a.nc * 16;
+  const int g = (int)((threads + kBlock - 1) / kBlock);
+  if (b <= 16)
     hipLaunchKernelGGL(tri_level_kernel<16>, dim3(g), dim3(kBlock), 0, st, a, rows, nrows, nn, b, u, x);
   else
     hipLaunchKernelGGL(tri_level_kernel<32>, dim3(g), dim3(kBlock), 0, st, a, rows, nrows, nn, b, u, x);
@@ -1705,24 +1711,23 @@ hipError_t launch_tri_level(hipStream_t st, const TriArgs& a, const int* rows, i
 // A run of consecutive SMALL levels of the Vecchia DAG in one workgroup:
 // the rows of level lv are rows[lptr[lv] .. lptr[lv+1]); the workgroup
 // barrier between levels replaces a kernel launch (same arithmetic as
-// tri_level_kernel).
+// tri_level_kernel: 16 lanes per (row, chain), 64 at a time).
 template <int BMAX>
 __global__ __launch_bounds__(1024) void tri_levels_block_kernel(TriArgs a, const int* __restrict__ rows,
                                                                 const int* __restrict__ lptr, int lv0, int lv1,
                                                                 const int* __restrict__ nn, int b,
                                                                 const double* __restrict__ u, double* x) {
+  const int l = threadIdx.x & 15, grp = threadIdx.x >> 4, ngrp = blockDim.x >> 4;
   for (int lv = lv0; lv < lv1; ++lv) {
     const int r0 = lptr[lv], cnt = (lptr[lv + 1] - r0) * a.nc;
-    for (int t = (int)threadIdx.x; t < cnt; t += blockDim.x) tri_row<BMAX>(a, rows[r0 + t / a.nc], t % a.nc, nn, b, u, x);
+    for (int it = grp; it < cnt; it += ngrp) tri_row16<BMAX>(a, rows[r0 + it / a.nc], it % a.nc, l, true, nn, b, u, x);
     __syncthreads();
   }
 }
 
 hipError_t launch_tri_levels_block(hipStream_t st, const TriArgs& a, const int* rows, const int* lptr, int lv0,
                                    int lv1, const int* nn, int b, const double* u, double* x) {
-  if (b <= 8)
-    hipLaunchKernelGGL(tri_levels_block_kernel<8>, dim3(1), dim3(1024), 0, st, a, rows, lptr, lv0, lv1, nn, b, u, x);
-  else if (b <= 16)
+  if (b <= 16)
     hipLaunchKernelGGL(tri_levels_block_kernel<16>, dim3(1), dim3(1024), 0, st, a, rows, lptr, lv0, lv1, nn, b, u,
                        x);
   else
