@@ -16,6 +16,15 @@
 
 namespace nngp {
 
+// DPP move of a double (both halves; lanes without a source read +0.0)
+template <int CTRL, int RM, bool BC>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, x);
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, RM, 0xF, BC);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, RM, 0xF, BC);
+  return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32));
+}
+
 // ------------------------------------------------------------------ RNG
 __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
@@ -1225,14 +1234,6 @@ struct TileState {
     }                                                                     \
   } while (0)
 
-// DPP move of a double (both halves; lanes without a source read +0.0)
-template <int CTRL, int RM, bool BC>
-__device__ __forceinline__ double dpp_f64(double x) {
-  const unsigned long long u = __builtin_bit_cast(unsigned long long, x);
-  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, RM, 0xF, BC);
-  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, RM, 0xF, BC);
-  return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32));
-}
 
 // one step of a segmented inclusive scan (flag f = "a segment starts here or
 // in an earlier lane of my partial"): (f_e, v_e) (+) (f, v) = (f_e | f, f ? v : v_e + v)
