@@ -143,3 +143,27 @@ def test_rccl_single_rank_communicator(P):
             ctx.sweep_chains(2, [0.0], [0.0], [0.0], [7], [0])
             res.append(ctx.get_field())
     np.testing.assert_array_equal(res[0], res[1])
+
+
+def test_group_shard_with_duplicated_observations_and_mu_vector(P):
+    """Locations with several observations (Heavy_metals-like, n_obs > n) and
+    a per-observation mean: the per-slot residual sums and observation counts
+    are replicated on every rank; still bitwise equal to one rank."""
+    n, m, G = 4000, 10, 4
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=21, dup_frac=0.15)
+    rng = np.random.default_rng(4)
+    field = rng.normal(size=n)
+    mu = 0.2 + 0.05 * rng.normal(size=len(y))
+    out = []
+    for g_count in (1, G):
+        ctxs = [P.ShardContext(locs, NN, col, lm, y, n_ranks=g_count, rank=g, device=0) for g in range(g_count)]
+        for c in ctxs:
+            c.factor(0, "matern15_isotropic", [1.0, 0.07, 0.0])
+            c.set_field(field)
+            c.set_mu(mu, 0.2)
+        P.sweep_chains_group(ctxs, 3, [0.2], [0.1], [-0.4], [9], [2])
+        out.append([c.get_field() for c in ctxs])
+        for c in ctxs:
+            c.close()
+    for f in out[1]:
+        np.testing.assert_array_equal(f, out[0][0])
