@@ -7,7 +7,7 @@ namespace nngp {
 
 constexpr int kWave = 64;
 constexpr int kBlock = 256;
-constexpr int kRedBlocks = 1024;  // max partial blocks of a reduction
+constexpr int kRedBlocks = 4096;  // max partial blocks of a reduction
 
 // per-chain scalars read by the sweep kernels from device memory (graph-replay safe)
 struct SweepScalars {
