@@ -1038,10 +1038,12 @@ enum SweepPart { kPrologue = 1, kColours = 2, kEpilogue = 4, kAll = 7 };
 static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, int mask, const double* z_dev, int parts = kAll) {
   const int n = c->n;
   SweepDev L = sweep_dev(c);
+  FieldPtrs fp;
+  for (int k = 0; k < kMaxChains; ++k) fp.p[k] = k < c->C ? c->ch[k].field_d : nullptr;
   if (parts & kPrologue) {
+    HIPCHK(c, launch_field_to_slots_multi(c->st, c->n, c->slot_dpos_d, fp, c->scal_d, c->w_slot_d, c->C, mask));
     for (int k = 0; k < c->C; ++k) {
       if (!((mask >> k) & 1)) continue;
-      HIPCHK(c, launch_field_to_slots(c->st, c->n, c->slot_dpos_d, c->ch[k].field_d, c->scal_d, c->w_slot_d, c->C, k));
       // factor pointer and beta0 read from device memory so a replayed graph
       // sees the current factor and beta0
       launch_row_stats(c->st, nullptr, c->nn_d, n, c->b, c->ch[k].field_d, 0.0, c->r_d + k, c->partials_d,
@@ -1079,11 +1081,8 @@ static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, int mask, const double*
       }
     }
   }
-  if (parts & kEpilogue) {
-    for (int k = 0; k < c->C; ++k)
-      if ((mask >> k) & 1)
-        HIPCHK(c, launch_slots_to_field(c->st, c->n, c->slot_dpos_d, c->w_slot_d, c->scal_d, c->ch[k].field_d, c->C, k));
-  }
+  if (parts & kEpilogue)
+    HIPCHK(c, launch_slots_to_field_multi(c->st, c->n, c->slot_dpos_d, fp, c->scal_d, c->w_slot_d, c->C, mask));
   return NNGP_OK;
 }
 

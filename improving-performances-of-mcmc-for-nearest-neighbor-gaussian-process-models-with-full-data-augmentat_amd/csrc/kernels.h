@@ -111,11 +111,13 @@ hipError_t launch_sell_refresh(hipStream_t st, const SweepDev& L, int nchunks, c
 hipError_t launch_residual_sums(hipStream_t st, int n, const SweepDev& L, int chain, const int* obs_ptr,
                                 const int* obs_idx, const double* y, const double* mu, double beta0);
 
-// w[x*C+chain] = field[dpos[x]] - beta0 (and back); x compact
-hipError_t launch_field_to_slots(hipStream_t st, int n, const int* slot_dpos, const double* field,
-                                 const SweepScalars* sc, double* w_slot, int C, int chain);
-hipError_t launch_slots_to_field(hipStream_t st, int n, const int* slot_dpos, const double* w_slot,
-                                 const SweepScalars* sc, double* field, int C, int chain);
+// w[x*C+chain] = field_chain[dpos[x]] - beta0 (and back), x compact, for
+// every chain in mask in one pass (field of chain k: f.p[k])
+struct FieldPtrs { double* p[kMaxChains]; };
+hipError_t launch_field_to_slots_multi(hipStream_t st, int n, const int* slot_dpos, const FieldPtrs& f,
+                                       const SweepScalars* sc, double* w_slot, int C, int mask);
+hipError_t launch_slots_to_field_multi(hipStream_t st, int n, const int* slot_dpos, const FieldPtrs& f,
+                                       const SweepScalars* sc, const double* w_slot, int C, int mask);
 
 // one colour of the chromatic sweep for the chains in a.chain_mask
 hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, const ColorLaunch& a);

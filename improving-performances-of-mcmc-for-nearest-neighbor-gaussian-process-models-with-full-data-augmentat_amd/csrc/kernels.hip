@@ -744,33 +744,39 @@ hipError_t launch_residual_sums(hipStream_t st, int n, const SweepDev& L, int ch
   return hipGetLastError();
 }
 
-__global__ void field_to_slots_kernel(int n, const int* __restrict__ slot_dpos,
-                                      const double* __restrict__ field,
-                                      const SweepScalars* __restrict__ sc, double* __restrict__ w,
-                                      int C) {
+// every chain in `mask` at once: slot_dpos read once, w written as whole
+// slot records (slot*C + chain)
+__global__ void field_to_slots_multi_kernel(int n, const int* __restrict__ slot_dpos, FieldPtrs f,
+                                            const SweepScalars* __restrict__ sc, double* __restrict__ w, int C,
+                                            int mask) {
   int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < n) w[(size_t)s * C] = field[slot_dpos[s]] - sc->beta0;
+  if (s >= n) return;
+  const int d = slot_dpos[s];
+#pragma unroll
+  for (int k = 0; k < kMaxChains; ++k)
+    if (k < C && ((mask >> k) & 1)) w[(size_t)s * C + k] = f.p[k][d] - sc[k].beta0;
 }
-__global__ void slots_to_field_kernel(int n, const int* __restrict__ slot_dpos,
-                                      const double* __restrict__ w,
-                                      const SweepScalars* __restrict__ sc, double* __restrict__ field,
-                                      int C) {
+__global__ void slots_to_field_multi_kernel(int n, const int* __restrict__ slot_dpos, FieldPtrs f,
+                                            const SweepScalars* __restrict__ sc, const double* __restrict__ w,
+                                            int C, int mask) {
   int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < n) field[slot_dpos[s]] = w[(size_t)s * C] + sc->beta0;
+  if (s >= n) return;
+  const int d = slot_dpos[s];
+#pragma unroll
+  for (int k = 0; k < kMaxChains; ++k)
+    if (k < C && ((mask >> k) & 1)) f.p[k][d] = w[(size_t)s * C + k] + sc[k].beta0;
 }
 
-hipError_t launch_field_to_slots(hipStream_t st, int n, const int* slot_dpos, const double* field,
-                                 const SweepScalars* sc, double* w_slot, int C, int chain) {
+hipError_t launch_field_to_slots_multi(hipStream_t st, int n, const int* slot_dpos, const FieldPtrs& f,
+                                       const SweepScalars* sc, double* w_slot, int C, int mask) {
   int g = (n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(field_to_slots_kernel, dim3(g), dim3(kBlock), 0, st, n, slot_dpos, field, sc + chain,
-                     w_slot + chain, C);
+  hipLaunchKernelGGL(field_to_slots_multi_kernel, dim3(g), dim3(kBlock), 0, st, n, slot_dpos, f, sc, w_slot, C, mask);
   return hipGetLastError();
 }
-hipError_t launch_slots_to_field(hipStream_t st, int n, const int* slot_dpos, const double* w_slot,
-                                 const SweepScalars* sc, double* field, int C, int chain) {
+hipError_t launch_slots_to_field_multi(hipStream_t st, int n, const int* slot_dpos, const FieldPtrs& f,
+                                       const SweepScalars* sc, const double* w_slot, int C, int mask) {
   int g = (n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(slots_to_field_kernel, dim3(g), dim3(kBlock), 0, st, n, slot_dpos, w_slot + chain,
-                     sc + chain, field, C);
+  hipLaunchKernelGGL(slots_to_field_multi_kernel, dim3(g), dim3(kBlock), 0, st, n, slot_dpos, f, sc, w_slot, C, mask);
   return hipGetLastError();
 }
 
