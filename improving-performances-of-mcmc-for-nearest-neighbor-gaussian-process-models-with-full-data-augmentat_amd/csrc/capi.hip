@@ -1042,14 +1042,9 @@ static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, int mask, const double*
   for (int k = 0; k < kMaxChains; ++k) fp.p[k] = k < c->C ? c->ch[k].field_d : nullptr;
   if (parts & kPrologue) {
     HIPCHK(c, launch_field_to_slots_multi(c->st, c->n, c->slot_dpos_d, fp, c->scal_d, c->w_slot_d, c->C, mask));
-    for (int k = 0; k < c->C; ++k) {
-      if (!((mask >> k) & 1)) continue;
-      // factor pointer and beta0 read from device memory so a replayed graph
-      // sees the current factor and beta0
-      launch_row_stats(c->st, nullptr, c->nn_d, n, c->b, c->ch[k].field_d, 0.0, c->r_d + k, c->partials_d,
-                       &c->scal_d[k].beta0, c->linv_cur_d + k, c->C);
-      HIPCHK(c, hipGetLastError());
-    }
+    // r = B w of every chain in one pass; factor pointers and beta0 read from
+    // device memory so a replayed graph sees the current factor and beta0
+    HIPCHK(c, launch_spmv_chains(c->st, c->linv_cur_d, c->nn_d, n, c->b, fp, c->scal_d, c->r_d, c->C, mask));
     // normals of sweep 0 (later sweeps' normals are generated inside the
     // previous sweep's colour launches; the tile engine draws them inline)
     if (!z_dev && c->engine == 0) HIPCHK(c, launch_normals_compact(c->st, L, mask, 0, n, c->zbuf_d));

@@ -99,6 +99,12 @@ int launch_row_stats(hipStream_t st, const double* linv, const int* nn, int n, i
                      const double* shift_dev = nullptr /* overrides shift when set */,
                      const double* const* linv_dev = nullptr /* overrides linv when set */,
                      int out_stride = 1);
+// r = B (field_chain - beta0_chain) for every chain in mask: out[k*C + chain]
+// (factor of chain k: *linv_dev[k]; the row's NNarray read once)
+// field pointer of each chain (device row order)
+struct FieldPtrs { double* p[kMaxChains]; };
+hipError_t launch_spmv_chains(hipStream_t st, const double* const* linv_dev, const int* nn, int n, int b,
+                              const FieldPtrs& f, const SweepScalars* sc, double* out, int C, int mask);
 // reduce `nblocks` x 4 partials into res[4] (deterministic order)
 hipError_t launch_reduce4(hipStream_t st, const double* partials, int nblocks, double* res);
 
@@ -113,7 +119,6 @@ hipError_t launch_residual_sums(hipStream_t st, int n, const SweepDev& L, int ch
 
 // w[x*C+chain] = field_chain[dpos[x]] - beta0 (and back), x compact, for
 // every chain in mask in one pass (field of chain k: f.p[k])
-struct FieldPtrs { double* p[kMaxChains]; };
 hipError_t launch_field_to_slots_multi(hipStream_t st, int n, const int* slot_dpos, const FieldPtrs& f,
                                        const SweepScalars* sc, double* w_slot, int C, int mask);
 hipError_t launch_slots_to_field_multi(hipStream_t st, int n, const int* slot_dpos, const FieldPtrs& f,

@@ -654,6 +654,51 @@ int launch_row_stats(hipStream_t st, const double* linv, const int* nn, int n, i
   return g;
 }
 
+// r = B (field - beta0) for every chain in mask in one pass: the row's
+// NNarray entries are read once for all chains; per chain the same products
+// and butterfly as row_stats_kernel (bitwise the same r).  Factor pointers
+// and beta0 are read from device memory (graph-replay safe).
+template <int G>
+__global__ __launch_bounds__(256) void spmv_chains_kernel(const double* const* __restrict__ linv_dev,
+                                                          const int* __restrict__ nn, int n, int b, FieldPtrs f,
+                                                          const SweepScalars* __restrict__ sc,
+                                                          double* __restrict__ out, int C, int mask) {
+  const int g = threadIdx.x & (G - 1);
+  const int rows_per_grid = gridDim.x * (blockDim.x / G);
+  for (int k = blockIdx.x * (blockDim.x / G) + threadIdx.x / G; k < n; k += rows_per_grid) {
+    const int idx = g < b ? nn[(size_t)k * b + g] : -1;
+#pragma unroll
+    for (int ch = 0; ch < kMaxChains; ++ch) {
+      if (ch >= C || !((mask >> ch) & 1)) continue;
+      double l = 0.0, xv = 0.0;
+      if (idx >= 0) {
+        l = linv_dev[ch][(size_t)k * b + g];
+        xv = f.p[ch][idx] - sc[ch].beta0;
+      }
+      double u = l * xv;
+#pragma unroll
+      for (int off = 1; off < G; off <<= 1) u += __shfl_xor(u, off, 64);
+      if (g == 0) out[(size_t)k * C + ch] = u;
+    }
+  }
+}
+
+hipError_t launch_spmv_chains(hipStream_t st, const double* const* linv_dev, const int* nn, int n, int b,
+                              const FieldPtrs& f, const SweepScalars* sc, double* out, int C, int mask) {
+  const int G = b <= 4 ? 4 : b <= 8 ? 8 : b <= 16 ? 16 : 32;
+  const long long rows_per_block = kBlock / G;
+  int g = (int)((n + rows_per_block - 1) / rows_per_block);
+  if (g > kRedBlocks) g = kRedBlocks;
+  if (g < 1) g = 1;
+  switch (G) {
+    case 4: hipLaunchKernelGGL(spmv_chains_kernel<4>, dim3(g), dim3(kBlock), 0, st, linv_dev, nn, n, b, f, sc, out, C, mask); break;
+    case 8: hipLaunchKernelGGL(spmv_chains_kernel<8>, dim3(g), dim3(kBlock), 0, st, linv_dev, nn, n, b, f, sc, out, C, mask); break;
+    case 16: hipLaunchKernelGGL(spmv_chains_kernel<16>, dim3(g), dim3(kBlock), 0, st, linv_dev, nn, n, b, f, sc, out, C, mask); break;
+    default: hipLaunchKernelGGL(spmv_chains_kernel<32>, dim3(g), dim3(kBlock), 0, st, linv_dev, nn, n, b, f, sc, out, C, mask); break;
+  }
+  return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void reduce4_kernel(const double* __restrict__ partials,
                                                       int nblocks, double* __restrict__ res) {
   double acc[4] = {0, 0, 0, 0};
