@@ -471,3 +471,78 @@ def test_tri_solve_every_row_width(P, O, m):
         Ls = [ctx.select(k).get_linv(0) for k in range(2)]
     for g, L in zip(got, Ls):
         np.testing.assert_allclose(g, O.tri_solve(L, NN, u), rtol=1e-9, atol=1e-10)
+
+
+def test_configs1_synthetic_1e5_m10_exponential(P, O):
+    """BASELINE configs[1]: synthetic 2-D, n = 1e5, m = 10, exponential
+    covariance -- factor, log-likelihood and two chromatic sweeps (default
+    engine, Philox normals) against the oracle."""
+    n, m = 100_000, 10
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=101)
+    cp = [1.0, 0.1, 0.0]
+    field = np.random.default_rng(2).normal(size=n)
+    seed, base = 4242, 3
+    with _ctx(P, locs, NN, col, lm, y) as ctx:
+        ctx.factor(0, "exponential_isotropic", cp)
+        Linv = ctx.get_linv(0)
+        ctx.set_field(field)
+        ctx.set_mu(None, 0.5)
+        ll = ctx.loglik(0, 0.5, 0.3)
+        ctx.sweep(2, 0.5, 0.3, -1.0, seed, base)
+        got = ctx.get_field()
+    Lo = O.vecchia_linv("exponential_isotropic", cp, locs, NN)
+    np.testing.assert_allclose(Linv, Lo, rtol=1e-9, atol=1e-10)
+    llo = O.loglik(Lo, field - 0.5, NN, 0.3)
+    assert abs(ll - llo) <= 1e-10 * abs(llo)
+    z = O.sweep_normals(seed, base, 2, n)
+    ref = O.sweep("local", field, Lo, NN, col, O.precision_diag(Lo, NN), np.ones(n, np.int32), y,
+                  np.full(n, 0.5), lm, 0.5, 0.3, -1.0, z)
+    np.testing.assert_allclose(got, ref, rtol=1e-8, atol=1e-9)
+
+
+def test_headline_size_1e6_m15_three_chains(P, O):
+    """The headline workload itself (n = 1e6, m = 15, Matern 3/2, 3 chains in
+    one context, the default engine): chain 1's field after one call of 2
+    sweeps against the oracle's local-form sweep with the same Philox normals
+    and the device's own factor (isolates the sweep), its log-likelihood
+    against the oracle's on that factor (1e-10), and the factor against the
+    oracle's per row within DESIGN §4's bound max(1e-10, 1e-14 cond(C_i)) x
+    max|row| (at this density, range 0.04 over 1e6 points, many local
+    covariances are near-singular)."""
+    n, m, C = 1_000_000, 15, 3
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=7)
+    cps = [[1.0, 0.05, 0.0], [1.2, 0.04, 0.0], [0.8, 0.06, 0.0]]
+    rng = np.random.default_rng(5)
+    fields = [rng.normal(size=n) for _ in range(C)]
+    with P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=C) as ctx:
+        for k in range(C):
+            ctx.select(k)
+            ctx.factor(0, "matern15_isotropic", cps[k])
+            ctx.set_field(fields[k])
+            ctx.set_mu(None, 0.1 * k)
+        ctx.select(1)
+        L1 = ctx.get_linv(0)
+        ll = ctx.loglik(0, 0.1, 0.2)
+        ctx.sweep_chains(2, [0.0, 0.1, 0.2], [0.0, 0.2, -0.1], [-0.5, -0.4, -0.6], [11, 12, 13], [0, 0, 0])
+        got = ctx.get_field()
+    llo = O.loglik(L1, fields[1] - 0.1, NN, 0.2)
+    assert abs(ll - llo) <= 1e-10 * abs(llo)
+    z = O.sweep_normals(12, 0, 2, n)
+    ref = O.sweep("local", fields[1], L1, NN, col, O.precision_diag(L1, NN), np.ones(n, np.int32), y,
+                  np.full(n, 0.1), lm, 0.1, 0.2, -0.4, z)
+    np.testing.assert_allclose(got, ref, rtol=1e-8, atol=1e-9)
+    Lo = O.vecchia_linv("matern15_isotropic", cps[1], locs, NN)
+    err = np.abs(L1 - Lo).max(axis=1)
+    scale = np.abs(Lo).max(axis=1)
+    bad = np.nonzero(err > 1e-10 * scale)[0]
+    if len(bad):
+        covs = np.stack([O.covmat("matern15_isotropic", cps[1], locs[NN[i][NN[i] != O.NA] - 1]) for i in bad
+                         if (NN[i] != O.NA).sum() == m + 1])
+        full = np.array([i for i in bad if (NN[i] != O.NA).sum() == m + 1])
+        kappa = np.linalg.cond(covs)
+        assert np.all(err[full] <= np.maximum(1e-10, 1e-14 * kappa) * scale[full])
+        short = np.setdiff1d(bad, full)  # the first m rows (fewer neighbours)
+        for i in short:
+            idx = NN[i][NN[i] != O.NA] - 1
+            k = np.linalg.cond(O.covmat("matern15_isotropic", cps[1], locs[idx]))
+            assert err[i] <= max(1e-10, 1e-14 * k) * scale[i]
