@@ -4,11 +4,15 @@
 // Kernel map (SURVEY.md §8a ids):
 //   scale_coords_kernel / factor_kernel  A4  GpGp::vecchia_Linv
 //   row_stats_kernel + reduce4_kernel    A6  ll_compressed_sparse_chol, B x, beta_0 stats
-//   sell_refresh_kernel                  A5  B values in sweep layout + precision_diag
+//   spmv_chains_kernel                   A1  r = B w of every chain at the start of a sweep call
+//   sell_refresh_kernel / tile_refresh   A5  B values in sweep layout + precision_diag
 //   residual_sums_kernel                 A7  residuals_sum
-//   sweep_color_kernel                   A1  one colour of the chromatic sweep
+//   sweep_tiles_kernel                   A1  the chromatic sweep, one persistent launch per call (default)
+//   sweep_color_kernel                   A1  one colour of the chromatic sweep (fallback)
+//   shard_ghost_kernel                   A1  colour-sharded sweep: halo updates after the exchange
+//   field/slots_to_*_multi_kernel        A1  field <-> compact slot order, every chain
 //   obs_reduce_kernel                    A8  SSR, dnorm ratio
-//   tri_level_kernel                     (next) Matrix::solve by DAG level
+//   tri_level_kernel / _levels_block     (next) Matrix::solve by DAG level
 #include "kernels.h"
 #include <cstdlib>
 
