@@ -1583,7 +1583,7 @@ template <int C, int NT, int PROBE>
 static hipError_t launch_tiles_c(hipStream_t st, const TileDev& D, const TileLaunch& a, int lds) {
   constexpr int RMAX = tile_rmax(C, NT);
   constexpr int DB = tile_double_buffer(C);
-  constexpr int GMAX = (DB && C >= 3) ? (512 / NT > 0 ? 512 / NT : 1) : (C >= 3 && NT == 512 ? 3 : (1024 / NT > 0 ? 1024 / NT : 1));
+  constexpr int GMAX = (DB && C >= 3) ? (512 / NT > 0 ? 512 / NT : 1) : (NT == 512 ? 3 : (1024 / NT > 0 ? 1024 / NT : 1));
   auto k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE>;
   lds = lds < kTSpreadLds ? kTSpreadLds : lds;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
