@@ -117,7 +117,9 @@ struct nngp_ctx {
   double* dwx_d = nullptr;        // n x C granules of 16 B
   unsigned* ctl_d = nullptr;      // [0] call id, [1] timeout word
   unsigned* tmo_h = nullptr;      // pinned copy of the timeout word after each launch
-  unsigned long long* tdbg_d = nullptr;  // NNGP_PROBE=9: per-tile phase times
+  unsigned long long* tdbg_d = nullptr;  // NNGP_PROBE=9: per-tile phase times, =2: per-phase timeline
+  size_t tdbg_n = 0;
+  int tprobe = 0;
   // colour-sharded sweep (nngp_ctx_create_shard; graph_prep.h ShardPlan):
   // this context is rank sp.rank of sp.G; it sweeps its own chunks of every
   // colour and exchanges {dw, w_new} of the colour's slots through xbuf_d
@@ -226,6 +228,8 @@ TileDev tile_dev(nngp_ctx* c) {
   D.scal = c->scal_d;
   D.ctl = c->ctl_d;
   D.dbg = c->tdbg_d;
+  D.probe = c->tprobe;
+  if (const char* v = std::getenv("NNGP_TILE_VARIANT")) D.variant = std::atoi(v);
   D.K = c->tl.K;
   D.C = c->C;
   D.T = c->tl.T;
@@ -586,9 +590,11 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     CK(hipMemsetAsync(c->dwx_d, 0, sizeof(double) * (size_t)n * C * 2, c->st));
     CK(hipMemsetAsync(c->ctl_d, 0, sizeof(unsigned) * 4, c->st));
     if (const char* pr = std::getenv("NNGP_PROBE"))
-      if (std::atoi(pr) == 9 && (C == 1 || C == 3)) {
-        CK(dalloc(&c->tdbg_d, (size_t)TL.T * 8));
-        CK(hipMemsetAsync(c->tdbg_d, 0, sizeof(unsigned long long) * TL.T * 8, c->st));
+      if ((std::atoi(pr) == 9 || std::atoi(pr) == 2) && (C == 1 || C == 3)) {
+        c->tprobe = std::atoi(pr) == 9 ? 1 : 2;
+        c->tdbg_n = (size_t)TL.T * (c->tprobe == 1 ? 8 : 512 * 8);
+        CK(dalloc(&c->tdbg_d, c->tdbg_n));
+        CK(hipMemsetAsync(c->tdbg_d, 0, sizeof(unsigned long long) * c->tdbg_n, c->st));
       }
   }
   CK(dalloc(&c->w_slot_d, NS * C));
@@ -1159,7 +1165,7 @@ int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const doub
   if ((rc = tile_timeout_check(c))) return rc;
   if (c->tdbg_d) {
     if (const char* path = std::getenv("NNGP_DBG_OUT")) {
-      std::vector<unsigned long long> h((size_t)c->tl.T * 8);
+      std::vector<unsigned long long> h(c->tdbg_n);
       HIPCHK(c, hipMemcpy(h.data(), c->tdbg_d, h.size() * 8, hipMemcpyDeviceToHost));
       if (FILE* f = std::fopen(path, "wb")) {
         std::fwrite(h.data(), 8, h.size(), f);

@@ -162,6 +162,8 @@ struct TileDev {
   unsigned long long* dbg;    // NNGP_PROBE=9: per-tile phase times (4 x u64), else null
   int K, C, T, n;
   int max_gslots;             // max foreign slots of a (tile, colour): LDS of their dw
+  int probe = 0;
+  int variant = 0;            // NNGP_TILE_VARIANT (experiments)              // dbg layout: 1 = per-tile segment sums (T x 8), 2 = timeline (T x 512 phases x 4)
 };
 
 struct TileLaunch {
@@ -175,7 +177,9 @@ int tile_lds_bytes(int max_rows, int C, int NT, int K, int max_batches, int max_
 // chains stay in registers (C >= 3: fewer cells per batch)
 // double-buffered batch registers (the next colour's loads in flight during
 // this colour's work) where two batches fit in registers
-constexpr int tile_double_buffer(int C) { return C <= 2 ? 1 : 0; }
+// (256-thread tiles at 3 chains, one wave per SIMD with 512 registers, double
+// buffered: 7.7k vs 10.7k chain-sweeps/s -- the own work needs the waves)
+constexpr int tile_double_buffer(int C, int NT) { return C <= 2 ? 1 : 0; }
 constexpr int tile_rmax(int C, int NT) { return 4096 / NT; }
 hipError_t launch_sweep_tiles(hipStream_t st, const TileDev& D, const TileLaunch& a, int max_rows, int NT,
                               int max_batches, int max_gslots);

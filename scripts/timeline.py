@@ -1,0 +1,63 @@
+"""Tile engine per-phase timeline (NNGP_PROBE=2 build path): thread 0 of every
+tile stamps the 100 MHz clock at the start of each colour phase, after the
+draw (granules published), after the hand-off poll and at the phase end.
+Usage: timeline.py [n] [m] [chains] [n_sweeps]"""
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+os.environ["NNGP_PROBE"] = "2"
+out = "/tmp/tile_timeline.bin"
+os.environ["NNGP_DBG_OUT"] = out
+import _pkgload  # noqa: E402
+import bench  # noqa: E402
+
+P = _pkgload.load()
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+m = int(sys.argv[2]) if len(sys.argv) > 2 else 15
+C = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+S = int(sys.argv[4]) if len(sys.argv) > 4 else 10
+cp = [1.0, 0.05, 0.0]
+wl = bench.make_workload(P, n, m, "matern15_isotropic", cp, seed=1000, device=0, chains=C)
+ctx = bench.open_context(P, wl, "matern15_isotropic", cp, 0, C, seed=7)
+info = ctx.info
+K = info["n_colors"]
+T = info["n_tiles"]
+print({k: info[k] for k in ("sweep_engine", "n_tiles", "tile_rows_max", "n_ghost_cells", "n_colors")})
+args = ([wl["beta0"]] * C, [wl["log_scale"]] * C, [wl["log_noise_variance"]] * C, [77 + k for k in range(C)])
+for rep in range(4):
+    t = time.perf_counter()
+    ctx.sweep_chains(S, *args, [rep * S] * C)
+    el = time.perf_counter() - t
+nph = S * K
+raw = np.fromfile(out, dtype=np.uint64).reshape(T, 512, 8)[:, :nph]
+spins = raw[..., 5].astype(np.float64)
+d = raw[..., :5].astype(np.float64) / 100.0  # us
+miss = d[..., 1] == 0              # (tile, colour) with no own batch: no publish stamp
+d[..., 1][miss] = d[..., 0][miss]
+d -= d[:, 0, 0].min()
+start, pub, hand, end, landed = d[..., 0], d[..., 1], d[..., 2], d[..., 3], d[..., 4]
+own = pub - start                  # own batches up to the draw barrier (publish)
+rest = hand - pub                  # scatter + stream issue + hand-off poll
+tail = end - hand                  # ghost adds + next batch prep
+dur = end - start
+print(f"C={C} last call {el*1e3:.3f} ms wall, launch span {end[:, -1].max():.1f} us, {end[:, -1].max()/nph:.2f} us/phase")
+print("per tile per phase (mean / p90 / max over tiles, averaged over phases):")
+for nm, a in (("own->publish", own), ("publish->prepped", landed - pub), ("prepped->handoff", hand - landed),
+              ("handoff->end", tail), ("phase", dur)):
+    print(f"  {nm:18s} mean {a.mean():6.2f}  p90 {np.percentile(a, 90, axis=0).mean():6.2f}  max {a.max(axis=0).mean():6.2f}")
+print(f"  poll spins (max over the tile's threads): mean {spins.mean():.2f}, p90 {np.percentile(spins, 90):.0f}, "
+      f"share of phases with spins {(spins > 0).mean():.2f}")
+# critical path: per phase, the spread of publish times across tiles
+spread = pub.max(axis=0) - pub.min(axis=0)
+print(f"  publish spread across tiles per phase: mean {spread.mean():.2f} us")
+# by colour (phases of the last sweeps)
+byc = dur.reshape(T, S, K).mean(axis=(0, 1))
+ownc = own.reshape(T, S, K).mean(axis=(0, 1))
+ownmax = own.reshape(T, S, K).max(axis=0).mean(axis=0)
+print("per colour: phase mean / own mean / own max over tiles")
+print(" ".join(f"{c}:{byc[c]:.1f}/{ownc[c]:.1f}/{ownmax[c]:.1f}" for c in range(K)))
+ctx.close()
