@@ -15,9 +15,11 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <numeric>
+#include <thread>
 
 namespace nngp {
 namespace {
@@ -116,6 +118,27 @@ struct TopM {
   }
   double worst() const { return c[cnt - 1].s; }
 };
+
+// host threads for the embarrassingly parallel init loops (NNGP_HOST_THREADS
+// overrides; results never depend on the count)
+int host_threads() {
+  if (const char* e = std::getenv("NNGP_HOST_THREADS")) return std::max(1, std::atoi(e));
+  unsigned h = std::thread::hardware_concurrency();
+  return (int)std::max(1u, std::min(h, 32u));
+}
+
+// f(t, lo, hi) over [0, n) split into contiguous chunks, one per thread
+template <class F>
+void parallel_chunks(long long n, F f) {
+  const int T = (int)std::min<long long>(host_threads(), std::max(1LL, n / 4096));
+  if (T <= 1) { f(0, 0LL, n); return; }
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t) {
+    const long long lo = n * t / T, hi = n * (t + 1) / T;
+    th.emplace_back([=, &f] { f(t, lo, hi); });
+  }
+  for (auto& x : th) x.join();
+}
 
 }  // namespace
 
@@ -223,68 +246,75 @@ void order_maxmin(const double* locs, int n, int d, std::vector<int>& order) {
 void find_ordered_nn(const double* locs, int n, int d, int m, std::vector<int>& nn) {
   const int b = m + 1;
   nn.assign((size_t)n * b, -1);
-  std::vector<Cand> buf(std::max(m, 1));
-  TopM top{m, 0, buf.data()};
-  auto write_row = [&](int i) {
+  auto write_row = [&](int i, const TopM& top) {
     nn[(size_t)i * b] = i;
     for (int t = 0; t < top.cnt; ++t) nn[(size_t)i * b + 1 + t] = top.c[t].j;
   };
   const int brute = std::min(n, std::max(64, 4 * b));
-  for (int i = 0; i < brute; ++i) {
-    top.reset();
-    if (m > 0)
-      for (int j = 0; j < i; ++j) top.offer(sqdist(locs, n, d, i, j), j);
-    write_row(i);
+  {
+    std::vector<Cand> buf(std::max(m, 1));
+    TopM top{m, 0, buf.data()};
+    for (int i = 0; i < brute; ++i) {
+      top.reset();
+      if (m > 0)
+        for (int j = 0; j < i; ++j) top.offer(sqdist(locs, n, d, i, j), j);
+      write_row(i, top);
+    }
   }
   if (m == 0) { for (int i = brute; i < n; ++i) nn[(size_t)i * b] = i; return; }
   Grid g;
-  long long cc[3], q[3];
   for (int lo = brute; lo < n;) {
     int hi = (int)std::min<long long>((long long)n, 2LL * lo);
     g.build(locs, n, d, hi, std::max(2.0, m / 3.0));
-    for (int i = lo; i < hi; ++i) {
-      top.reset();
-      g.cell_of(locs, n, i, cc);
-      long long maxR = std::max(g.nc[0], std::max(g.nc[1], g.nc[2]));
-      for (long long R = 0;; ++R) {
-        // visit cells at Chebyshev distance exactly R
-        long long lo_c[3], hi_c[3];
-        for (int k = 0; k < 3; ++k) {
-          if (k < g.dg) { lo_c[k] = std::max(0LL, cc[k] - R); hi_c[k] = std::min(g.nc[k] - 1, cc[k] + R); }
-          else { lo_c[k] = hi_c[k] = 0; }
-        }
-        auto scan_cell = [&](const long long* qq) {
-          long long id = g.id_of(qq);
-          for (int t = g.start[id]; t < g.start[id + 1]; ++t) {
-            int j = g.pts[t];
-            if (j >= i) break;  // pts ascending inside a cell
-            top.offer(sqdist(locs, n, d, i, j), j);
+    // the queries of a block are independent given the grid of [0, hi)
+    parallel_chunks(hi - lo, [&](int, long long q0, long long q1) {
+      std::vector<Cand> buf(std::max(m, 1));
+      TopM top{m, 0, buf.data()};
+      long long cc[3], q[3];
+      for (int i = lo + (int)q0; i < lo + (int)q1; ++i) {
+        top.reset();
+        g.cell_of(locs, n, i, cc);
+        long long maxR = std::max(g.nc[0], std::max(g.nc[1], g.nc[2]));
+        for (long long R = 0;; ++R) {
+          // visit cells at Chebyshev distance exactly R
+          long long lo_c[3], hi_c[3];
+          for (int k = 0; k < 3; ++k) {
+            if (k < g.dg) { lo_c[k] = std::max(0LL, cc[k] - R); hi_c[k] = std::min(g.nc[k] - 1, cc[k] + R); }
+            else { lo_c[k] = hi_c[k] = 0; }
           }
-        };
-        for (q[2] = lo_c[2]; q[2] <= hi_c[2]; ++q[2])
-          for (q[1] = lo_c[1]; q[1] <= hi_c[1]; ++q[1]) {
-            long long outer = 0;
-            if (g.dg >= 2) outer = std::max(outer, std::llabs(q[1] - cc[1]));
-            if (g.dg >= 3) outer = std::max(outer, std::llabs(q[2] - cc[2]));
-            if (outer == R) {
-              for (q[0] = lo_c[0]; q[0] <= hi_c[0]; ++q[0]) scan_cell(q);
-            } else {
-              // only the two cells at |dq0| == R are on the ring
-              q[0] = cc[0] - R;
-              if (q[0] >= 0) scan_cell(q);
-              q[0] = cc[0] + R;
-              if (R > 0 && q[0] < g.nc[0]) scan_cell(q);
+          auto scan_cell = [&](const long long* qq) {
+            long long id = g.id_of(qq);
+            for (int t = g.start[id]; t < g.start[id + 1]; ++t) {
+              int j = g.pts[t];
+              if (j >= i) break;  // pts ascending inside a cell
+              top.offer(sqdist(locs, n, d, i, j), j);
             }
+          };
+          for (q[2] = lo_c[2]; q[2] <= hi_c[2]; ++q[2])
+            for (q[1] = lo_c[1]; q[1] <= hi_c[1]; ++q[1]) {
+              long long outer = 0;
+              if (g.dg >= 2) outer = std::max(outer, std::llabs(q[1] - cc[1]));
+              if (g.dg >= 3) outer = std::max(outer, std::llabs(q[2] - cc[2]));
+              if (outer == R) {
+                for (q[0] = lo_c[0]; q[0] <= hi_c[0]; ++q[0]) scan_cell(q);
+              } else {
+                // only the two cells at |dq0| == R are on the ring
+                q[0] = cc[0] - R;
+                if (q[0] >= 0) scan_cell(q);
+                q[0] = cc[0] + R;
+                if (R > 0 && q[0] < g.nc[0]) scan_cell(q);
+              }
+            }
+          if (R >= maxR) break;
+          // every unvisited point is >= R*cs away (tiny margin for cell rounding)
+          if (top.cnt == std::min(m, i)) {
+            double bound = ((double)R - 1e-6) * g.cs;
+            if (bound > 0 && bound * bound > top.worst()) break;
           }
-        if (R >= maxR) break;
-        // every unvisited point is >= R*cs away (tiny margin for cell rounding)
-        if (top.cnt == std::min(m, i)) {
-          double bound = ((double)R - 1e-6) * g.cs;
-          if (bound > 0 && bound * bound > top.worst()) break;
         }
+        write_row(i, top);
       }
-      write_row(i);
-    }
+    });
     lo = hi;
   }
 }
@@ -303,22 +333,58 @@ int greedy_coloring(const int* nn, int n, int b, std::vector<int>& colors) {
       if (a >= 0) crow[fill[a]++] = k;
     }
   colors.assign(n, 0);
+  // Blocks of nodes: the moral predecessors j < i of every node of the block
+  // (the members of the rows through i, Coloring.R:14-16) are gathered in
+  // parallel, deduplicated per node; then the first-fit pass runs over the
+  // block in index order (Coloring.R:14-18), so the colours are those of the
+  // sequential algorithm.
+  const int nthr = host_threads();
+  const int blk = 1 << 18;
+  std::vector<long long> pptr(blk + 1);
+  std::vector<std::vector<int>> pred(nthr);
+  std::vector<std::vector<int>> seen(nthr);
   std::vector<int> mark(64, 0);
   int K = 0;
-  for (int i = 0; i < n; ++i) {
-    int stamp = i + 1;
-    for (int p = cptr[i]; p < cptr[i + 1]; ++p) {
-      int k = crow[p];
-      for (int t = 0; t < b; ++t) {
-        int j = nn[(size_t)k * b + t];
-        if (j >= 0 && j < i) mark[colors[j]] = stamp;
+  for (int i0 = 0; i0 < n; i0 += blk) {
+    const int i1 = std::min(n, i0 + blk);
+    const int nb = i1 - i0;
+    std::vector<int> cnt(nb, 0);
+    const int T = std::max(1, std::min(nthr, nb / 1024));
+    std::vector<std::vector<int>> part(T);
+    std::vector<int> tlo(T + 1);
+    for (int t = 0; t <= T; ++t) tlo[t] = (int)((long long)nb * t / T);
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        std::vector<int>& sn = seen[t];
+        if ((int)sn.size() < n) sn.assign(n, -1);
+        std::vector<int>& out = part[t];
+        out.clear();
+        for (int ii = tlo[t]; ii < tlo[t + 1]; ++ii) {
+          const int i = i0 + ii;
+          for (int p = cptr[i]; p < cptr[i + 1]; ++p) {
+            const int k = crow[p];
+            for (int u = 0; u < b; ++u) {
+              const int j = nn[(size_t)k * b + u];
+              if (j >= 0 && j < i && sn[j] != i) { sn[j] = i; out.push_back(j); ++cnt[ii]; }
+            }
+          }
+        }
+      });
+    for (auto& x : th) x.join();
+    for (int t = 0; t < T; ++t) {
+      const int* pj = part[t].data();
+      for (int ii = tlo[t]; ii < tlo[t + 1]; ++ii) {
+        const int i = i0 + ii, stamp = i + 1;
+        for (int q = 0; q < cnt[ii]; ++q) mark[colors[pj[q]]] = stamp;
+        pj += cnt[ii];
+        int c = 1;
+        while (c < (int)mark.size() && mark[c] == stamp) ++c;
+        if (c + 1 >= (int)mark.size()) mark.resize(2 * mark.size() + 2, 0);
+        colors[i] = c;
+        K = std::max(K, c);
       }
     }
-    int c = 1;
-    while (c < (int)mark.size() && mark[c] == stamp) ++c;
-    if (c + 1 >= (int)mark.size()) mark.resize(2 * mark.size() + 2, 0);
-    colors[i] = c;
-    K = std::max(K, c);
   }
   return K;
 }

@@ -16,7 +16,10 @@ from .model import covparms
 
 
 def mcmc_nngp_predict_field(mcmc_nngp_list, predicted_locs, burn_in=0.5, n_cores=1, m=10, seed=1,
-                            device=-1):
+                            device=-1, z_new=None):
+    """predict.R:1-60.  ``z_new`` (optional) replaces the rnorm draws of the
+    new locations (predict.R:50): z_new[k][i] = the normals of chain k's i-th
+    prediction; by default they come from numpy's generator seeded ``seed``."""
     L = mcmc_nngp_list
     locs = L["locs"]
     predicted_locs = np.asarray(predicted_locs, np.float64)
@@ -32,7 +35,7 @@ def mcmc_nngp_predict_field(mcmc_nngp_list, predicted_locs, burn_in=0.5, n_cores
     stored = stored[stored > burn_in * stored.max()].astype(int)
     rng = np.random.default_rng(seed)
     out = []
-    for chain in L["records"].values():
+    for kc, chain in enumerate(L["records"].values()):
         shapes = chain["params"]["shape"][stored - 1]
         _, first_idx = np.unique(shapes, axis=0, return_index=True)
         need = np.zeros(len(stored), bool)
@@ -46,7 +49,8 @@ def mcmc_nngp_predict_field(mcmc_nngp_list, predicted_locs, burn_in=0.5, n_cores
             sd = np.exp(0.5 * chain["params"]["log_scale"][i_chain - 1, 0])
             w = chain["params"]["field"][i_field] - chain["params"]["beta_0"][i_chain - 1, 0]
             u = ctx.spmv(0, np.concatenate([w, np.zeros(N - n)]))[:n]
-            x = ctx.tri_solve(0, np.concatenate([u / sd, rng.normal(size=N - n)]))
+            z = rng.normal(size=N - n) if z_new is None else np.asarray(z_new[kc][k], np.float64)
+            x = ctx.tri_solve(0, np.concatenate([u / sd, z]))
             samples[k] = sd * x[n:]
         out.append(samples)
     ctx.close()
@@ -71,7 +75,7 @@ def mcmc_nngp_predict_fixed_effects(mcmc_nngp_list, X_predicted, burn_in=0.5, n_
     allnames = ["beta_0"] + list(L["X"].get("names", []))
     subset = [allnames.index(nm) for nm in names]
     out = []
-    for chain in L["records"].values():
+    for kc, chain in enumerate(L["records"].values()):
         bm = np.column_stack([chain["params"]["beta_0"]] + ([chain["params"]["beta"]] if "beta" in chain["params"] else []))
         bm = bm[stored - 1].copy()
         if bm.shape[1] > 1:

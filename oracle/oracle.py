@@ -229,3 +229,62 @@ def dense_B(Linv, NNarray) -> np.ndarray:
             if NNarray[i, j] != NA:
                 B[i, NNarray[i, j] - 1] = Linv[i, j]
     return B
+
+
+# ---------------------------------------------------------------- posterior prediction
+def _plogis(x):
+    return 1.0 / (1.0 + np.exp(-x))
+
+
+def predict_covparms(shape_params, shape) -> np.ndarray:
+    """c(1, shape, 0) with predict.R:34-38's transforms: exp() for log_*,
+    1.5 * plogis() for qlogis_* (not the MCMC's .5 + .5 * plogis)."""
+    out = [1.0]
+    for name, v in zip(shape_params, np.atleast_1d(shape)):
+        if name[:3] == "log":
+            out.append(float(np.exp(v)))
+        elif name[:6] == "qlogis":
+            out.append(float(1.5 * _plogis(v)))
+    return np.array(out + [0.0])
+
+
+def predict_field(mcmc_nngp_list, predicted_locs, z_new, burn_in=0.5, m=10):
+    """Restatement of Scripts/mcmc_nngp_predict.R:1-60 (mcmc_nngp_predict_field).
+
+    z_new[k] is an (n_samples, n_pred) array of the normals chain k draws for
+    the new locations (predict.R:50, rnorm), so the device path can be fed the
+    same values.  Returns the per-chain (n_samples, n_pred) sample arrays."""
+    L = mcmc_nngp_list
+    locs = np.asarray(L["locs"], np.float64)
+    pred = np.asarray(predicted_locs, np.float64)
+    allloc = np.vstack([locs, pred])                                   # :4
+    NN = find_ordered_nn(allloc, m)                                    # :5
+    n, N = locs.shape[0], allloc.shape[0]
+    covfun = L["space_time_model"]["covfun"]["stationary_covfun"]
+    sp = L["space_time_model"]["covfun"]["shape_params"]
+    chains = list(L["records"].values())
+    stored = np.asarray(chains[0]["saved_field"])                      # :13
+    stored = stored[stored > burn_in * stored.max()].astype(int)       # :14
+    out = []
+    for k, chain in enumerate(chains):                                 # :16-18
+        samples = np.zeros((len(stored), pred.shape[0]))               # :21
+        shapes = np.asarray(chain["params"]["shape"])[stored - 1]
+        shapes = shapes.reshape(len(stored), -1)
+        seen = set()
+        Linv = None
+        for ip, i_chain in enumerate(stored):                          # :25-28
+            i_field = int(np.nonzero(np.asarray(chain["saved_field"]) == i_chain)[0][0])  # :30
+            key = tuple(shapes[ip])
+            if key not in seen:                                        # :23,32 !duplicated
+                seen.add(key)
+                cp = predict_covparms(sp, shapes[ip])
+                Linv = vecchia_linv(covfun, cp, allloc, NN)            # :39
+            sd = np.exp(0.5 * float(np.asarray(chain["params"]["log_scale"])[i_chain - 1].ravel()[0]))  # :43
+            b0 = float(np.asarray(chain["params"]["beta_0"])[i_chain - 1].ravel()[0])
+            w = np.asarray(chain["params"]["field"])[i_field] - b0
+            # B[1:n, 1:n] w: rows < n of the stacked factor reference columns < n only
+            u = linv_mult(Linv, np.concatenate([w, np.zeros(N - n)]), NN)[:n]   # :49
+            x = tri_solve(Linv, NN, np.concatenate([u / sd, np.asarray(z_new[k][ip], np.float64)]))  # :46-52
+            samples[ip] = sd * x[n:]                                   # :44,53
+        out.append(samples)
+    return out

@@ -179,3 +179,56 @@ def test_shard_plan_emulation(tmp_path, n, m, G, sweeps, seed):
                     str(csrc / "graph_prep.cpp"), "-o", str(exe)], check=True)
     out = subprocess.run([str(exe), str(n), str(m), str(G), str(sweeps), str(seed)], capture_output=True, text=True)
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
+
+
+def test_predict_fixed_effects_closed_form(P):
+    """mcmc_nngp_predict_fixed_effects (predict.R:67-104) on a hand-made list:
+    beta_0 de-centred by X_mean (:94), columns matched by name (:87), no
+    intercept by default (:81-85), burn-in on the saved iterations (:73)."""
+    import pandas as pd
+
+    beta0 = np.array([[1.0], [2.0], [3.0], [4.0]])
+    beta = np.array([[0.5, -1.0], [0.6, -1.1], [0.7, -1.2], [0.8, -1.3]])
+    L = {"X": {"names": ["a", "b"], "X_mean": np.array([10.0, 20.0])},
+         "records": {"chain_1": {"saved_field": np.array([1.0, 2.0, 3.0, 4.0]),
+                                 "iterations": np.array([[0, 0.0], [4, 1.0]]),
+                                 "params": {"beta_0": beta0, "beta": beta}}}}
+    Xp = pd.DataFrame({"b": [1.0, 2.0], "a": [3.0, 0.5]})
+    out = P.mcmc_nngp_predict_fixed_effects(L, Xp, burn_in=0.5)
+    s = out["predicted_fixed_effects_samples"][0]
+    # stored iterations 3, 4 (> .5 * 4); model matrix columns (b, a) -> beta (b, a)
+    exp = np.array([[beta[k, 1] * 1.0 + beta[k, 0] * 3.0, beta[k, 1] * 2.0 + beta[k, 0] * 0.5] for k in (2, 3)])
+    np.testing.assert_allclose(s, exp, rtol=1e-15)
+    out = P.mcmc_nngp_predict_fixed_effects(L, Xp, burn_in=0.5, add_intercept=True)
+    s = out["predicted_fixed_effects_samples"][0]
+    b0 = beta0[2:, 0] - beta[2:] @ np.array([10.0, 20.0])
+    exp2 = np.column_stack([b0, b0]) + exp
+    np.testing.assert_allclose(s, exp2, rtol=1e-14)
+
+
+def test_predict_oracle_reuses_factor_like_predict_R(O):
+    """The oracle's predict.R restatement recomputes the factor only at the
+    first appearance of a shape (!duplicated, predict.R:23,32): a later return
+    to an earlier shape keeps the most recent factor (a reference quirk)."""
+    rng = np.random.default_rng(0)
+    n, m = 60, 4
+    locs = rng.uniform(size=(n, 2))
+    pred = rng.uniform(size=(7, 2))
+    a, b = np.log(0.3), np.log(0.1)
+    fields = rng.normal(size=(3, n))
+    L = {"locs": locs, "space_time_model": {"covfun": {"stationary_covfun": "exponential_isotropic",
+                                                       "shape_params": ["log_range"]}},
+         "records": {"chain_1": {"saved_field": np.array([1.0, 2.0, 3.0]),
+                                 "params": {"shape": np.array([[a], [b], [a]]), "log_scale": np.zeros((3, 1)),
+                                            "beta_0": np.zeros((3, 1)), "field": fields}}}}
+    z = [rng.normal(size=(3, 7))]
+    got = O.predict_field(L, pred, z, burn_in=0.0, m=m)[0]
+    allloc = np.vstack([locs, pred])
+    NN = O.find_ordered_nn(allloc, m)
+    Lb = O.vecchia_linv("exponential_isotropic", [1.0, np.exp(b), 0.0], allloc, NN)
+    u = O.linv_mult(Lb, np.concatenate([fields[2], np.zeros(7)]), NN)[:n]
+    x = O.tri_solve(Lb, NN, np.concatenate([u, z[0][2]]))
+    np.testing.assert_allclose(got[2], x[n:], rtol=1e-13, atol=1e-13)
+    # and the dense form: B x = c(B11 w, z)
+    B = O.dense_B(Lb, NN)
+    np.testing.assert_allclose(B @ x, np.concatenate([B[:n, :n] @ fields[2], z[0][2]]), atol=1e-10)

@@ -502,7 +502,7 @@ def test_configs1_synthetic_1e5_m10_exponential(P, O):
 
 def test_headline_size_1e6_m15_three_chains(P, O):
     """The headline workload itself (n = 1e6, m = 15, Matern 3/2, 3 chains in
-    one context, the default engine): chain 1's field after one call of 2
+    one context, the default engine): every chain's field after one call of 2
     sweeps against the oracle's local-form sweep with the same Philox normals
     and the device's own factor (isolates the sweep), its log-likelihood
     against the oracle's on that factor (1e-10), and the factor against the
@@ -520,17 +520,26 @@ def test_headline_size_1e6_m15_three_chains(P, O):
             ctx.factor(0, "matern15_isotropic", cps[k])
             ctx.set_field(fields[k])
             ctx.set_mu(None, 0.1 * k)
+        Ls = []
+        for k in range(C):
+            ctx.select(k)
+            Ls.append(ctx.get_linv(0))
         ctx.select(1)
-        L1 = ctx.get_linv(0)
+        L1 = Ls[1]
         ll = ctx.loglik(0, 0.1, 0.2)
-        ctx.sweep_chains(2, [0.0, 0.1, 0.2], [0.0, 0.2, -0.1], [-0.5, -0.4, -0.6], [11, 12, 13], [0, 0, 0])
-        got = ctx.get_field()
+        b0s, lss, lnvs, seeds = [0.0, 0.1, 0.2], [0.0, 0.2, -0.1], [-0.5, -0.4, -0.6], [11, 12, 13]
+        ctx.sweep_chains(2, b0s, lss, lnvs, seeds, [0, 0, 0])
+        got = []
+        for k in range(C):
+            ctx.select(k)
+            got.append(ctx.get_field())
     llo = O.loglik(L1, fields[1] - 0.1, NN, 0.2)
     assert abs(ll - llo) <= 1e-10 * abs(llo)
-    z = O.sweep_normals(12, 0, 2, n)
-    ref = O.sweep("local", fields[1], L1, NN, col, O.precision_diag(L1, NN), np.ones(n, np.int32), y,
-                  np.full(n, 0.1), lm, 0.1, 0.2, -0.4, z)
-    np.testing.assert_allclose(got, ref, rtol=1e-8, atol=1e-9)
+    for k in range(C):  # every chain of the batched call
+        z = O.sweep_normals(seeds[k], 0, 2, n)
+        ref = O.sweep("local", fields[k], Ls[k], NN, col, O.precision_diag(Ls[k], NN), np.ones(n, np.int32), y,
+                      np.full(n, 0.1 * k), lm, b0s[k], lss[k], lnvs[k], z)
+        np.testing.assert_allclose(got[k], ref, rtol=1e-8, atol=1e-9, err_msg=f"chain {k}")
     Lo = O.vecchia_linv("matern15_isotropic", cps[1], locs, NN)
     err = np.abs(L1 - Lo).max(axis=1)
     scale = np.abs(Lo).max(axis=1)

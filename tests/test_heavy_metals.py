@@ -37,15 +37,17 @@ def test_model_matrix_has_r_treatment_contrasts(P, heavy):
 
 
 @pytest.mark.gpu
-def test_heavy_metals_device_path_matches_oracle(P, O, heavy):
-    """exponential_sphere, m = 5 on the real locations: the device factor,
-    one chromatic sweep and a few full Gibbs iterations (with the 156-column
-    design and interweaving) agree with the oracle."""
+@pytest.mark.parametrize("m", [5, 10])
+def test_heavy_metals_device_path_matches_oracle(P, O, heavy, m):
+    """exponential_sphere on the real locations, m = 5 (the paper run,
+    run_script.R:8-12) and m = 10 (BASELINE configs[2]): the device factor and
+    a few full Gibbs iterations (with the 156-column design and interweaving)
+    agree with the oracle."""
     import mcmc_oracle as MO
     from nngp_amd.update_gaussian import _philox_key, _run_chain
 
     L = P.mcmc_nngp_initialize(heavy["observed_locs"], heavy["observed_field"], X_locs=heavy["X_locs"],
-                               stationary_covfun="exponential_sphere", m=5, n_chains=1, seed=1)
+                               stationary_covfun="exponential_sphere", m=m, n_chains=1, seed=1)
     va, st = L["vecchia_approx"], L["states"]["chain_1"]
     ctx = L["_contexts"][0]
     assert va["n_locs"] == 58097 and L["X"]["X"].shape[1] == 156
