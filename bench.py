@@ -95,12 +95,12 @@ def cpu_baseline(P, wl, covfun, cp, budget_s, chains):
     mu = np.full(n, wl["beta0"])
     z = O.sweep_normals(3, 0, 1, n)
 
-    def run(form, out, k):
+    def run(form, out, k, threads=1):
         field = np.asarray(wl["field0"]).copy()
         done, t0 = 0, time.time()
         while True:
             field = O.sweep(form, field, Lo, wl["NN"], wl["col"], D, opl, wl["y"], mu, wl["lm"], wl["beta0"],
-                            wl["log_scale"], wl["log_noise_variance"], z)
+                            wl["log_scale"], wl["log_noise_variance"], z, threads=threads)
             done += 1
             if time.time() - t0 > budget_s / 2 or done >= 20:
                 break
@@ -113,15 +113,27 @@ def cpu_baseline(P, wl, covfun, cp, budget_s, chains):
     for x in th:
         x.join()
     masked = sum(d / el for d, el in res)
-    loc = [None]
+    # one chain on all the host cores the process may use (OMP_NUM_THREADS on
+    # the GPU box), masked form and the optimised local form
+    host_cpus = os.cpu_count() or 1
+    omp = max(1, min(64, int(os.environ.get("OMP_NUM_THREADS") or host_cpus)))
+    one, locmt, loc = [None], [None], [None]
+    run("masked", one, 0, omp)
+    run("local", locmt, 0, omp)
     run("local", loc, 0)
+    rate = lambda r: r[0][0] / r[0][1]  # noqa: E731
     return {"value": masked, "unit": "sweeps/s", "cores": chains, "kind": "port",
             "sample": (f"oracle C restatement of the reference's masked-form chromatic sweep "
                        f"(update_Gaussian.R:257-275), {chains} chains on {chains} host threads (the reference's "
                        f"mclapply over chains), same n={n} workload, whole sweeps until ~{budget_s / 2:.0f}s each "
-                       f"({sum(d for d, _ in res)} sweeps); local-form oracle 1 thread "
-                       f"{loc[0][0] / loc[0][1]:.3g} sweeps/s; oracle factor build {t_factor:.1f}s"),
-            "local_form_value_1_thread": loc[0][0] / loc[0][1]}
+                       f"({sum(d for d, _ in res)} sweeps); 1 chain x {omp} OpenMP threads: masked form "
+                       f"{rate(one):.3g}, local form {rate(locmt):.3g} sweeps/s; local form 1 thread "
+                       f"{rate(loc):.3g} sweeps/s; oracle factor build {t_factor:.1f}s; host os.cpu_count() "
+                       f"{host_cpus}"),
+            "host_cpus": host_cpus,
+            "one_chain_all_cores": {"value": rate(one), "threads": omp, "form": "masked"},
+            "local_form_all_cores": {"value": rate(locmt), "threads": omp, "form": "local"},
+            "local_form_value_1_thread": rate(loc)}
 
 
 def mcmc_iterations(P, wl, covfun, cp, ctx, iters, warmup, sync):

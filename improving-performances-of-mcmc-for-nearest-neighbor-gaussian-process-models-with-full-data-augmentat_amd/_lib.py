@@ -16,6 +16,8 @@ import numpy as np
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("NNGP_LIB", PKG_DIR / "libnngp.so"))
 NA_INTEGER = -(2 ** 31)
+# nngp_status (include/nngp.h)
+NNGP_OK, NNGP_ERR_ARG, NNGP_ERR_HIP, NNGP_ERR_CHOL, NNGP_ERR_STATE, NNGP_ERR_NOMEM, NNGP_ERR_NODEV, NNGP_ERR_COMM = range(8)
 
 COVFUNS = {
     "exponential_isotropic": 0, "exponential_sphere": 1, "exponential_scaledim": 2,

@@ -12,7 +12,7 @@ from .update_gaussian import mcmc_nngp_update_Gaussian
 
 def mcmc_nngp_run(mcmc_nngp_list, Gelman_Rubin_Brooks_stop=(1.1, 1.1), burn_in=0.5, n_cores=None,
                   field_thinning=1.0, n_iterations_update=200, ancillary=True, n_chromatic=10,
-                  save_name=None, n_cycles=1, plot_beta=False, verbose=True):
+                  save_name=None, n_cycles=1, plot_beta=False, verbose=True, on_chol_error="error"):
     L = mcmc_nngp_list
     cycle = 1
     while cycle <= n_cycles:
@@ -26,7 +26,8 @@ def mcmc_nngp_run(mcmc_nngp_list, Gelman_Rubin_Brooks_stop=(1.1, 1.1), burn_in=0
             space_time_model=L["space_time_model"], vecchia_approx=L["vecchia_approx"],
             states=L["states"], iterations=first["iterations"],  # chain 1's matrix for all (run.R:16)
             n_iterations_update=n_iterations_update, n_cores=n_cores, field_thinning=field_thinning,
-            ancillary=ancillary, n_chromatic=n_chromatic, contexts=L.get("_contexts"), seed=L.get("seed", 1))
+            ancillary=ancillary, n_chromatic=n_chromatic, contexts=L.get("_contexts"), seed=L.get("seed", 1),
+            on_chol_error=on_chol_error)
         for name, rec in L["records"].items():
             L["states"][name] = res[name]["state"]
             iter_start = rec["iterations"][-1, 0]

@@ -37,7 +37,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from ._lib import NNGPError
+from ._lib import NNGP_ERR_CHOL, NNGPError
 from .context import ChainContext, make_chain_views
 from .model import covparms
 
@@ -61,8 +61,23 @@ def _interweave_prep(ctx, X, va):
     return {"Xl": Xl, "SX": SX, "covmat": cov, "covmat_chol": np.linalg.cholesky(cov).T}
 
 
+def _propose_factor(ctx, covfun, cp, on_chol_error):
+    """vecchia_Linv of a proposal (update_Gaussian.R:123,179).  In the
+    reference a local covariance that is not positive definite makes GpGp
+    raise an R error, which ends the update call (on_chol_error="error", the
+    default); on_chol_error="reject" treats the proposal as rejected instead.
+    Any other failure (HIP, memory, a timeout) always propagates."""
+    try:
+        ctx.factor(1, covfun, cp)
+        return True
+    except NNGPError as e:
+        if e.status == NNGP_ERR_CHOL and on_chol_error == "reject":
+            return False
+        raise
+
+
 def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_iterations_update,
-                   field_thinning, ancillary, n_chromatic, iter_start, seed):
+                   field_thinning, ancillary, n_chromatic, iter_start, seed, on_chol_error="error"):
     """Chain i's n_iterations_update Gibbs iterations; yields its device
     requests -- ("anc", beta_0, dlog_scale, ok) for the ancillary proposal and
     ("sweep", n_sweeps, beta_0, log_scale, log_noise_variance, key, counter)
@@ -117,11 +132,7 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
             innov = rng.normal(0.0, np.exp(0.5 * tk["covariance_params_ancillary"]["logvar"]), n_shape + 1)
             new_ls = params["log_scale"] + innov[0]
             new_shape = params["shape"] + innov[1:]
-            ok = True
-            try:
-                ctx.factor(1, covfun, covparms(sp_names, new_shape))
-            except Exception:
-                ok = False  # non-PD local covariance: the proposal is rejected
+            ok = _propose_factor(ctx, covfun, covparms(sp_names, new_shape), on_chol_error)
             # every chain stops here each iteration (ok=False: nothing to
             # propose) so the chains of one context stay in lockstep
             yield ("anc", params["beta_0"], new_ls - params["log_scale"], ok)
@@ -147,11 +158,7 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
         new_ls = params["log_scale"] + innov[0]
         if np.exp(new_ls) < var_y:
             new_shape = params["shape"] + innov[1:]
-            ok = True
-            try:
-                ctx.factor(1, covfun, covparms(sp_names, new_shape))
-            except Exception:
-                ok = False
+            ok = _propose_factor(ctx, covfun, covparms(sp_names, new_shape), on_chol_error)
             if ok:
                 gp_ratio = (ctx.loglik(1, params["beta_0"], new_ls)
                             - ctx.loglik(0, params["beta_0"], params["log_scale"]))
@@ -241,10 +248,10 @@ def _serve_one(ctx, req):
 
 
 def _run_chain(i, state, ctx, X, observed_field, space_time_model, va, n_iterations_update,
-               field_thinning, ancillary, n_chromatic, iter_start, seed):
+               field_thinning, ancillary, n_chromatic, iter_start, seed, on_chol_error="error"):
     """One chain alone (each request served on its own)."""
     prog = _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_iterations_update,
-                          field_thinning, ancillary, n_chromatic, iter_start, seed)
+                          field_thinning, ancillary, n_chromatic, iter_start, seed, on_chol_error)
     try:
         req = next(prog)
         while True:
@@ -316,8 +323,13 @@ def _drive(programs, contexts):
 
 def mcmc_nngp_update_Gaussian(locs, X, observed_field, space_time_model, vecchia_approx, states,
                               n_iterations_update, n_cores=None, field_thinning=1.0, ancillary=True,
-                              n_chromatic=10, iterations=None, contexts=None, seed=1, devices=None):
-    """Returns one {"state", "records"} per chain (update_Gaussian.R:315)."""
+                              n_chromatic=10, iterations=None, contexts=None, seed=1, devices=None,
+                              on_chol_error="error"):
+    """Returns one {"state", "records"} per chain (update_Gaussian.R:315).
+    on_chol_error: "error" (GpGp's behaviour: a non positive definite local
+    covariance of a proposal raises) or "reject" (the proposal is rejected)."""
+    if on_chol_error not in ("error", "reject"):
+        raise ValueError("on_chol_error must be 'error' or 'reject'")
     iter_start = int(iterations[-1, 0]) if iterations is not None else 0
     names = list(states.keys()) if isinstance(states, dict) else [f"chain_{i + 1}" for i in range(len(states))]
     st_list = list(states.values()) if isinstance(states, dict) else list(states)
@@ -327,6 +339,6 @@ def mcmc_nngp_update_Gaussian(locs, X, observed_field, space_time_model, vecchia
     y = np.asarray(observed_field, np.float64)
     programs = [_chain_program(i, st, contexts[i], X, y, space_time_model, vecchia_approx,
                                int(n_iterations_update), float(field_thinning), bool(ancillary),
-                               int(n_chromatic), iter_start, seed)
+                               int(n_chromatic), iter_start, seed, on_chol_error)
                 for i, st in enumerate(st_list)]
     return dict(zip(names, _drive(programs, contexts)))

@@ -430,6 +430,131 @@ void or_sweep_local(int n_sweeps, const double *Linv, const int *NN, int n, int 
 }
 
 /* ------------------------------------------------------------------ */
+/* Multi-threaded forms (OpenMP) of the two sweeps above, for the CPU     */
+/* baseline "one chain on all host cores" (BASELINE.md).  Bitwise equal   */
+/* to the serial forms: every output element is summed by one thread in   */
+/* the serial order (columns of B are walked with rows ascending, as the  */
+/* serial crossprod adds them), and within a colour the local form's     */
+/* row updates are disjoint (each Vecchia row is a moral clique).         */
+/* ------------------------------------------------------------------ */
+static void or_csc(const double *Linv, const int *NN, int n, int b, int **cnt_o, int **crow_o, double **cval_o) {
+  int *cnt = (int *)calloc((size_t)n + 1, sizeof(int));
+  for (int k = 0; k < n; ++k)
+    for (int j = 0; j < b; ++j) {
+      int idx = NN[k + (size_t)j * n];
+      if (idx != OR_NA) cnt[idx]++;
+    }
+  for (int i = 0; i < n; ++i) cnt[i + 1] += cnt[i];
+  int *crow = (int *)malloc(sizeof(int) * (size_t)cnt[n]);
+  double *cval = (double *)malloc(sizeof(double) * (size_t)cnt[n]);
+  int *fill = (int *)malloc(sizeof(int) * (size_t)n);
+  memcpy(fill, cnt, sizeof(int) * (size_t)n);
+  for (int k = 0; k < n; ++k)
+    for (int j = 0; j < b; ++j) {
+      int idx = NN[k + (size_t)j * n];
+      if (idx == OR_NA) continue;
+      int p = fill[idx - 1]++;
+      crow[p] = k; cval[p] = Linv[k + (size_t)j * n];
+    }
+  free(fill);
+  *cnt_o = cnt; *crow_o = crow; *cval_o = cval;
+}
+
+static void or_colour_lists(const int *coloring, int n, int *K_o, int **cptr_o, int **clist_o) {
+  int K = 0;
+  for (int i = 0; i < n; ++i) if (coloring[i] > K) K = coloring[i];
+  int *cptr = (int *)calloc((size_t)K + 2, sizeof(int));
+  for (int i = 0; i < n; ++i) cptr[coloring[i] + 1]++;
+  for (int c = 0; c <= K; ++c) cptr[c + 1] += cptr[c];
+  int *clist = (int *)malloc(sizeof(int) * (size_t)n);
+  int *cfill = (int *)malloc(sizeof(int) * ((size_t)K + 1));
+  memcpy(cfill, cptr, sizeof(int) * ((size_t)K + 1));
+  for (int i = 0; i < n; ++i) clist[cfill[coloring[i]]++] = i;
+  free(cfill);
+  *K_o = K; *cptr_o = cptr; *clist_o = clist;
+}
+
+void or_sweep_masked_mt(int nthreads, int n_sweeps, const double *Linv, const int *NN, int n, int b,
+                        const int *coloring, const double *D, const int *obs_per_loc,
+                        const double *y, const double *mu, const int *locs_match, int n_obs,
+                        double beta0, double log_scale, double log_noise_var,
+                        const double *z, double *field) {
+  int K, *cptr, *clist, *cnt, *crow;
+  double *cval;
+  or_colour_lists(coloring, n, &K, &cptr, &clist);
+  or_csc(Linv, NN, n, b, &cnt, &crow, &cval);
+  double *R = (double *)malloc(sizeof(double) * (size_t)n);
+  double *w = (double *)malloc(sizeof(double) * (size_t)n);
+  double *v = (double *)malloc(sizeof(double) * (size_t)n);
+  double is2 = exp(-log_scale), it2 = exp(-log_noise_var);
+  for (int s = 0; s < n_sweeps; ++s) {
+    or_residuals_sum(y, mu, locs_match, n_obs, n, R);
+    for (int c = 1; c <= K; ++c) {
+#pragma omp parallel num_threads(nthreads)
+      {
+#pragma omp for schedule(static)
+        for (int i = 0; i < n; ++i) w[i] = (coloring[i] != c) ? field[i] - beta0 : 0.0;
+#pragma omp for schedule(static)
+        for (int k = 0; k < n; ++k) {       /* B %*% (masked field), row k as or_linv_mult */
+          double u = 0.0;
+          for (int j = 0; j < b; ++j) {
+            int idx = NN[k + (size_t)j * n];
+            if (idx == OR_NA) continue;
+            u += Linv[k + (size_t)j * n] * w[idx - 1];
+          }
+          v[k] = u;
+        }
+#pragma omp for schedule(dynamic, 256)
+        for (int q = cptr[c]; q < cptr[c + 1]; ++q) {  /* crossprod(B[,sel], v), rows ascending */
+          int i = clist[q];
+          double t = 0.0;
+          for (int p = cnt[i]; p < cnt[i + 1]; ++p) t += cval[p] * v[crow[p]];
+          double P = is2 * D[i] + it2 * obs_per_loc[i];
+          double cm = beta0 - (1.0 / P) * (t * is2 - it2 * R[i]);
+          field[i] = cm + z[(size_t)s * n + i] / sqrt(P);
+        }
+      }
+    }
+  }
+  free(R); free(w); free(v); free(cptr); free(clist); free(cnt); free(crow); free(cval);
+}
+
+void or_sweep_local_mt(int nthreads, int n_sweeps, const double *Linv, const int *NN, int n, int b,
+                       const int *coloring, const double *D, const int *obs_per_loc,
+                       const double *y, const double *mu, const int *locs_match, int n_obs,
+                       double beta0, double log_scale, double log_noise_var,
+                       const double *z, double *field) {
+  int K, *cptr, *clist, *cnt, *crow;
+  double *cval;
+  or_colour_lists(coloring, n, &K, &cptr, &clist);
+  or_csc(Linv, NN, n, b, &cnt, &crow, &cval);
+  double *R = (double *)malloc(sizeof(double) * (size_t)n);
+  double *w = (double *)malloc(sizeof(double) * (size_t)n);
+  double *r = (double *)malloc(sizeof(double) * (size_t)n);
+  double is2 = exp(-log_scale), it2 = exp(-log_noise_var);
+  or_residuals_sum(y, mu, locs_match, n_obs, n, R);
+  for (int i = 0; i < n; ++i) w[i] = field[i] - beta0;
+  or_linv_mult(Linv, w, NN, n, b, r);
+  for (int s = 0; s < n_sweeps; ++s)
+    for (int c = 1; c <= K; ++c) {
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 256)
+      for (int q = cptr[c]; q < cptr[c + 1]; ++q) {
+        int i = clist[q];
+        double acc = 0;
+        for (int p = cnt[i]; p < cnt[i + 1]; ++p) acc += cval[p] * r[crow[p]];
+        acc -= D[i] * w[i];
+        double P = is2 * D[i] + it2 * obs_per_loc[i];
+        double wn = (it2 * R[i] - is2 * acc) / P + z[(size_t)s * n + i] / sqrt(P);
+        double dw = wn - w[i];
+        w[i] = wn;
+        for (int p = cnt[i]; p < cnt[i + 1]; ++p) r[crow[p]] += cval[p] * dw;
+      }
+    }
+  for (int i = 0; i < n; ++i) field[i] = w[i] + beta0;
+  free(R); free(w); free(r); free(cptr); free(clist); free(cnt); free(crow); free(cval);
+}
+
+/* ------------------------------------------------------------------ */
 /* GpGp::find_ordered_nn restated (exact, no jitter): row i = [i, the m  */
 /* nearest j < i by ascending Euclidean distance on the raw coordinates, */
 /* ties broken by smaller index], NA-padded.  Brute force O(n^2 m).      */

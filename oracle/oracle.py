@@ -10,6 +10,7 @@ Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
 from __future__ import annotations
 
 import ctypes as C
+import functools
 import os
 import subprocess
 from pathlib import Path
@@ -64,6 +65,8 @@ def lib():
                       C.c_int, C.c_double, C.c_double, C.c_double, dp, dp]
         L.or_sweep_masked.argtypes = sweep_args
         L.or_sweep_local.argtypes = sweep_args
+        L.or_sweep_masked_mt.argtypes = [C.c_int] + sweep_args
+        L.or_sweep_local_mt.argtypes = [C.c_int] + sweep_args
         L.or_find_ordered_nn.argtypes = [dp, C.c_int, C.c_int, C.c_int, ip]
         L.or_greedy_coloring.restype = C.c_int
         L.or_greedy_coloring.argtypes = [ip, C.c_int, C.c_int, ip]
@@ -204,12 +207,17 @@ def tri_solve(Linv, NNarray, u) -> np.ndarray:
 
 
 def sweep(form: str, field, Linv, NNarray, coloring, D, obs_per_loc, y, mu, locs_match,
-          beta0, log_scale, log_noise_var, z) -> np.ndarray:
-    """n_sweeps = z.shape[0] chromatic sweeps; returns the new field."""
+          beta0, log_scale, log_noise_var, z, threads: int = 1) -> np.ndarray:
+    """n_sweeps = z.shape[0] chromatic sweeps; returns the new field.
+    threads > 1: the OpenMP forms (bitwise equal to the serial ones)."""
     n, b = NNarray.shape
     z = np.atleast_2d(np.asarray(z, np.float64))
     out = _f(field).copy()
-    fn = lib().or_sweep_masked if form == "masked" else lib().or_sweep_local
+    if threads > 1:
+        fn = lib().or_sweep_masked_mt if form == "masked" else lib().or_sweep_local_mt
+        fn = functools.partial(fn, int(threads))
+    else:
+        fn = lib().or_sweep_masked if form == "masked" else lib().or_sweep_local
     fn(z.shape[0], _colmajor(Linv, np.float64), _colmajor(NNarray, np.int32), n, b, _i(coloring),
        _f(D), _i(obs_per_loc), _f(y), _f(mu), _i(locs_match), len(y), float(beta0),
        float(log_scale), float(log_noise_var), np.ascontiguousarray(z), out)

@@ -1,0 +1,433 @@
+/*
+ * nngp_shim.c -- R .Call shim over the C ABI of include/nngp.h.
+ *
+ * One .Call entry point per nngp.h function (R_registerRoutines below), so
+ * the R host code of the reference (Scripts/mcmc_nngp_*.R) can drive the
+ * MI355X hot path.  Conventions:
+ *  - a context is an external pointer with a finalizer (nngp_ctx_destroy);
+ *  - R's own arrays cross unchanged (column-major, 1-based, NA_integer_ ==
+ *    INT_MIN), integers as INTSXP, reals as REALSXP; uint64 seeds / counters
+ *    arrive as doubles (exact below 2^53);
+ *  - a non-zero nngp_status becomes Rf_error with the context's message.
+ *    The library is C/C++ behind a C ABI and has returned before Rf_error
+ *    runs, so no longjmp crosses a C++ frame; temporaries are R-allocated.
+ *  - HIP must not be initialised before a fork(): the R side replaces
+ *    parallel::mclapply over chains (update_Gaussian.R:25-26) by contexts
+ *    holding up to 4 chains each.
+ */
+#include <R.h>
+#include <Rinternals.h>
+#include <R_ext/Rdynload.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "nngp.h"
+
+static SEXP ctx_tag(void) { return Rf_install("nngp_ctx"); }
+
+static void ctx_finalizer(SEXP p) {
+  nngp_ctx* c = (nngp_ctx*)R_ExternalPtrAddr(p);
+  if (c) {
+    nngp_ctx_destroy(c);
+    R_ClearExternalPtr(p);
+  }
+}
+
+static SEXP wrap_ctx(nngp_ctx* c) {
+  SEXP p = PROTECT(R_MakeExternalPtr(c, ctx_tag(), R_NilValue));
+  R_RegisterCFinalizerEx(p, ctx_finalizer, TRUE);
+  UNPROTECT(1);
+  return p;
+}
+
+static nngp_ctx* get_ctx(SEXP p) {
+  if (TYPEOF(p) != EXTPTRSXP || R_ExternalPtrTag(p) != ctx_tag()) Rf_error("nngp: not a context");
+  nngp_ctx* c = (nngp_ctx*)R_ExternalPtrAddr(p);
+  if (!c) Rf_error("nngp: the context was destroyed");
+  return c;
+}
+
+/* status -> R error (message copied first: the context may be gone after) */
+static void check(int st, const nngp_ctx* c) {
+  if (st == NNGP_OK) return;
+  char msg[512];
+  const char* m = c ? nngp_ctx_last_error(c) : NULL;
+  snprintf(msg, sizeof msg, "nngp: %s%s%s", nngp_status_string(st), (m && m[0]) ? ": " : "", m ? m : "");
+  Rf_error("%s (status %d)", msg, st);
+}
+
+static int as_int(SEXP x) { return Rf_asInteger(x); }
+static double as_real(SEXP x) { return Rf_asReal(x); }
+static const double* rptr(SEXP x) { return TYPEOF(x) == NILSXP ? NULL : REAL(x); }
+
+static void to_u64(SEXP x, uint64_t* out, int n) {
+  if (XLENGTH(x) < n) Rf_error("nngp: need %d seeds / counters", n);
+  for (int k = 0; k < n; ++k) out[k] = (uint64_t)REAL(x)[k];
+}
+
+/* ---------- library ---------- */
+SEXP C_nngp_abi_version(void) { return Rf_ScalarInteger(nngp_abi_version()); }
+SEXP C_nngp_status_string(SEXP st) { return Rf_mkString(nngp_status_string(as_int(st))); }
+
+/* ---------- graph preparation ---------- */
+SEXP C_nngp_order_maxmin(SEXP locs) {
+  int n = Rf_nrows(locs), d = Rf_ncols(locs);
+  SEXP o = PROTECT(Rf_allocVector(INTSXP, n));
+  check(nngp_order_maxmin(REAL(locs), n, d, INTEGER(o)), NULL);
+  UNPROTECT(1);
+  return o;
+}
+
+SEXP C_nngp_find_ordered_nn(SEXP locs, SEXP m) {
+  int n = Rf_nrows(locs), d = Rf_ncols(locs), mm = as_int(m);
+  SEXP nn = PROTECT(Rf_allocMatrix(INTSXP, n, mm + 1));
+  check(nngp_find_ordered_nn(REAL(locs), n, d, mm, INTEGER(nn)), NULL);
+  UNPROTECT(1);
+  return nn;
+}
+
+SEXP C_nngp_greedy_coloring(SEXP NNarray) {
+  int n = Rf_nrows(NNarray), b = Rf_ncols(NNarray), K = 0;
+  SEXP col = PROTECT(Rf_allocVector(INTSXP, n));
+  check(nngp_greedy_coloring(INTEGER(NNarray), n, b, INTEGER(col), &K), NULL);
+  UNPROTECT(1);
+  return col;
+}
+
+/* ---------- contexts ---------- */
+SEXP C_nngp_ctx_create(SEXP locs, SEXP NNarray, SEXP coloring, SEXP locs_match, SEXP y, SEXP n_chains,
+                       SEXP device) {
+  nngp_ctx* c = NULL;
+  check(nngp_ctx_create(REAL(locs), Rf_nrows(locs), Rf_ncols(locs), INTEGER(NNarray), Rf_ncols(NNarray),
+                        INTEGER(coloring), INTEGER(locs_match), REAL(y), (int)XLENGTH(y), as_int(n_chains),
+                        as_int(device), &c),
+        NULL);
+  return wrap_ctx(c);
+}
+
+SEXP C_nngp_ctx_create_shard(SEXP locs, SEXP NNarray, SEXP coloring, SEXP locs_match, SEXP y, SEXP n_chains,
+                             SEXP device, SEXP n_ranks, SEXP rank) {
+  nngp_ctx* c = NULL;
+  check(nngp_ctx_create_shard(REAL(locs), Rf_nrows(locs), Rf_ncols(locs), INTEGER(NNarray), Rf_ncols(NNarray),
+                              INTEGER(coloring), INTEGER(locs_match), REAL(y), (int)XLENGTH(y),
+                              as_int(n_chains), as_int(device), as_int(n_ranks), as_int(rank), &c),
+        NULL);
+  return wrap_ctx(c);
+}
+
+SEXP C_nngp_ctx_destroy(SEXP p) {
+  ctx_finalizer(p);
+  return R_NilValue;
+}
+
+SEXP C_nngp_ctx_last_error(SEXP p) { return Rf_mkString(nngp_ctx_last_error(get_ctx(p))); }
+
+SEXP C_nngp_set_chain(SEXP p, SEXP chain) {
+  nngp_ctx* c = get_ctx(p);
+  check(nngp_set_chain(c, as_int(chain)), c);
+  return R_NilValue;
+}
+
+SEXP C_nngp_ctx_info(SEXP p) {
+  nngp_ctx* c = get_ctx(p);
+  nngp_info inf;
+  check(nngp_ctx_info(c, &inf), c);
+  const char* nm[] = {"n", "b", "d", "n_obs", "n_colors", "n_levels", "nnz", "n_entries", "max_collen", "device",
+                      "n_chains", "lanes_per_chain", "n_chunks", "sweep_engine", "n_tiles", "tile_rows_max",
+                      "n_ghost_cells", "n_ranks", "rank", "shard_owned", "shard_needed_rows",
+                      "shard_exchange_slots"};
+  const double v[] = {inf.n, inf.b, inf.d, inf.n_obs, inf.n_colors, inf.n_levels, (double)inf.nnz,
+                      (double)inf.n_entries, inf.max_collen, inf.device, inf.n_chains, inf.lanes_per_chain,
+                      inf.n_chunks, inf.sweep_engine, inf.n_tiles, inf.tile_rows_max, (double)inf.n_ghost_cells,
+                      inf.n_ranks, inf.rank, (double)inf.shard_owned, (double)inf.shard_needed_rows,
+                      (double)inf.shard_exchange_slots};
+  const int k = (int)(sizeof v / sizeof v[0]);
+  SEXP out = PROTECT(Rf_allocVector(REALSXP, k)), names = PROTECT(Rf_allocVector(STRSXP, k));
+  for (int i = 0; i < k; ++i) {
+    REAL(out)[i] = v[i];
+    SET_STRING_ELT(names, i, Rf_mkChar(nm[i]));
+  }
+  Rf_setAttrib(out, R_NamesSymbol, names);
+  UNPROTECT(2);
+  return out;
+}
+
+/* ---------- factor (A4/A5) ---------- */
+SEXP C_nngp_factor(SEXP p, SEXP which, SEXP covfun, SEXP covparms) {
+  nngp_ctx* c = get_ctx(p);
+  check(nngp_factor(c, as_int(which), as_int(covfun), REAL(covparms), (int)XLENGTH(covparms)), c);
+  return R_NilValue;
+}
+
+SEXP C_nngp_get_linv(SEXP p, SEXP which) {
+  nngp_ctx* c = get_ctx(p);
+  nngp_info inf;
+  check(nngp_ctx_info(c, &inf), c);
+  SEXP L = PROTECT(Rf_allocMatrix(REALSXP, inf.n, inf.b));
+  check(nngp_get_linv(c, as_int(which), REAL(L)), c);
+  UNPROTECT(1);
+  return L;
+}
+
+SEXP C_nngp_set_linv(SEXP p, SEXP which, SEXP Linv) {
+  nngp_ctx* c = get_ctx(p);
+  check(nngp_set_linv(c, as_int(which), REAL(Linv)), c);
+  return R_NilValue;
+}
+
+SEXP C_nngp_accept_factor(SEXP p) {
+  nngp_ctx* c = get_ctx(p);
+  check(nngp_accept_factor(c), c);
+  return R_NilValue;
+}
+
+static int ctx_n(nngp_ctx* c) {
+  nngp_info inf;
+  check(nngp_ctx_info(c, &inf), c);
+  return inf.n;
+}
+
+SEXP C_nngp_get_precision_diag(SEXP p) {
+  nngp_ctx* c = get_ctx(p);
+  SEXP D = PROTECT(Rf_allocVector(REALSXP, ctx_n(c)));
+  check(nngp_get_precision_diag(c, REAL(D)), c);
+  UNPROTECT(1);
+  return D;
+}
+
+/* ---------- state ---------- */
+SEXP C_nngp_set_field(SEXP p, SEXP field) {
+  nngp_ctx* c = get_ctx(p);
+  check(nngp_set_field(c, REAL(field)), c);
+  return R_NilValue;
+}
+
+SEXP C_nngp_get_field(SEXP p) {
+  nngp_ctx* c = get_ctx(p);
+  SEXP f = PROTECT(Rf_allocVector(REALSXP, ctx_n(c)));
+  check(nngp_get_field(c, REAL(f)), c);
+  UNPROTECT(1);
+  return f;
+}
+
+SEXP C_nngp_set_mu(SEXP p, SEXP mu, SEXP beta0) {
+  nngp_ctx* c = get_ctx(p);
+  check(nngp_set_mu(c, rptr(mu), as_real(beta0)), c);
+  return R_NilValue;
+}
+
+SEXP C_nngp_records_reserve(SEXP p, SEXP n_rows) {
+  nngp_ctx* c = get_ctx(p);
+  check(nngp_records_reserve(c, as_int(n_rows)), c);
+  return R_NilValue;
+}
+
+SEXP C_nngp_record_field(SEXP p, SEXP row) {
+  nngp_ctx* c = get_ctx(p);
+  check(nngp_record_field(c, as_int(row)), c);
+  return R_NilValue;
+}
+
+/* rows [row0, row0 + n_rows) as an n_rows x n matrix (records$field layout) */
+SEXP C_nngp_get_records(SEXP p, SEXP row0, SEXP n_rows) {
+  nngp_ctx* c = get_ctx(p);
+  const int n = ctx_n(c), r = as_int(n_rows);
+  SEXP tmp = PROTECT(Rf_allocVector(REALSXP, (R_xlen_t)r * n));  /* row-major from the library */
+  check(nngp_get_records(c, as_int(row0), r, REAL(tmp)), c);
+  SEXP out = PROTECT(Rf_allocMatrix(REALSXP, r, n));
+  for (int i = 0; i < r; ++i)
+    for (int j = 0; j < n; ++j) REAL(out)[i + (R_xlen_t)j * r] = REAL(tmp)[(R_xlen_t)i * n + j];
+  UNPROTECT(2);
+  return out;
+}
+
+/* ---------- kernels ---------- */
+SEXP C_nngp_loglik(SEXP p, SEXP which, SEXP beta0, SEXP log_scale) {
+  nngp_ctx* c = get_ctx(p);
+  double ll = 0;
+  check(nngp_loglik(c, as_int(which), as_real(beta0), as_real(log_scale), &ll), c);
+  return Rf_ScalarReal(ll);
+}
+
+SEXP C_nngp_sweep(SEXP p, SEXP n_sweeps, SEXP beta0, SEXP log_scale, SEXP lnv, SEXP seed, SEXP counter_base,
+                  SEXP z) {
+  nngp_ctx* c = get_ctx(p);
+  check(nngp_sweep(c, as_int(n_sweeps), as_real(beta0), as_real(log_scale), as_real(lnv),
+                   (uint64_t)as_real(seed), (uint64_t)as_real(counter_base), rptr(z)),
+        c);
+  return R_NilValue;
+}
+
+SEXP C_nngp_sweep_chains(SEXP p, SEXP n_sweeps, SEXP beta0, SEXP log_scale, SEXP lnv, SEXP seed,
+                         SEXP counter_base) {
+  nngp_ctx* c = get_ctx(p);
+  uint64_t s[4], cb[4];
+  const int k = (int)XLENGTH(beta0);
+  if (k < 1 || k > 4) Rf_error("nngp: 1..4 chains per context");
+  to_u64(seed, s, k);
+  to_u64(counter_base, cb, k);
+  check(nngp_sweep_chains(c, as_int(n_sweeps), REAL(beta0), REAL(log_scale), REAL(lnv), s, cb), c);
+  return R_NilValue;
+}
+
+SEXP C_nngp_sweep_timed(SEXP p, SEXP n_sweeps, SEXP beta0, SEXP log_scale, SEXP lnv, SEXP seed,
+                        SEXP counter_base) {
+  nngp_ctx* c = get_ctx(p);
+  uint64_t s[4], cb[4];
+  const int k = (int)XLENGTH(beta0);
+  if (k < 1 || k > 4) Rf_error("nngp: 1..4 chains per context");
+  to_u64(seed, s, k);
+  to_u64(counter_base, cb, k);
+  double ms = 0, kms = 0;
+  check(nngp_sweep_timed(c, as_int(n_sweeps), REAL(beta0), REAL(log_scale), REAL(lnv), s, cb, &ms, &kms), c);
+  SEXP out = PROTECT(Rf_allocVector(REALSXP, 2));
+  REAL(out)[0] = ms;
+  REAL(out)[1] = kms;
+  UNPROTECT(1);
+  return out;
+}
+
+SEXP C_nngp_ancillary_propose(SEXP p, SEXP beta0, SEXP dlog_scale) {
+  nngp_ctx* c = get_ctx(p);
+  check(nngp_ancillary_propose(c, as_real(beta0), as_real(dlog_scale)), c);
+  return R_NilValue;
+}
+
+SEXP C_nngp_ancillary_propose_chains(SEXP p, SEXP chain_mask, SEXP beta0, SEXP dlog_scale) {
+  nngp_ctx* c = get_ctx(p);
+  check(nngp_ancillary_propose_chains(c, as_int(chain_mask), REAL(beta0), REAL(dlog_scale)), c);
+  return R_NilValue;
+}
+
+SEXP C_nngp_field_response_ratio(SEXP p, SEXP beta0, SEXP lnv) {
+  nngp_ctx* c = get_ctx(p);
+  double r = 0;
+  check(nngp_field_response_ratio(c, as_real(beta0), as_real(lnv), &r), c);
+  return Rf_ScalarReal(r);
+}
+
+SEXP C_nngp_accept_field(SEXP p) {
+  nngp_ctx* c = get_ctx(p);
+  check(nngp_accept_field(c), c);
+  return R_NilValue;
+}
+
+SEXP C_nngp_beta0_stats(SEXP p) {
+  nngp_ctx* c = get_ctx(p);
+  SEXP out = PROTECT(Rf_allocVector(REALSXP, 2));
+  check(nngp_beta0_stats(c, REAL(out), REAL(out) + 1), c);
+  UNPROTECT(1);
+  return out;
+}
+
+SEXP C_nngp_sum_squared_residuals(SEXP p, SEXP beta0) {
+  nngp_ctx* c = get_ctx(p);
+  double ssr = 0;
+  check(nngp_sum_squared_residuals(c, as_real(beta0), &ssr), c);
+  return Rf_ScalarReal(ssr);
+}
+
+SEXP C_nngp_spmv(SEXP p, SEXP which, SEXP X) {
+  nngp_ctx* c = get_ctx(p);
+  const int n = ctx_n(c);
+  const int ncols = Rf_isMatrix(X) ? Rf_ncols(X) : 1;
+  if ((Rf_isMatrix(X) ? Rf_nrows(X) : (int)XLENGTH(X)) != n) Rf_error("nngp_spmv: X must have n rows");
+  SEXP Y = PROTECT(Rf_isMatrix(X) ? Rf_allocMatrix(REALSXP, n, ncols) : Rf_allocVector(REALSXP, n));
+  check(nngp_spmv(c, as_int(which), REAL(X), ncols, REAL(Y)), c);
+  UNPROTECT(1);
+  return Y;
+}
+
+SEXP C_nngp_tri_solve(SEXP p, SEXP which, SEXP u) {
+  nngp_ctx* c = get_ctx(p);
+  SEXP x = PROTECT(Rf_allocVector(REALSXP, ctx_n(c)));
+  check(nngp_tri_solve(c, as_int(which), REAL(u), REAL(x)), c);
+  UNPROTECT(1);
+  return x;
+}
+
+SEXP C_nngp_device_normals(SEXP device, SEXP seed, SEXP sweep, SEXP n) {
+  SEXP z = PROTECT(Rf_allocVector(REALSXP, as_int(n)));
+  check(nngp_device_normals(as_int(device), (uint64_t)as_real(seed), (uint64_t)as_real(sweep), as_int(n), REAL(z)),
+        NULL);
+  UNPROTECT(1);
+  return z;
+}
+
+/* ---------- colour-sharded sweep ---------- */
+SEXP C_nngp_shard_unique_id(void) {
+  SEXP id = PROTECT(Rf_allocVector(RAWSXP, NNGP_SHARD_ID_BYTES));
+  check(nngp_shard_unique_id(RAW(id), NNGP_SHARD_ID_BYTES), NULL);
+  UNPROTECT(1);
+  return id;
+}
+
+SEXP C_nngp_shard_comm_init(SEXP p, SEXP id) {
+  nngp_ctx* c = get_ctx(p);
+  check(nngp_shard_comm_init(c, RAW(id), (int)XLENGTH(id)), c);
+  return R_NilValue;
+}
+
+SEXP C_nngp_sweep_chains_group(SEXP ctxs, SEXP n_sweeps, SEXP beta0, SEXP log_scale, SEXP lnv, SEXP seed,
+                               SEXP counter_base) {
+  const int G = (int)XLENGTH(ctxs);
+  if (G < 1 || G > 64) Rf_error("nngp: 1..64 ranks");
+  nngp_ctx* cs[64];
+  for (int g = 0; g < G; ++g) cs[g] = get_ctx(VECTOR_ELT(ctxs, g));
+  uint64_t s[4], cb[4];
+  const int k = (int)XLENGTH(beta0);
+  if (k < 1 || k > 4) Rf_error("nngp: 1..4 chains per context");
+  to_u64(seed, s, k);
+  to_u64(counter_base, cb, k);
+  check(nngp_sweep_chains_group(cs, G, as_int(n_sweeps), REAL(beta0), REAL(log_scale), REAL(lnv), s, cb), cs[0]);
+  return R_NilValue;
+}
+
+/* ---------- registration ---------- */
+#define E(name, n) {#name, (DL_FUNC)&name, n}
+static const R_CallMethodDef call_methods[] = {
+    E(C_nngp_abi_version, 0),
+    E(C_nngp_status_string, 1),
+    E(C_nngp_order_maxmin, 1),
+    E(C_nngp_find_ordered_nn, 2),
+    E(C_nngp_greedy_coloring, 1),
+    E(C_nngp_ctx_create, 7),
+    E(C_nngp_ctx_create_shard, 9),
+    E(C_nngp_ctx_destroy, 1),
+    E(C_nngp_ctx_last_error, 1),
+    E(C_nngp_set_chain, 2),
+    E(C_nngp_ctx_info, 1),
+    E(C_nngp_factor, 4),
+    E(C_nngp_get_linv, 2),
+    E(C_nngp_set_linv, 3),
+    E(C_nngp_accept_factor, 1),
+    E(C_nngp_get_precision_diag, 1),
+    E(C_nngp_set_field, 2),
+    E(C_nngp_get_field, 1),
+    E(C_nngp_set_mu, 3),
+    E(C_nngp_records_reserve, 2),
+    E(C_nngp_record_field, 2),
+    E(C_nngp_get_records, 3),
+    E(C_nngp_loglik, 4),
+    E(C_nngp_sweep, 8),
+    E(C_nngp_sweep_chains, 7),
+    E(C_nngp_sweep_timed, 7),
+    E(C_nngp_ancillary_propose, 3),
+    E(C_nngp_ancillary_propose_chains, 4),
+    E(C_nngp_field_response_ratio, 3),
+    E(C_nngp_accept_field, 1),
+    E(C_nngp_beta0_stats, 1),
+    E(C_nngp_sum_squared_residuals, 2),
+    E(C_nngp_spmv, 3),
+    E(C_nngp_tri_solve, 3),
+    E(C_nngp_device_normals, 4),
+    E(C_nngp_shard_unique_id, 0),
+    E(C_nngp_shard_comm_init, 2),
+    E(C_nngp_sweep_chains_group, 7),
+    {NULL, NULL, 0}};
+#undef E
+
+void R_init_nngpamd(DllInfo* dll) {
+  R_registerRoutines(dll, NULL, call_methods, NULL, NULL);
+  R_useDynamicSymbols(dll, FALSE);
+}

@@ -232,3 +232,90 @@ def test_predict_oracle_reuses_factor_like_predict_R(O):
     # and the dense form: B x = c(B11 w, z)
     B = O.dense_B(Lb, NN)
     np.testing.assert_allclose(B @ x, np.concatenate([B[:n, :n] @ fields[2], z[0][2]]), atol=1e-10)
+
+
+class _FailingCtx:
+    """Stand-in device context whose proposal factor (which = 1) fails with a
+    given nngp status: exercises the MH step's error handling on the host."""
+
+    def __init__(self, status):
+        self.status = status
+
+    def factor(self, which, covfun, cp):
+        from nngp_amd._lib import NNGPError
+
+        if which == 1:
+            raise NNGPError(self.status, "injected")
+
+    def set_field(self, f):
+        pass
+
+    def set_mu(self, mu, b0):
+        pass
+
+    def beta0_stats(self):
+        return 1.0, 0.0
+
+    def sum_squared_residuals(self, b0):
+        return 1.0
+
+    def get_field(self):
+        return np.zeros(4)
+
+
+def _program(ctx, on_chol_error):
+    from nngp_amd.update_gaussian import _chain_program
+
+    va = {"n_obs": 4, "n_locs": 4, "locs_match": np.arange(1, 5)}
+    stm = {"covfun": {"stationary_covfun": "exponential_isotropic", "shape_params": ["log_range"]}}
+    state = {"params": {"beta_0": 0.0, "beta": None, "log_scale": -5.0, "shape": np.array([0.0]),
+                        "log_noise_variance": 0.0, "field": np.zeros(4)},
+             "transition_kernels": {"covariance_params_sufficient": {"logvar": -2.0},
+                                    "covariance_params_ancillary": {"logvar": -2.0},
+                                    "log_noise_variance": {"logvar": -1.0}}}
+    return _chain_program(0, state, ctx, {"X": None, "locs": []}, np.array([0.0, 1.0, 2.0, 3.0]), stm, va,
+                          1, 0.0, True, 1, 0, 1, on_chol_error)
+
+
+def test_mh_proposal_factor_failures(P):
+    """update_Gaussian.R:123,179: GpGp raises on a non positive definite local
+    covariance, which ends the update (default on_chol_error="error"); with
+    "reject" only that status rejects the proposal; every other failure
+    (here a HIP error) propagates in both modes."""
+    from nngp_amd._lib import NNGP_ERR_CHOL, NNGP_ERR_HIP, NNGPError
+
+    with pytest.raises(NNGPError):
+        next(_program(_FailingCtx(NNGP_ERR_CHOL), "error"))
+    g = _program(_FailingCtx(NNGP_ERR_CHOL), "reject")
+    req = next(g)
+    assert req[0] == "anc" and req[3] is False      # ancillary proposal rejected
+    assert g.send(None)[0] == "sweep"               # sufficient proposal rejected too, the iteration goes on
+    for mode in ("error", "reject"):
+        with pytest.raises(NNGPError) as e:
+            next(_program(_FailingCtx(NNGP_ERR_HIP), mode))
+        assert e.value.status == NNGP_ERR_HIP
+
+
+def test_r_shim_wraps_every_abi_entry_point():
+    """rpkg/src/nngp_shim.c: one registered .Call routine per function of
+    include/nngp.h (nngp_ctx_last_error / status_string included), and the
+    shim compiles (a declarations-only R API stand-in under tests/cpp: this
+    image has no R; `R CMD INSTALL rpkg` builds it against R's headers)."""
+    import subprocess
+
+    root = Path(__file__).resolve().parent.parent
+    hdr = (root / "include" / "nngp.h").read_text()
+    shim = (root / "rpkg" / "src" / "nngp_shim.c").read_text()
+    declared = set(re.findall(r"\b(nngp_[a-z0-9_]+)\s*\(", hdr)) - {"nngp_ctx"}
+    for fn in sorted(declared):
+        assert re.search(rf"\b{fn}\s*\(", shim.split("#include \"nngp.h\"")[1]), f"{fn} not called by the shim"
+    registered = set(re.findall(r"E\((C_nngp_[a-z0-9_]+),", shim))
+    defined = set(re.findall(r"^SEXP (C_nngp_[a-z0-9_]+)\(", shim, re.M))
+    assert registered == defined and len(defined) >= len(declared) - 2
+    r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-Wno-cast-function-type", "-fsyntax-only",
+                        f"-I{root / 'tests' / 'cpp' / 'r_api_stub'}", f"-I{root / 'include'}",
+                        str(root / "rpkg" / "src" / "nngp_shim.c")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    rfun = (root / "rpkg" / "R" / "nngp.R").read_text() + (root / "rpkg" / "R" / "mcmc_nngp_update_Gaussian.R").read_text()
+    for c in defined:
+        assert c in rfun, f"{c} has no R wrapper"

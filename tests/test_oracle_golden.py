@@ -215,3 +215,25 @@ def test_triangular_solve_inverts_linv_mult(O):
     locs, NN, Linv = _problem(O, n=300, m=9)
     x = np.random.default_rng(5).normal(size=300)
     np.testing.assert_allclose(O.tri_solve(Linv, NN, O.linv_mult(Linv, x, NN)), x, rtol=1e-9, atol=1e-10)
+
+
+@pytest.mark.parametrize("form", ["masked", "local"])
+def test_threaded_oracle_sweeps_bitwise_equal_serial(O, form):
+    """The OpenMP sweeps of the CPU baseline (one chain on all host cores)
+    give exactly the serial restatement's field."""
+    rng = np.random.default_rng(4)
+    n, m = 3000, 8
+    locs = rng.uniform(size=(n, 2))
+    locs = locs[O.order_maxmin_exact(locs) - 1]
+    NN = O.find_ordered_nn(locs, m)
+    col = O.greedy_coloring(NN)
+    Lo = O.vecchia_linv("exponential_isotropic", [1.0, 0.1, 0.0], locs, NN)
+    D = O.precision_diag(Lo, NN)
+    y = rng.normal(size=n)
+    lm = np.arange(1, n + 1, dtype=np.int32)
+    f0 = rng.normal(size=n)
+    z = rng.normal(size=(2, n))
+    args = (Lo, NN, col, D, np.ones(n, np.int32), y, np.full(n, 0.2), lm, 0.2, 0.1, -0.3, z)
+    ref = O.sweep(form, f0, *args)
+    for th in (2, 5):
+        np.testing.assert_array_equal(O.sweep(form, f0, *args, threads=th), ref)
