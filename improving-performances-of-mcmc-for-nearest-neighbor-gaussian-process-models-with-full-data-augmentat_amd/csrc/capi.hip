@@ -229,7 +229,6 @@ TileDev tile_dev(nngp_ctx* c) {
   D.ctl = c->ctl_d;
   D.dbg = c->tdbg_d;
   D.probe = c->tprobe;
-  if (const char* v = std::getenv("NNGP_TILE_VARIANT")) D.variant = std::atoi(v);
   D.K = c->tl.K;
   D.C = c->C;
   D.T = c->tl.T;

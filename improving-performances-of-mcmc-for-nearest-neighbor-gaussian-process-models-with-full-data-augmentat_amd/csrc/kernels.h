@@ -159,11 +159,10 @@ struct TileDev {
   const double* r;            // device rows x C (r = B w at call start)
   const SweepScalars* scal;   // C
   unsigned* ctl;              // [0] call id (bumped on the device before every launch), [1] timeout word
-  unsigned long long* dbg;    // NNGP_PROBE=9: per-tile phase times (4 x u64), else null
+  unsigned long long* dbg;    // NNGP_PROBE=9 / 2: per-tile phase times / per-phase timeline, else null
   int K, C, T, n;
   int max_gslots;             // max foreign slots of a (tile, colour): LDS of their dw
-  int probe = 0;
-  int variant = 0;            // NNGP_TILE_VARIANT (experiments)              // dbg layout: 1 = per-tile segment sums (T x 8), 2 = timeline (T x 512 phases x 4)
+  int probe = 0;              // dbg layout: 1 = per-tile segment sums (T x 8), 2 = timeline (T x 512 phases x 8)
 };
 
 struct TileLaunch {

@@ -1185,31 +1185,8 @@ struct TileBatchRegs {
   double w[IMAX], zs[IMAX];   // w; prepped: z / sqrt(P)
 };
 
-// cache policy of a stream load: temporal (default: stays in L2 / the
-// Infinity Cache) or non-temporal
-template <bool TEMPORAL, class X>
-__device__ __forceinline__ X tile_ld(const X* p) {
-  if constexpr (TEMPORAL) return *p;
-  else return __builtin_nontemporal_load(p);
-}
-typedef double f64x2_t __attribute__((ext_vector_type(2)));
-template <bool TEMPORAL>
-__device__ __forceinline__ int2 tile_ld(const int2* p) {
-  const long long v = tile_ld<TEMPORAL>(reinterpret_cast<const long long*>(p));
-  return make_int2((int)(v & 0xFFFFFFFFll), (int)(v >> 32));
-}
-template <bool TEMPORAL>
-__device__ __forceinline__ double2 tile_ld(const double2* p) {
-  const f64x2_t v = tile_ld<TEMPORAL>(reinterpret_cast<const f64x2_t*>(p));
-  return make_double2(v.x, v.y);
-}
-
-// POL (stream cache policy bits): 1 = cell indices temporal, 2 = chain 0's
-// cell values temporal, 4 = ghost cells temporal, 8 = per-slot records
-// non-temporal (default: records temporal, cells and ghosts non-temporal)
-
 // the batch's per-slot records (the draw preparation waits for them)
-template <int C, int NT, int RMAX, int POL = 0>
+template <int C, int NT, int RMAX>
 __device__ __forceinline__ void tile_load_items(const TileDev& D, const int4 B, TileBatchRegs<C, NT, RMAX>& b, int t) {
   b.R = B.y & 0xFFFF; b.ns = B.z; b.x0 = B.w;
 #pragma unroll
@@ -1218,121 +1195,39 @@ __device__ __forceinline__ void tile_load_items(const TileDev& D, const int4 B, 
     if (u < b.ns * C) {
       const int q = u / C;
       const size_t xu = (size_t)b.x0 * C + u;  // = (x0 + q) * C + chain
-      const int2 si = tile_ld<!(POL & 8)>(D.sinfo + b.x0 + q);
+      const int2 si = D.sinfo[b.x0 + q];
       b.nobs[k] = si.x;
       b.flag[k] = si.y;
-      b.loc[k] = tile_ld<!(POL & 8)>(D.slot_loc + b.x0 + q);
-      const double2 dr = tile_ld<!(POL & 8)>(D.dr + xu);
+      b.loc[k] = D.slot_loc[b.x0 + q];
+      const double2 dr = D.dr[xu];
       b.a0[k] = dr.x;
       b.a1[k] = dr.y;
-      b.w[k] = tile_ld<!(POL & 8)>(D.w_slot + xu);
+      b.w[k] = D.w_slot[xu];
     }
   }
 }
 
 // the batch's cells: thread t's run f = t*R + j sits at off + j*NT + t
-template <int C, int NT, int RMAX, int POL = 0>
+template <int C, int NT, int RMAX>
 __device__ __forceinline__ void tile_load_cells(const TileDev& D, const int4 B, TileBatchRegs<C, NT, RMAX>& b, int t) {
   const bool live = t < (B.y >> 16);  // threads past nthr hold padding only: no load
 #pragma unroll
   for (int j = 0; j < RMAX; ++j) {
     if (j < b.R && live) {
       const long long e = B.x + (long long)j * NT + t;
-      b.pk[j] = tile_ld<(POL & 1) != 0>(D.cell_pk + e);
-      b.v[j][0] = tile_ld<(POL & 2) != 0>(D.cell_val + e);
+      b.pk[j] = __builtin_nontemporal_load(D.cell_pk + e);
 #pragma unroll
-      for (int ch = 1; ch < C; ++ch) b.v[j][ch] = tile_ld<false>(D.cell_val + ch * D.n_cells + e);
+      for (int ch = 0; ch < C; ++ch) b.v[j][ch] = __builtin_nontemporal_load(D.cell_val + ch * D.n_cells + e);
     } else {
       b.pk[j] = kTPad;
     }
   }
 }
 
-template <int C, int NT, int RMAX, int POL = 0>
-__device__ __forceinline__ void tile_load_batch(const TileDev& D, const int4 B, TileBatchRegs<C, NT, RMAX>& b, int t) {
-  tile_load_items<C, NT, RMAX, POL>(D, B, b, t);
-  tile_load_cells<C, NT, RMAX, POL>(D, B, b, t);
-}
-
-// split form of the batch loads (VAR bit 7): the slots' locations first (the
-// normals need only them), then the cells, then the rest of the records
 template <int C, int NT, int RMAX>
-__device__ __forceinline__ void tile_load_locs(const TileDev& D, const int4 B, TileBatchRegs<C, NT, RMAX>& b, int t) {
-  b.R = B.y & 0xFFFF; b.ns = B.z; b.x0 = B.w;
-#pragma unroll
-  for (int k = 0; k < TileBatchRegs<C, NT, RMAX>::IMAX; ++k) {
-    const int u = t + k * NT;
-    if (u < b.ns * C) b.loc[k] = D.slot_loc[b.x0 + u / C];
-  }
-}
-
-template <int C, int NT, int RMAX, int POL = 0>
-__device__ __forceinline__ void tile_load_records(const TileDev& D, TileBatchRegs<C, NT, RMAX>& b, int t) {
-#pragma unroll
-  for (int k = 0; k < TileBatchRegs<C, NT, RMAX>::IMAX; ++k) {
-    const int u = t + k * NT;
-    if (u < b.ns * C) {
-      const int q = u / C;
-      const size_t xu = (size_t)b.x0 * C + u;
-      const int2 si = tile_ld<!(POL & 8)>(D.sinfo + b.x0 + q);
-      b.nobs[k] = si.x;
-      b.flag[k] = si.y;
-      const double2 dr = tile_ld<!(POL & 8)>(D.dr + xu);
-      b.a0[k] = dr.x;
-      b.a1[k] = dr.y;
-      b.w[k] = tile_ld<!(POL & 8)>(D.w_slot + xu);
-    }
-  }
-}
-
-// L2 prefetch of a byte range: thread t touches the 64-B lines l of [a, b)
-// with (base + l) % NT == t (base = lines of the ranges before this one).
-// The loads are inline asm into ONE register that stays live until
-// tile_touch_wait: no VGPR per line, and the compiler's own vmcnt waits do not
-// see them (its counted waits can only get more conservative).
-template <int NT>
-__device__ __forceinline__ void touch_range(const void* p, long long a, long long b, int& base, int t, unsigned& sink) {
-  if (b <= a) return;
-  const long long la = a >> 6, nl = ((b - 1) >> 6) - la + 1;
-  int l = t - base % NT;
-  if (l < 0) l += NT;
-  for (; l < nl; l += NT) {
-    const long long off = ((la + l) << 6) > a ? ((la + l) << 6) : a;
-    const char* q = reinterpret_cast<const char*>(p) + off;
-    asm volatile("global_load_dword %0, %1, off" : "+v"(sink) : "v"(q) : "memory");
-  }
-  base += (int)nl;
-}
-
-// everything of batch B (records, cells) and the ghost cells [g0, g1) that
-// the next hand-off and phase will load: pulled into the XCD's L2 while the
-// own work runs (one register set cannot hold them: the real loads follow the
-// own work and then hit L2)
-template <int C, int NT>
-__device__ __forceinline__ void tile_touch(const TileDev& D, const int4 B, bool batch, int g0, int g1, int t,
-                                           unsigned& sink) {
-  int base = 0;
-  if (batch) {
-    const long long x0 = B.w, ns = B.z, e0 = B.x, ne = (long long)(B.y & 0xFFFF) * NT;
-    touch_range<NT>(D.sinfo, x0 * 8, (x0 + ns) * 8, base, t, sink);
-    touch_range<NT>(D.slot_loc, x0 * 4, (x0 + ns) * 4, base, t, sink);
-    touch_range<NT>(D.dr, x0 * C * 16, (x0 + ns) * C * 16, base, t, sink);
-    touch_range<NT>(D.w_slot, x0 * C * 8, (x0 + ns) * C * 8, base, t, sink);
-    touch_range<NT>(D.cell_pk, e0 * 4, (e0 + ne) * 4, base, t, sink);
-#pragma unroll
-    for (int ch = 0; ch < C; ++ch)
-      touch_range<NT>(D.cell_val, (ch * D.n_cells + e0) * 8, (ch * D.n_cells + e0 + ne) * 8, base, t, sink);
-  }
-  if (g1 > g0) {
-    touch_range<NT>(D.gcell, (long long)g0 * 8, (long long)g1 * 8, base, t, sink);
-#pragma unroll
-    for (int ch = 0; ch < C; ++ch)
-      touch_range<NT>(D.gval, (ch * D.n_gcells + g0) * 8, (ch * D.n_gcells + g1) * 8, base, t, sink);
-  }
-}
-
-__device__ __forceinline__ void tile_touch_wait(unsigned& sink) {
-  asm volatile("s_waitcnt vmcnt(0)" : "+v"(sink) : : "memory");
+__device__ __forceinline__ void tile_load_batch(const TileDev& D, const int4 B, TileBatchRegs<C, NT, RMAX>& b, int t) {
+  tile_load_items<C, NT, RMAX>(D, B, b, t);
+  tile_load_cells<C, NT, RMAX>(D, B, b, t);
 }
 
 // everything of the Gibbs draw but acc: P = D/s2 + n/t2, w' = (cR - acc/s2)/P
@@ -1360,40 +1255,6 @@ __device__ __forceinline__ void tile_prep_items(const TileDev& D, const TileLaun
   }
 }
 
-// the two halves of tile_prep_items: the normals (locations only) -> zs,
-// then the rest once the records are in
-template <int C, int NT, int RMAX>
-__device__ __forceinline__ void tile_prep_normals(const TileDev& D, const TileLaunch& a,
-                                                  const unsigned long long* seed_s, int s,
-                                                  TileBatchRegs<C, NT, RMAX>& b, int t) {
-#pragma unroll
-  for (int k = 0; k < TileBatchRegs<C, NT, RMAX>::IMAX; ++k) {
-    const int u = t + k * NT;
-    if (u < b.ns * C) {
-      const int q = u / C, ch = u - q * C;
-      if (a.z_in) b.zs[k] = a.z_in[((size_t)s * D.n + b.x0 + q) * C + ch];
-      else b.zs[k] = normal_loc(seed_s[2 * ch], seed_s[2 * ch + 1] + s, (uint32_t)b.loc[k]);
-    }
-  }
-}
-
-template <int C, int NT, int RMAX>
-__device__ __forceinline__ void tile_prep_rest(const double* sc_s, TileBatchRegs<C, NT, RMAX>& b, int t) {
-#pragma unroll
-  for (int k = 0; k < TileBatchRegs<C, NT, RMAX>::IMAX; ++k) {
-    const int u = t + k * NT;
-    if (u < b.ns * C) {
-      const int q = u / C, ch = u - q * C;
-      const double inv_s2 = sc_s[2 * ch], inv_t2 = sc_s[2 * ch + 1];
-      const double P = b.a0[k] * inv_s2 + (double)b.nobs[k] * inv_t2;
-      const double cR = inv_t2 * b.a1[k] + inv_s2 * (b.a0[k] * b.w[k]);
-      b.a0[k] = cR;
-      b.a1[k] = 1.0 / P;
-      b.zs[k] = b.zs[k] / sqrt(P);
-    }
-  }
-}
-
 // ghost cells of one chunk: local row, foreign slot, B values
 template <int C, int GMAX>
 struct TileGhostRegs {
@@ -1401,18 +1262,18 @@ struct TileGhostRegs {
   double gv[GMAX][C];
 };
 
-template <int C, int NT, int GMAX, int POL = 0>
+template <int C, int NT, int GMAX>
 __device__ __forceinline__ void tile_load_ghosts(const TileDev& D, int gb, int g1, TileGhostRegs<C, GMAX>& g, int t) {
 #pragma unroll
   for (int k = 0; k < GMAX; ++k) {
     const int e = gb + k * NT + t;
     g.lr[k] = -1;
     if (e < g1) {
-      const long long raw = tile_ld<(POL & 4) != 0>(reinterpret_cast<const long long*>(D.gcell) + e);
+      const long long raw = __builtin_nontemporal_load(reinterpret_cast<const long long*>(D.gcell) + e);
       g.lr[k] = (int)(raw & 0xFFFFFFFFll);
       g.gx[k] = (int)(raw >> 32);
 #pragma unroll
-      for (int ch = 0; ch < C; ++ch) g.gv[k][ch] = tile_ld<(POL & 4) != 0>(D.gval + ch * D.n_gcells + e);
+      for (int ch = 0; ch < C; ++ch) g.gv[k][ch] = __builtin_nontemporal_load(D.gval + ch * D.n_gcells + e);
     }
   }
 }
@@ -1452,7 +1313,6 @@ struct TileState {
 // NNGP_PROBE=2 timeline: thread 0 of every tile stores the 100 MHz clock at
 // points k of phase S.ph (no waits added besides the clock read's own)
 constexpr int kTimelinePhases = 512;
-constexpr int kTileVarDefault = 4;  // round-1 load order (measured best, NNGP_TILE_VARIANT A/B)
 #define TLSTAMP(S, k)                                                                         \
   do {                                                                                        \
     if (PROBE == 2 && (S).t == 0 && (S).ph < kTimelinePhases)                                 \
@@ -1596,9 +1456,13 @@ __device__ __forceinline__ void tile_own_batch(const TileDev& D, const TileLaunc
 }
 
 // one colour phase ph = sweep*K + c with `cur` holding its prepared first
-// batch; the next phase's first batch is loaded into `nxt` at the start (its
-// HBM stream overlaps this colour's work) and prepared during the hand-off
-template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE, int VAR>
+// batch.  Double-buffered (DB): the next phase's first batch is loaded into
+// `nxt` at the start (its HBM stream overlaps this colour's work); otherwise
+// after the own work, before the hand-off.  (Measured and dropped, see
+// the normals pregenerated by a separate kernel -- no Philox here,
+// 132 instead of 255 VGPRs at 1 chain --, double buffering at 3 chains, an L2
+// prefetch of the next stream during the own work, other load orders.)
+template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE>
 __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a, TileState& S, int ph,
                                            TileBatchRegs<C, NT, RMAX>& cur, TileBatchRegs<C, NT, RMAX>& nxt,
                                            TileGhostRegs<C, GMAX>& gr, TileGhostRegs<C, GMAX>& grn) {
@@ -1618,65 +1482,32 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
   // NT items' slot indices load now, behind the own work
   const int gs0 = S.gsp_s[c], nfi = (S.gsp_s[c + 1] - gs0) * C;
   const int gsl_pref = t < nfi ? D.gslot[gs0 + t / C] : 0;
-  constexpr bool prep_late = VAR & 1;  // NNGP_TILE_VARIANT bit 0: draw prep after the ghost adds
-  constexpr bool touch = !DB && (VAR & 2);  // bit 1: L2 prefetch of the next stream during the own work
-  unsigned sink = 0;
   if (DB) {
-    // the next colour's first batch and first ghost chunk: their HBM stream
+    // the next colour's first batch (and ghost chunk): their HBM stream
     // overlaps this colour's work (two register sets)
-    if (more) tile_load_batch<C, NT, RMAX, ((VAR >> 3) & 15)>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
-    if (has_next && gn1 > gn0) tile_load_ghosts<C, NT, GMAX, ((VAR >> 3) & 15)>(D, gn0, gn1, grn, t);
-  } else if (touch) {
-    tile_touch<C, NT>(D, more ? S.batch_s[S.bptr_s[cn]] : make_int4(0, 0, 0, 0), more, g0, g1, t, sink);
+    if (more) tile_load_batch<C, NT, RMAX>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
+    if (has_next && gn1 > gn0) tile_load_ghosts<C, NT, GMAX>(D, gn0, gn1, grn, t);
   }
   // ---- 1. own batches
   for (int bi = bfirst; bi < bend; ++bi) {
     if (bi != bfirst) {  // rare: a colour with more than one batch in this tile
       __syncthreads();   // acc_s is indexed by slot-in-batch: every wave is done with the last batch
-      tile_load_batch<C, NT, RMAX, ((VAR >> 3) & 15)>(D, S.batch_s[bi], cur, t);
+      tile_load_batch<C, NT, RMAX>(D, S.batch_s[bi], cur, t);
       tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, s, cur, t);
     }
     tile_own_batch<C, NT, RMAX, PROBE>(D, a, S, cur, epoch);
   }
-  if (touch) tile_touch_wait(sink);
-  // ---- 2. (one register set) the next colour's records, the first poll of
-  // this colour's granules, this colour's ghost cells and the next colour's
-  // cells, in the order they are consumed (loads return in order)
-  const int4 nb = more ? S.batch_s[S.bptr_s[cn]] : make_int4(0, 0, 0, 0);
-  constexpr bool orig = VAR & 4;  // bit 2: round-1 order (cells, records, ghosts; prep; then the first poll)
+  // ---- 2. (one register set) the next colour's batch, this colour's ghost
+  // cells, the next batch's draw scalars, then the first poll of this
+  // colour's granules
+  if (!DB) {
+    if (more) tile_load_batch<C, NT, RMAX>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
+    if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
+  }
+  if (more) tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, sn, nxt, t);
   const bool pol = t < nfi;
   u32x4_t gfirst;
-  if (orig && (VAR & 128)) {
-    // the normals of the next batch are computed while its stream lands
-    if (!DB) {
-      if (more) {
-        tile_load_locs<C, NT, RMAX>(D, nb, nxt, t);
-        tile_load_cells<C, NT, RMAX, ((VAR >> 3) & 15)>(D, nb, nxt, t);
-        tile_load_records<C, NT, RMAX, ((VAR >> 3) & 15)>(D, nxt, t);
-      }
-      if (g1 > g0) tile_load_ghosts<C, NT, GMAX, ((VAR >> 3) & 15)>(D, g0, g1, gr, t);
-    }
-    if (more) {
-      tile_prep_normals<C, NT, RMAX>(D, a, S.seed_s, sn, nxt, t);
-      tile_prep_rest<C, NT, RMAX>(S.sc_s, nxt, t);
-    }
-    if (pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * C + t % C) * 16), 0, 16);
-  } else if (orig) {
-    if (!DB) {
-      if (more) tile_load_batch<C, NT, RMAX, ((VAR >> 3) & 15)>(D, nb, nxt, t);
-      if (g1 > g0) tile_load_ghosts<C, NT, GMAX, ((VAR >> 3) & 15)>(D, g0, g1, gr, t);
-    }
-    if (!prep_late && more) tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, sn, nxt, t);
-    if (pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * C + t % C) * 16), 0, 16);
-  } else {
-    if (!DB && more) tile_load_items<C, NT, RMAX, ((VAR >> 3) & 15)>(D, nb, nxt, t);
-    if (pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * C + t % C) * 16), 0, 16);
-    if (!DB) {
-      if (g1 > g0) tile_load_ghosts<C, NT, GMAX, ((VAR >> 3) & 15)>(D, g0, g1, gr, t);
-      if (more) tile_load_cells<C, NT, RMAX, ((VAR >> 3) & 15)>(D, nb, nxt, t);
-    }
-    if (!prep_late && more) tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, sn, nxt, t);
-  }
+  if (pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * C + t % C) * 16), 0, 16);
   TSTAMP(S, 5);
   TLSTAMP(S, 4);
   // ---- 3. hand-off: the granule of each (foreign slot, chain) of this colour
@@ -1715,7 +1546,7 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
     *S.spin_s = 0;
   }
   for (int gb = g0; gb < g1; gb += NT * GMAX) {
-    if (gb != g0) tile_load_ghosts<C, NT, GMAX, ((VAR >> 3) & 15)>(D, gb, g1, gr, t);
+    if (gb != g0) tile_load_ghosts<C, NT, GMAX>(D, gb, g1, gr, t);
 #pragma unroll
     for (int k = 0; k < GMAX; ++k)
       if (gr.lr[k] >= 0)
@@ -1724,13 +1555,12 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
   }
   // ---- 4. the next batch's draw scalars (registers only: no barrier needed
   // before them; the barrier below orders the ghost adds before the products)
-  if (prep_late && more) tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, sn, nxt, t);
   __syncthreads();
   TSTAMP(S, 6);
   TLSTAMP(S, 3);
 }
 
-template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE, int VAR>
+template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE>
 __global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D, TileLaunch a) {
   using BR = TileBatchRegs<C, NT, RMAX>;
   constexpr int NW = NT / 64;
@@ -1791,11 +1621,11 @@ __global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D, TileLaunch a
   TSTAMP(S, 7);
   if (DB) {
     for (int ph = 0; ph < S.nph; ph += 2) {
-      tile_phase<C, NT, RMAX, GMAX, DB, PROBE, VAR>(D, a, S, ph, A, B, GA, GB);
-      if (ph + 1 < S.nph) tile_phase<C, NT, RMAX, GMAX, DB, PROBE, VAR>(D, a, S, ph + 1, B, A, GB, GA);
+      tile_phase<C, NT, RMAX, GMAX, DB, PROBE>(D, a, S, ph, A, B, GA, GB);
+      if (ph + 1 < S.nph) tile_phase<C, NT, RMAX, GMAX, DB, PROBE>(D, a, S, ph + 1, B, A, GB, GA);
     }
   } else {
-    for (int ph = 0; ph < S.nph; ++ph) tile_phase<C, NT, RMAX, GMAX, DB, PROBE, VAR>(D, a, S, ph, A, A, GA, GA);
+    for (int ph = 0; ph < S.nph; ++ph) tile_phase<C, NT, RMAX, GMAX, DB, PROBE>(D, a, S, ph, A, A, GA, GA);
   }
   if (PROBE == 1 && t == 0) {
     unsigned long long* o = D.dbg + (size_t)T * 8;
@@ -1804,12 +1634,12 @@ __global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D, TileLaunch a
 }
 #undef TSTAMP
 
-template <int C, int NT, int PROBE, int VAR = kTileVarDefault>
+template <int C, int NT, int PROBE>
 static hipError_t launch_tiles_c(hipStream_t st, const TileDev& D, const TileLaunch& a, int lds) {
   constexpr int RMAX = tile_rmax(C, NT);
   constexpr int DB = tile_double_buffer(C, NT);
   constexpr int GMAX = NT == 256 ? 4 : (NT == 512 ? 3 : 1);
-  auto k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE, VAR>;
+  auto k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE>;
   lds = lds < kTSpreadLds ? kTSpreadLds : lds;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return e;
@@ -1832,14 +1662,6 @@ static hipError_t launch_tiles_nt(hipStream_t st, const TileDev& D, const TileLa
       case 1: return launch_tiles_c<1, NT, 2>(st, D, a, lds);
       case 3: return launch_tiles_c<3, NT, 2>(st, D, a, lds);
       default: break;
-    }
-  }
-  if (NT == 512 && D.variant) {  // NNGP_TILE_VARIANT experiments (512-thread tiles, 1 and 3 chains)
-    switch (D.C * 256 + D.variant) {
-#define TV(c, v) case c * 256 + v: return launch_tiles_c<c, NT, 0, v>(st, D, a, lds);
-      TV(1, 4) TV(3, 4) TV(1, 132) TV(3, 132)
-#undef TV
-      default: return hipErrorInvalidValue;
     }
   }
   switch (D.C) {
