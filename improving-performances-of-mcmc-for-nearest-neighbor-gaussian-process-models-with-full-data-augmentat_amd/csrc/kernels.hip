@@ -1188,7 +1188,7 @@ struct TileBatchRegs {
 // the batch's per-slot records (the draw preparation waits for them)
 template <int C, int NT, int RMAX>
 __device__ __forceinline__ void tile_load_items(const TileDev& D, const int4 B, TileBatchRegs<C, NT, RMAX>& b, int t) {
-  b.R = B.y & 0xFFFF; b.ns = B.z; b.x0 = B.w;
+  b.ns = B.z; b.x0 = B.w;
 #pragma unroll
   for (int k = 0; k < TileBatchRegs<C, NT, RMAX>::IMAX; ++k) {
     const int u = t + k * NT;
@@ -1210,6 +1210,7 @@ __device__ __forceinline__ void tile_load_items(const TileDev& D, const int4 B, 
 // the batch's cells: thread t's run f = t*R + j sits at off + j*NT + t
 template <int C, int NT, int RMAX>
 __device__ __forceinline__ void tile_load_cells(const TileDev& D, const int4 B, TileBatchRegs<C, NT, RMAX>& b, int t) {
+  b.R = B.y & 0xFFFF;
   const bool live = t < (B.y >> 16);  // threads past nthr hold padding only: no load
 #pragma unroll
   for (int j = 0; j < RMAX; ++j) {
@@ -1339,8 +1340,8 @@ __device__ __forceinline__ void seg_scan_step(double (&v)[C], int& f) {
 // scatter.  LDS and registers only, plus the draws' stores: no global load
 // (a load here would wait behind the next batch's prefetch, vmcnt is in order)
 template <int C, int NT, int RMAX, int PROBE>
-__device__ __forceinline__ void tile_own_batch(const TileDev& D, const TileLaunch& a, TileState& S,
-                                               TileBatchRegs<C, NT, RMAX>& b, unsigned epoch) {
+__device__ __forceinline__ void tile_own_draw(const TileDev& D, const TileLaunch& a, TileState& S,
+                                              TileBatchRegs<C, NT, RMAX>& b, unsigned epoch) {
   constexpr int IMAX = TileBatchRegs<C, NT, RMAX>::IMAX;
   const int t = S.t, lane = S.lane, wv = S.wv;
   double* r_s = S.r_s;
@@ -1441,6 +1442,14 @@ __device__ __forceinline__ void tile_own_batch(const TileDev& D, const TileLaunc
   __syncthreads();
   TSTAMP(S, 3);
   TLSTAMP(S, 1);
+}
+
+// ... and its scatter r_k += B[k,i] dw_i (dw in acc_s).  Needs only the
+// batch's cells: its per-slot records may be overwritten by then.
+template <int C, int NT, int RMAX, int PROBE>
+__device__ __forceinline__ void tile_own_scatter(TileState& S, const TileBatchRegs<C, NT, RMAX>& b, int R) {
+  double* r_s = S.r_s;
+  const double* acc_s = S.acc_s;
 #pragma unroll
   for (int j = 0; j < RMAX; ++j) {
     if (j < R) {
@@ -1488,26 +1497,41 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
     if (more) tile_load_batch<C, NT, RMAX>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
     if (has_next && gn1 > gn0) tile_load_ghosts<C, NT, GMAX>(D, gn0, gn1, grn, t);
   }
-  // ---- 1. own batches
+  // ---- 1. own batches.  One register set (!DB): after the draw of the last
+  // batch, the next colour's per-slot records, this colour's ghost cells and
+  // the first poll of its granules go out before the scatter (the draw's
+  // records are dead, the scatter needs only the cells), the next cells
+  // after it
+  const bool pol = t < nfi;
+  u32x4_t gfirst;
   for (int bi = bfirst; bi < bend; ++bi) {
     if (bi != bfirst) {  // rare: a colour with more than one batch in this tile
       __syncthreads();   // acc_s is indexed by slot-in-batch: every wave is done with the last batch
       tile_load_batch<C, NT, RMAX>(D, S.batch_s[bi], cur, t);
       tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, s, cur, t);
     }
-    tile_own_batch<C, NT, RMAX, PROBE>(D, a, S, cur, epoch);
+    tile_own_draw<C, NT, RMAX, PROBE>(D, a, S, cur, epoch);
+    const int R = cur.R;
+    if (!DB && bi + 1 == bend) {
+      if (more) tile_load_items<C, NT, RMAX>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
+      if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
+      if (pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * C + t % C) * 16), 0, 16);
+    }
+    tile_own_scatter<C, NT, RMAX, PROBE>(S, cur, R);
   }
-  // ---- 2. (one register set) the next colour's batch, this colour's ghost
-  // cells, the next batch's draw scalars, then the first poll of this
-  // colour's granules
+  TLSTAMP(S, 6);
+  // ---- 2. the next colour's cells (one register set), the next batch's
+  // draw scalars, then (two register sets) the first poll
   if (!DB) {
-    if (more) tile_load_batch<C, NT, RMAX>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
-    if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
+    if (bend == bfirst) {  // no own batch of this colour in the tile
+      if (more) tile_load_items<C, NT, RMAX>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
+      if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
+      if (pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * C + t % C) * 16), 0, 16);
+    }
+    if (more) tile_load_cells<C, NT, RMAX>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
   }
   if (more) tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, sn, nxt, t);
-  const bool pol = t < nfi;
-  u32x4_t gfirst;
-  if (pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * C + t % C) * 16), 0, 16);
+  if (DB && pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * C + t % C) * 16), 0, 16);
   TSTAMP(S, 5);
   TLSTAMP(S, 4);
   // ---- 3. hand-off: the granule of each (foreign slot, chain) of this colour

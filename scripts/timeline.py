@@ -35,18 +35,20 @@ for rep in range(4):
 nph = S * K
 raw = np.fromfile(out, dtype=np.uint64).reshape(T, 512, 8)[:, :nph]
 spins = raw[..., 5].astype(np.float64)
-d = raw[..., :5].astype(np.float64) / 100.0  # us
+d = raw[..., [0, 1, 2, 3, 4, 6]].astype(np.float64) / 100.0  # us
 miss = d[..., 1] == 0              # (tile, colour) with no own batch: no publish stamp
 d[..., 1][miss] = d[..., 0][miss]
 d -= d[:, 0, 0].min()
-start, pub, hand, end, landed = d[..., 0], d[..., 1], d[..., 2], d[..., 3], d[..., 4]
+start, pub, hand, end, landed, scat = d[..., 0], d[..., 1], d[..., 2], d[..., 3], d[..., 4], d[..., 5]
+scat = np.where(raw[..., 6] == 0, pub, scat)
 own = pub - start                  # own batches up to the draw barrier (publish)
 rest = hand - pub                  # scatter + stream issue + hand-off poll
 tail = end - hand                  # ghost adds + next batch prep
 dur = end - start
 print(f"C={C} last call {el*1e3:.3f} ms wall, launch span {end[:, -1].max():.1f} us, {end[:, -1].max()/nph:.2f} us/phase")
 print("per tile per phase (mean / p90 / max over tiles, averaged over phases):")
-for nm, a in (("own->publish", own), ("publish->prepped", landed - pub), ("prepped->handoff", hand - landed),
+for nm, a in (("own->publish", own), ("publish->scattered", scat - pub), ("scattered->prepped", landed - scat),
+              ("prepped->handoff", hand - landed),
               ("handoff->end", tail), ("phase", dur)):
     print(f"  {nm:18s} mean {a.mean():6.2f}  p90 {np.percentile(a, 90, axis=0).mean():6.2f}  max {a.max(axis=0).mean():6.2f}")
 print(f"  poll spins (max over the tile's threads): mean {spins.mean():.2f}, p90 {np.percentile(spins, 90):.0f}, "
