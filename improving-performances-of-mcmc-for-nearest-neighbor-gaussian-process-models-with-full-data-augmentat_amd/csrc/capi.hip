@@ -65,6 +65,8 @@ struct nngp_ctx {
   int* slot_dpos_d = nullptr;
   int* dpos_d = nullptr;          // loc -> device row, on the device
   double* stage_h = nullptr;      // pinned n-double staging for field-sized copies
+  double* mu_stage_h = nullptr;   // pinned n_obs-double staging of set_mu
+  hipEvent_t mu_stage_ev = nullptr;
   double* perm_d = nullptr;       // device n-double scratch of those copies (R order)
   int* chunk_first_d = nullptr;  // nchunks+1
   int* loc_rank_d = nullptr;     // n: compact index of each location (Vecchia order)
@@ -357,6 +359,8 @@ void nngp_ctx_destroy(nngp_ctx* c) {
   if (c->res_h) hipHostFree(c->res_h);
   if (c->linv_cur_h) hipHostFree(c->linv_cur_h);
   if (c->stage_h) hipHostFree(c->stage_h);
+  if (c->mu_stage_h) hipHostFree(c->mu_stage_h);
+  if (c->mu_stage_ev) hipEventDestroy(c->mu_stage_ev);
   if (c->tmo_h) hipHostFree(c->tmo_h);
   if (c->st) hipStreamDestroy(c->st);
   delete c;
@@ -758,6 +762,11 @@ int nngp_ctx_info(const nngp_ctx* c, nngp_info* info) {
   info->shard_owned = c->shard ? c->sp.owned : 0;
   info->shard_needed_rows = c->shard ? c->sp.needed_rows : 0;
   info->shard_exchange_slots = c->shard ? c->sp.xoff[c->sp.K] : 0;
+  info->tile_ghost_pass = c->engine == 1 ? c->tl.NT * tile_gmax(c->tl.NT) : 0;
+  info->tile_ghost_cells_max = 0;
+  if (c->engine == 1)
+    for (size_t i = 0; i + 1 < c->tl.gptr.size(); ++i)
+      info->tile_ghost_cells_max = std::max(info->tile_ghost_cells_max, c->tl.gptr[i + 1] - c->tl.gptr[i]);
   return NNGP_OK;
 }
 
@@ -970,12 +979,23 @@ int nngp_set_mu(nngp_ctx* c, const double* mu, double beta0) {
   int rc;
   if ((rc = set_device(c))) return rc;
   ChainState& S = c->ch[c->cur];
-  if (mu) HIPCHK(c, hipMemcpyAsync(S.mu_d, mu, c->n_obs * sizeof(double), hipMemcpyHostToDevice, c->st));
+  if (mu) {
+    // through pinned staging: the call returns before the copy runs (the
+    // previous copy out of the stage is waited for first -- normally long done)
+    if (!c->mu_stage_h) {
+      HIPCHK(c, hipHostMalloc((void**)&c->mu_stage_h, sizeof(double) * c->n_obs, hipHostMallocDefault));
+      HIPCHK(c, hipEventCreateWithFlags(&c->mu_stage_ev, hipEventDisableTiming));
+    } else {
+      HIPCHK(c, hipEventSynchronize(c->mu_stage_ev));
+    }
+    std::memcpy(c->mu_stage_h, mu, sizeof(double) * c->n_obs);
+    HIPCHK(c, hipMemcpyAsync(S.mu_d, c->mu_stage_h, c->n_obs * sizeof(double), hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, hipEventRecord(c->mu_stage_ev, c->st));
+  }
   S.mu_is_const = (mu == nullptr);
   S.mu_beta0 = beta0;
   HIPCHK(c, launch_residual_sums(c->st, c->n, sweep_dev(c), c->cur, c->obs_ptr_d, c->obs_idx_d, c->y_d,
                                  mu ? S.mu_d : nullptr, beta0));
-  HIPCHK(c, hipStreamSynchronize(c->st));
   S.have_mu = true;
   return NNGP_OK;
 }
@@ -1245,16 +1265,51 @@ static int enqueue_shard_allgather(nngp_ctx* c, int col) {
   return NNGP_OK;
 }
 
+// Host checks of everything the per-colour loop reads, so that a failure can
+// only happen before the first collective is enqueued or after the last one
+// (a rank leaving the loop half way would leave its peers waiting in the next
+// all-gather).
+static int shard_plan_check(const nngp_ctx* c) {
+  const ShardPlan& P = c->sp;
+  const int G = P.G, K = P.K;
+  if (G < 1 || G > 64 || P.rank < 0 || P.rank >= G || K < 1) return NNGP_ERR_ARG;
+  if ((int)P.cb.size() != K * (G + 1) || (int)P.seg0.size() != K * (G + 1) || (int)P.cnt.size() != K ||
+      (int)P.xoff.size() != K + 1 || (int)P.gptr.size() != K + 1 || (int)P.pair_ptr.size() != K + 1)
+    return NNGP_ERR_ARG;
+  for (int col = 0; col < K; ++col) {
+    if (P.cnt[col] < 0 || P.xoff[col + 1] - P.xoff[col] != (long long)G * P.cnt[col]) return NNGP_ERR_ARG;
+    if (P.gptr[col] > P.gptr[col + 1] || P.gptr[col + 1] > (int)P.grow.size()) return NNGP_ERR_ARG;
+    if (P.pair_ptr[col] > P.pair_ptr[col + 1]) return NNGP_ERR_ARG;
+    for (int h = 0; h < G; ++h) {
+      const size_t i = (size_t)col * (G + 1) + h;
+      if (P.cb[i] > P.cb[i + 1] || P.seg0[i] > P.seg0[i + 1] || P.seg0[i + 1] - P.seg0[i] > P.cnt[col])
+        return NNGP_ERR_ARG;
+    }
+  }
+  return NNGP_OK;
+}
+
 static int shard_call(nngp_ctx* c, int n_sweeps, int mask) {
   if (c->sp.G > 1 && !c->comm)
     return fail_msg(c, NNGP_ERR_STATE, "sharded sweep: no communicator (nngp_shard_comm_init) -- or use nngp_sweep_chains_group");
+  if (shard_plan_check(c)) return fail_msg(c, NNGP_ERR_ARG, "sharded sweep: inconsistent shard plan");
   int rc;
   if ((rc = enqueue_sweep_body(c, n_sweeps, mask, nullptr, kPrologue))) return rc;
   for (int s = 0; s < n_sweeps; ++s)
     for (int col = 0; col < c->sp.K; ++col) {
-      if ((rc = enqueue_shard_own(c, s, col, mask, n_sweeps))) return rc;
-      if ((rc = enqueue_shard_allgather(c, col))) return rc;
-      if ((rc = enqueue_shard_ghosts(c, col, mask))) return rc;
+      if (!(rc = enqueue_shard_own(c, s, col, mask, n_sweeps)) && !(rc = enqueue_shard_allgather(c, col)))
+        rc = enqueue_shard_ghosts(c, col, mask);
+      if (rc) {
+        // a launch or RCCL failure half way (the checks above exclude the
+        // argument errors): abort the communicator so this rank does not
+        // leave queued collectives its peers wait on; the shard is unusable
+        // until the contexts are recreated
+        if (c->comm) {
+          ncclCommAbort(c->comm);
+          c->comm = nullptr;
+        }
+        return rc;
+      }
     }
   if ((rc = enqueue_sweep_body(c, n_sweeps, mask, nullptr, kEpilogue))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->st));
@@ -1442,8 +1497,7 @@ int nngp_ancillary_propose(nngp_ctx* c, double beta0, double dlog_scale) {
   HIPCHK(c, hipGetLastError());
   if ((rc = tri_solve_dev(c, tri_one(S.linv_d[1]), c->tmp_d, c->tmp2_d))) return rc;
   HIPCHK(c, launch_axpby_shift(c->st, c->n, c->tmp2_d, 1, std::exp(0.5 * dlog_scale), beta0, S.field_prop_d));
-  HIPCHK(c, hipStreamSynchronize(c->st));
-  return NNGP_OK;
+  return NNGP_OK;  // stream-ordered: the proposal is read by the next call on this context
 }
 
 int nngp_ancillary_propose_chains(nngp_ctx* c, int chain_mask, const double* beta0, const double* dlog_scale) {
@@ -1474,8 +1528,7 @@ int nngp_ancillary_propose_chains(nngp_ctx* c, int chain_mask, const double* bet
     if ((chain_mask >> k) & 1)
       HIPCHK(c, launch_axpby_shift(c->st, c->n, c->tmp2_d + k, c->C, std::exp(0.5 * dlog_scale[k]), beta0[k],
                                    c->ch[k].field_prop_d));
-  HIPCHK(c, hipStreamSynchronize(c->st));
-  return NNGP_OK;
+  return NNGP_OK;  // stream-ordered
 }
 
 int nngp_field_response_ratio(nngp_ctx* c, double beta0, double lnv, double* ratio) {
@@ -1499,8 +1552,7 @@ int nngp_accept_field(nngp_ctx* c) {
   if ((rc = set_device(c))) return rc;
   ChainState& S = c->ch[c->cur];
   HIPCHK(c, hipMemcpyAsync(S.field_d, S.field_prop_d, c->n * sizeof(double), hipMemcpyDeviceToDevice, c->st));
-  HIPCHK(c, hipStreamSynchronize(c->st));
-  return NNGP_OK;
+  return NNGP_OK;  // stream-ordered: no host sync
 }
 
 int nngp_beta0_stats(nngp_ctx* c, double* oqo, double* oqf) {

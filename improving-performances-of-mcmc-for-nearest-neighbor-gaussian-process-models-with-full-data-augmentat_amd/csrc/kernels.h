@@ -180,6 +180,8 @@ int tile_lds_bytes(int max_rows, int C, int NT, int K, int max_batches, int max_
 // buffered: 7.7k vs 10.7k chain-sweeps/s -- the own work needs the waves)
 constexpr int tile_double_buffer(int C, int NT) { return C <= 2 ? 1 : 0; }
 constexpr int tile_rmax(int C, int NT) { return 4096 / NT; }
+// ghost-cell registers per thread: NT * GMAX ghost cells of a (tile, colour) per pass
+constexpr int tile_gmax(int NT) { return NT == 256 ? 4 : (NT == 512 ? 3 : 1); }
 hipError_t launch_sweep_tiles(hipStream_t st, const TileDev& D, const TileLaunch& a, int max_rows, int NT,
                               int max_batches, int max_gslots);
 // chain `chain`: cell/ghost values from Linv (device order) and precision_diag

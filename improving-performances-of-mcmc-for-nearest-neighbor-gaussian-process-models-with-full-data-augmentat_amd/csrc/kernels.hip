@@ -1434,7 +1434,10 @@ __device__ __forceinline__ void tile_own_draw(const TileDev& D, const TileLaunch
       if (b.flag[k] & kTExported) {
         const unsigned long long uu = __builtin_bit_cast(unsigned long long, dw);
         u32x4_t g;
-        g.x = (unsigned)uu; g.y = (unsigned)(uu >> 32); g.z = epoch; g.w = S.call;
+        // {dw, epoch, call ^ dw_lo ^ dw_hi}: one 16-B write-through store.  The
+        // tag word also checks the payload, so a torn read (new tag, old dw --
+        // not observed on gfx950, not architecturally excluded) is not taken
+        g.x = (unsigned)uu; g.y = (unsigned)(uu >> 32); g.z = epoch; g.w = S.call ^ g.x ^ g.y;
         __builtin_amdgcn_raw_buffer_store_b128(g, S.gran, (int)(xu * 16), 0, 16);
       }
     }
@@ -1547,7 +1550,7 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
       u32x4_t g = u0 == 0 ? gfirst : __builtin_amdgcn_raw_buffer_load_b128(S.gran, off, 0, 16);
       double dw = 0.0;
       for (unsigned spins = 0;; ++spins) {
-        if (g.z == epoch && g.w == S.call) {
+        if (g.z == epoch && (g.w ^ g.x ^ g.y) == S.call) {
           dw = __builtin_bit_cast(double, (unsigned long long)g.x | ((unsigned long long)g.y << 32));
           if (PROBE == 2) atomicMax(S.spin_s, spins);
           break;
@@ -1662,7 +1665,7 @@ template <int C, int NT, int PROBE>
 static hipError_t launch_tiles_c(hipStream_t st, const TileDev& D, const TileLaunch& a, int lds) {
   constexpr int RMAX = tile_rmax(C, NT);
   constexpr int DB = tile_double_buffer(C, NT);
-  constexpr int GMAX = NT == 256 ? 4 : (NT == 512 ? 3 : 1);
+  constexpr int GMAX = tile_gmax(NT);
   auto k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE>;
   lds = lds < kTSpreadLds ? kTSpreadLds : lds;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);

@@ -77,7 +77,7 @@ def _propose_factor(ctx, covfun, cp, on_chol_error):
 
 
 def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_iterations_update,
-                   field_thinning, ancillary, n_chromatic, iter_start, seed, on_chol_error="error"):
+                   field_thinning, ancillary, n_chromatic, iter_start, seed, on_chol_error="error", var_y=None):
     """Chain i's n_iterations_update Gibbs iterations; yields its device
     requests -- ("anc", beta_0, dlog_scale, ok) for the ancillary proposal and
     ("sweep", n_sweeps, beta_0, log_scale, log_noise_variance, key, counter)
@@ -89,7 +89,8 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
     params = {k: (np.array(v, copy=True) if isinstance(v, np.ndarray) else v) for k, v in state["params"].items()}
     tk = {k: dict(v) for k, v in state["transition_kernels"].items()}
     n_obs = va["n_obs"]
-    var_y = float(np.var(observed_field, ddof=1))
+    if var_y is None:
+        var_y = float(np.var(observed_field, ddof=1))
     has_X = X.get("X") is not None
     has_locs = has_X and len(X["locs"]) > 0
     n_shape = len(sp_names)
@@ -337,8 +338,9 @@ def mcmc_nngp_update_Gaussian(locs, X, observed_field, space_time_model, vecchia
         contexts = make_chain_views(locs, vecchia_approx["NNarray"], vecchia_approx["coloring"],
                                     vecchia_approx["locs_match"], observed_field, len(st_list), devices)
     y = np.asarray(observed_field, np.float64)
+    var_y = float(np.var(y, ddof=1))  # var(observed_field), :167,286 (once for all chains)
     programs = [_chain_program(i, st, contexts[i], X, y, space_time_model, vecchia_approx,
                                int(n_iterations_update), float(field_thinning), bool(ancillary),
-                               int(n_chromatic), iter_start, seed, on_chol_error)
+                               int(n_chromatic), iter_start, seed, on_chol_error, var_y)
                 for i, st in enumerate(st_list)]
     return dict(zip(names, _drive(programs, contexts)))

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define NNGP_ABI_VERSION 5
+#define NNGP_ABI_VERSION 6
 #define NNGP_SHARD_ID_BYTES 128 /* RCCL unique id */
 
 typedef enum {
@@ -102,6 +102,8 @@ typedef struct {
   long long shard_owned;          /* locations swept by this rank */
   long long shard_needed_rows;    /* rows of B its columns touch (its r halo included) */
   long long shard_exchange_slots; /* slots of all colours' exchange regions (padded) */
+  int tile_ghost_pass;       /* tile engine: ghost cells a (tile, colour) applies per register pass */
+  int tile_ghost_cells_max;  /* tile engine: most ghost cells of one (tile, colour) */
 } nngp_info;
 
 /* ---------- library ---------- */

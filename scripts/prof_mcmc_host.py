@@ -1,5 +1,6 @@
 import cProfile, pstats, sys, io
-sys.path.insert(0, '.')
+import os
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
 import numpy as np, torch
 import _pkgload, bench
 P = _pkgload.load()

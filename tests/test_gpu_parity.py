@@ -555,3 +555,43 @@ def test_headline_size_1e6_m15_three_chains(P, O):
             idx = NN[i][NN[i] != O.NA] - 1
             k = np.linalg.cond(O.covmat("matern15_isotropic", cps[1], locs[idx]))
             assert err[i] <= max(1e-10, 1e-14 * k) * scale[i]
+
+
+@pytest.mark.parametrize("C", [1, 3])
+def test_tile_engine_multipass_ghost_cells(P, O, C, monkeypatch):
+    """Tile engine with 1024-thread tiles (NNGP_TILE_NT=1024: one ghost
+    register per thread, 1024 ghost cells per pass) on 32 tiles at n = 1e5,
+    m = 20: some (tile, colour) holds more ghost cells than a pass, so the
+    hand-off applies them in several passes -- double-buffered at 1 chain, one
+    register set at 3 chains.  Every chain against the oracle's local-form
+    sweep with the same Philox normals (2 sweeps, 1e-8)."""
+    monkeypatch.setenv("NNGP_TILES", "32")
+    monkeypatch.setenv("NNGP_TILE_NT", "1024")
+    monkeypatch.delenv("NNGP_ENGINE", raising=False)
+    n, m = 100_000, 20
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=21)
+    cps = [[1.0, 0.1, 0.0], [0.7, 0.05, 0.0], [1.3, 0.08, 0.0]][:C]
+    rng = np.random.default_rng(2)
+    fields = [rng.normal(size=n) for _ in range(C)]
+    b0s, lss, lnvs, seeds = [0.1, -0.2, 0.3][:C], [0.0, 0.2, -0.3][:C], [-0.5, -0.2, -0.9][:C], [5, 6, 7][:C]
+    with P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=C) as ctx:
+        info = ctx.info
+        assert info["sweep_engine"] == 1 and info["n_tiles"] == 32
+        assert info["tile_ghost_cells_max"] > info["tile_ghost_pass"] == 1024, info
+        Ls = []
+        for k in range(C):
+            ctx.select(k)
+            ctx.factor(0, "exponential_isotropic", cps[k])
+            ctx.set_field(fields[k])
+            ctx.set_mu(None, b0s[k])
+            Ls.append(ctx.get_linv(0))
+        ctx.sweep_chains(2, b0s, lss, lnvs, seeds, [3] * C)
+        got = []
+        for k in range(C):
+            ctx.select(k)
+            got.append(ctx.get_field())
+    for k in range(C):
+        z = O.sweep_normals(seeds[k], 3, 2, n)
+        ref = O.sweep("local", fields[k], Ls[k], NN, col, O.precision_diag(Ls[k], NN), np.ones(n, np.int32), y,
+                      np.full(n, b0s[k]), lm, b0s[k], lss[k], lnvs[k], z)
+        np.testing.assert_allclose(got[k], ref, rtol=1e-8, atol=1e-9, err_msg=f"chain {k}")
