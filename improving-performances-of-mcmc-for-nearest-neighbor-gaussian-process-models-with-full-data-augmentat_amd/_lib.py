@@ -37,8 +37,10 @@ ABI_SYMBOLS = (
     "nngp_tri_solve", "nngp_sweep_timed", "nngp_device_normals",
     "nngp_ctx_create_shard", "nngp_shard_unique_id", "nngp_shard_comm_init", "nngp_sweep_chains_group",
     "nngp_records_reserve", "nngp_record_field", "nngp_get_records",
+    "nngp_shard_ipc_handle", "nngp_shard_ipc_open",
 )
 SHARD_ID_BYTES = 128  # NNGP_SHARD_ID_BYTES
+IPC_HANDLE_BYTES = 64  # NNGP_IPC_HANDLE_BYTES
 
 
 class NNGPError(RuntimeError):
@@ -113,6 +115,8 @@ def _load():
     L.nngp_shard_unique_id.argtypes = [C.c_char_p, C.c_int]
     L.nngp_shard_comm_init.argtypes = [_vp, C.c_char_p, C.c_int]
     L.nngp_sweep_chains_group.argtypes = [C.POINTER(_vp), C.c_int, C.c_int, _dp, _dp, _dp, _up, _up]
+    L.nngp_shard_ipc_handle.argtypes = [_vp, C.c_char_p, C.c_int]
+    L.nngp_shard_ipc_open.argtypes = [_vp, C.c_char_p, C.c_int]
     L.nngp_records_reserve.argtypes = [_vp, C.c_int]
     L.nngp_record_field.argtypes = [_vp, C.c_int]
     L.nngp_get_records.argtypes = [_vp, C.c_int, C.c_int, _dp]

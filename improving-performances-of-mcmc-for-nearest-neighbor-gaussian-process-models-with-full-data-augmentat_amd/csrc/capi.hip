@@ -135,6 +135,13 @@ struct nngp_ctx {
   double2* xbuf_d = nullptr;      // exchange regions of all colours: slot x C
   int* sp_pairs_d = nullptr;      // normal pairs of the rank
   ncclComm_t comm = nullptr;
+  // tile shard (engine 1 on a shard context): rank trank of tG runs tiles
+  // [trank*tTl, (trank+1)*tTl) of the layout (graph_prep.h TileLayout::G)
+  int tG = 0, trank = 0, tTl = 0;
+  uint32_t* rmask_d = nullptr;     // per slot: remote reader ranks
+  TileDev* tdev_d = nullptr;       // kTileRanksMax entries: this rank's TileDev, or a group's
+  double* peer_gx[kTileRanksMax] = {};  // the other ranks' granule buffers (IPC mappings)
+  bool peers_open = false;
   std::map<long long, hipGraphExec_t> graphs;  // key: n_sweeps << 8 | chain mask
   std::vector<hipGraph_t> graph_objs;
 };
@@ -223,6 +230,7 @@ TileDev tile_dev(nngp_ctx* c) {
   D.erow = c->erow_d;
   D.sinfo = c->sinfo_d;
   D.slot_loc = c->compact_loc_d;
+  D.rmask = c->rmask_d;
   D.dr = c->dr_d;
   D.w_slot = c->w_slot_d;
   D.dwx = c->dwx_d;
@@ -350,6 +358,11 @@ void nngp_ctx_destroy(nngp_ctx* c) {
                              c->erow_ptr_d, c->erow_d, c->dwx_d, c->ctl_d, c->tdbg_d, c->sg_row_d,
                              c->sg_recv_d, c->sg_src_d, c->sg_val_d, c->xbuf_d, c->sp_pairs_d};
   if (c->comm) ncclCommDestroy(c->comm);
+  if (c->peers_open)
+    for (int h = 0; h < c->tG; ++h)
+      if (h != c->trank && c->peer_gx[h]) hipIpcCloseMemHandle(c->peer_gx[h]);
+  ptrs.push_back(c->rmask_d);
+  ptrs.push_back(c->tdev_d);
   for (int k = 0; k < kMaxChains; ++k) {
     ChainState& s = c->ch[k];
     ptrs.insert(ptrs.end(), {s.linv_d[0], s.linv_d[1], s.field_d, s.field_prop_d, s.mu_d, s.rec_d});
@@ -428,12 +441,17 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       delete c;
       return fail_msg(nullptr, NNGP_ERR_ARG, "NNGP_ENGINE must be colors or tiles");
     }
-    if (es != "colors" && shard_G == 0) {
+    // shards: the tile shard when it fits (G ranks x up to one tile per CU;
+    // NNGP_TILES = the total), else the colour shard
+    const int G = shard_G > 0 ? shard_G : 1;
+    if (es != "colors" && G <= kTileRanksMax) {
       int cus = 0, lds_max = 0;
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 0;
       if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeSharedMemPerBlockOptin, device) != hipSuccess) lds_max = 0;
-      int T = std::max(1, std::min(cus, (n + kTileTarget - 1) / kTileTarget));
-      if (const char* te = std::getenv("NNGP_TILES")) T = std::max(1, std::min(cus, std::atoi(te)));
+      int T = std::max(1, std::min(G * cus, (n + kTileTarget - 1) / kTileTarget));
+      if (const char* te = std::getenv("NNGP_TILES")) T = std::max(1, std::min(G * cus, std::atoi(te)));
+      T = std::min(T, n);
+      T = std::max(G, T / G * G);  // a multiple of the ranks
       std::string terr;
       int NT = kTileNT;
       if (const char* te = std::getenv("NNGP_TILE_NT")) NT = std::atoi(te);
@@ -441,7 +459,8 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
         delete c;
         return fail_msg(nullptr, NNGP_ERR_ARG, "NNGP_TILE_NT must be 256, 512 or 1024");
       }
-      bool ok = cus > 0 && build_tile_layout(nn.data(), n, b, coloring, locs, d, T, NT, tile_rmax(n_chains, NT), c->tl, terr);
+      bool ok = cus > 0 && T <= n &&
+                build_tile_layout(nn.data(), n, b, coloring, locs, d, T, NT, tile_rmax(n_chains, NT), c->tl, terr, G);
       const int need = ok ? tile_lds_bytes(c->tl.max_rows, n_chains, NT, c->tl.K, c->tl.max_batches, c->tl.max_gslots) : 0;
       if (ok && need > lds_max) {
         ok = false;
@@ -450,6 +469,12 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       }
       if (ok) {
         c->engine = 1;
+        if (shard_G > 0) {
+          c->shard = true;
+          c->tG = G;
+          c->trank = shard_rank;
+          c->tTl = T / G;
+        }
       } else {
         c->tl = TileLayout();
         if (es == "tiles") { delete c; return fail_msg(nullptr, NNGP_ERR_ARG, "tile engine: " + terr); }
@@ -470,6 +495,10 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     if (!build_sweep_layout(nn.data(), n, b, coloring, locs, d, LW, c->lay, err)) {
       delete c;
       return fail_msg(nullptr, NNGP_ERR_ARG, err);
+    }
+    if (shard_G > 0 && shard_G > kMaxRanks) {
+      delete c;
+      return fail_msg(nullptr, NNGP_ERR_ARG, "colour shard: too many ranks");
     }
     if (shard_G > 0) {
       if (!build_shard_plan(nn.data(), n, b, coloring, c->lay, shard_G, shard_rank, c->sp, err)) {
@@ -592,6 +621,11 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     CK(upload(c->erow_d, TL.erow.data(), TL.erow.size(), c->st));
     CK(hipMemsetAsync(c->dwx_d, 0, sizeof(double) * (size_t)n * C * 2, c->st));
     CK(hipMemsetAsync(c->ctl_d, 0, sizeof(unsigned) * 4, c->st));
+    if (c->tG > 1) {
+      CK(dalloc(&c->rmask_d, TL.rmask.size()));
+      CK(upload(c->rmask_d, TL.rmask.data(), TL.rmask.size(), c->st));
+    }
+    if (c->tG > 0) CK(dalloc(&c->tdev_d, kTileRanksMax));
     if (const char* pr = std::getenv("NNGP_PROBE"))
       if ((std::atoi(pr) == 9 || std::atoi(pr) == 2) && (C == 1 || C == 3)) {
         c->tprobe = std::atoi(pr) == 9 ? 1 : 2;
@@ -683,7 +717,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     CK(upload(c->ent_src_d, L.ent_src.data(), (size_t)L.n_entries, c->st));
     CK(hipMemsetAsync(c->ent_val_d, 0, sizeof(double) * std::max<long long>(1, L.n_entries * C), c->st));
   }
-  if (c->shard) {
+  if (c->shard && c->engine == 0) {
     const ShardPlan& SP = c->sp;
     const size_t ng = SP.grow.size();
     CK(dalloc(&c->sg_row_d, ng));
@@ -710,6 +744,10 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       CK(dalloc(&c->dbg_d, (size_t)L.nchunks * 8));
       CK(hipMemset(c->dbg_d, 0, sizeof(unsigned long long) * L.nchunks * 8));
     }
+  if (c->tG > 0) {
+    const TileDev D = tile_dev(c);
+    CK(hipMemcpy(c->tdev_d, &D, sizeof(TileDev), hipMemcpyHostToDevice));
+  }
   CK(hipStreamSynchronize(c->st));
 #undef CK
   *out = c;
@@ -757,11 +795,23 @@ int nngp_ctx_info(const nngp_ctx* c, nngp_info* info) {
   info->n_tiles = c->engine == 1 ? c->tl.T : 0;
   info->tile_rows_max = c->engine == 1 ? c->tl.max_rows : 0;
   info->n_ghost_cells = c->engine == 1 ? (long long)c->tl.gsrc.size() : (long long)c->sp.grow.size();
-  info->n_ranks = c->shard ? c->sp.G : 0;
-  info->rank = c->shard ? c->sp.rank : 0;
-  info->shard_owned = c->shard ? c->sp.owned : 0;
-  info->shard_needed_rows = c->shard ? c->sp.needed_rows : 0;
-  info->shard_exchange_slots = c->shard ? c->sp.xoff[c->sp.K] : 0;
+  if (c->tG > 0) {
+    const TileLayout& TL = c->tl;
+    const int r = c->trank;
+    info->n_ranks = c->tG;
+    info->rank = r;
+    info->shard_owned = TL.rank_slot0[r + 1] - TL.rank_slot0[r];
+    info->shard_needed_rows = TL.erow_ptr[(size_t)(r + 1) * c->tTl] - TL.erow_ptr[(size_t)r * c->tTl];
+    long long x = 0;
+    for (uint32_t m : TL.rmask) x += m != 0;
+    info->shard_exchange_slots = x;
+  } else {
+    info->n_ranks = c->shard ? c->sp.G : 0;
+    info->rank = c->shard ? c->sp.rank : 0;
+    info->shard_owned = c->shard ? c->sp.owned : 0;
+    info->shard_needed_rows = c->shard ? c->sp.needed_rows : 0;
+    info->shard_exchange_slots = c->shard ? c->sp.xoff[c->sp.K] : 0;
+  }
   info->tile_ghost_pass = c->engine == 1 ? c->tl.NT * tile_gmax(c->tl.NT) : 0;
   info->tile_ghost_cells_max = 0;
   if (c->engine == 1)
@@ -1126,6 +1176,10 @@ static int graph_for(nngp_ctx* c, int n_sweeps, int mask, hipGraphExec_t* out, i
 }
 
 static int shard_call(nngp_ctx* c, int n_sweeps, int mask);
+// a call that needs the other ranks (a 1-rank tile shard is a plain tile context)
+static bool sharded_call(const nngp_ctx* c) { return c->shard && !(c->engine == 1 && c->tG == 1); }
+static int shard_ranks(const nngp_ctx* c) { return c->tG > 0 ? c->tG : c->sp.G; }
+static int shard_rank(const nngp_ctx* c) { return c->tG > 0 ? c->trank : c->sp.rank; }
 
 int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double lnv, uint64_t seed,
                uint64_t counter_base, const double* z) {
@@ -1136,7 +1190,7 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
   const int k = c->cur, mask = 1 << k;
   if ((rc = sweep_prepare(c, k, beta0, log_scale, lnv, seed, counter_base))) return rc;
   if ((rc = upload_scalars(c))) return rc;
-  if (c->shard) {
+  if (sharded_call(c)) {
     if (z) return fail_msg(c, NNGP_ERR_ARG, "sweep: injected normals are not supported on shard contexts");
     return shard_call(c, n_sweeps, mask);
   }
@@ -1176,7 +1230,7 @@ int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const doub
   for (int k = 0; k < c->C; ++k)
     if ((rc = sweep_prepare(c, k, beta0[k], log_scale[k], lnv[k], seed[k], counter_base[k]))) return rc;
   if ((rc = upload_scalars(c))) return rc;
-  if (c->shard) return shard_call(c, n_sweeps, (1 << c->C) - 1);
+  if (sharded_call(c)) return shard_call(c, n_sweeps, (1 << c->C) - 1);
   hipGraphExec_t ex;
   if ((rc = graph_for(c, n_sweeps, (1 << c->C) - 1, &ex))) return rc;
   HIPCHK(c, hipGraphLaunch(ex, c->st));
@@ -1289,7 +1343,114 @@ static int shard_plan_check(const nngp_ctx* c) {
   return NNGP_OK;
 }
 
+// ---------------------------------------------------------------- tile shard
+// A call of the tile-sharded sweep on rank trank: prologue
+// (full replica: r = B w of every row), one persistent launch of the rank's
+// tiles (draws read by other ranks' tiles go into their granule buffers over
+// xGMI), then every rank's own slots of w to the others (one RCCL broadcast
+// per rank, in place) and the epilogue (field = w + beta0 of every slot).
+// The next call's launch starts after every rank's broadcast, i.e. after
+// every rank's tiles have stopped polling: granules of consecutive calls
+// never mix (and carry the call id besides).
+static int tile_shard_exchange(nngp_ctx* c) {
+  const TileLayout& TL = c->tl;
+  ncclResult_t e = ncclGroupStart();
+  for (int h = 0; h < c->tG && e == ncclSuccess; ++h) {
+    const size_t s0 = (size_t)TL.rank_slot0[h] * c->C, cnt = (size_t)(TL.rank_slot0[h + 1] - TL.rank_slot0[h]) * c->C;
+    e = ncclBroadcast(c->w_slot_d + s0, c->w_slot_d + s0, cnt, ncclDouble, h, c->comm, c->st);
+  }
+  ncclResult_t e2 = ncclGroupEnd();
+  if (e == ncclSuccess) e = e2;
+  if (e != ncclSuccess) return fail_msg(c, NNGP_ERR_COMM, std::string("tile shard broadcast: ") + ncclGetErrorString(e));
+  return NNGP_OK;
+}
+
+static TileShard tile_shard_args(nngp_ctx* const* ranks, int G, int g0, int Tl) {
+  TileShard sh;
+  sh.G = G;
+  sh.Tl = Tl;
+  sh.tile0 = g0 * Tl;
+  sh.rank0 = g0;
+  sh.devs = ranks[g0]->tdev_d;
+  sh.call = ranks[g0]->ctl_d;
+  for (int h = 0; h < G; ++h) sh.gx[h] = ranks[h]->dwx_d;
+  return sh;
+}
+
+static int tile_shard_call(nngp_ctx* c, int n_sweeps, int mask) {
+  if (!c->comm)
+    return fail_msg(c, NNGP_ERR_STATE, "tile shard: no communicator (nngp_shard_comm_init) -- or use nngp_sweep_chains_group");
+  if (!c->peers_open)
+    return fail_msg(c, NNGP_ERR_STATE, "tile shard: the other ranks' granule buffers are not open (nngp_shard_ipc_open)");
+  if (!c->rmask_d || c->tG < 2) return fail_msg(c, NNGP_ERR_STATE, "tile shard: no remote-reader plan");
+  int rc;
+  if ((rc = enqueue_sweep_body(c, n_sweeps, mask, nullptr, kPrologue))) return rc;
+  HIPCHK(c, launch_tile_call_bump(c->st, c->ctl_d));
+  TileShard sh;
+  sh.G = c->tG;
+  sh.Tl = c->tTl;
+  sh.tile0 = c->trank * c->tTl;
+  sh.rank0 = c->trank;
+  sh.devs = c->tdev_d;
+  sh.call = c->ctl_d;
+  for (int h = 0; h < c->tG; ++h) sh.gx[h] = h == c->trank ? c->dwx_d : c->peer_gx[h];
+  TileLaunch a;
+  a.n_sweeps = n_sweeps;
+  a.chain_mask = mask;
+  a.z_in = nullptr;
+  hipError_t e = launch_sweep_tiles(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NT, c->tl.max_batches,
+                                    c->tl.max_gslots, &sh, c->tTl);
+  if (e == hipSuccess) e = hipMemcpyAsync(c->tmo_h, c->ctl_d + 1, sizeof(unsigned), hipMemcpyDeviceToHost, c->st);
+  // the broadcasts go out even after a failed launch: the peers wait in them
+  rc = tile_shard_exchange(c);
+  if (e != hipSuccess || rc) {
+    if (c->comm) {
+      ncclCommAbort(c->comm);
+      c->comm = nullptr;
+    }
+    return e != hipSuccess ? fail_hip(c, e, "tile shard launch") : rc;
+  }
+  if ((rc = enqueue_sweep_body(c, n_sweeps, mask, nullptr, kEpilogue))) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  return tile_timeout_check(c);
+}
+
+int nngp_shard_ipc_handle(nngp_ctx* c, unsigned char* handle, int len) {
+  if (!c || !handle || len < (int)sizeof(hipIpcMemHandle_t)) return NNGP_ERR_ARG;
+  if (c->tG < 1) return fail_msg(c, NNGP_ERR_STATE, "shard_ipc_handle: not a tile shard context");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  hipIpcMemHandle_t h;
+  HIPCHK(c, hipIpcGetMemHandle(&h, c->dwx_d));
+  std::memcpy(handle, &h, sizeof h);
+  return NNGP_OK;
+}
+
+int nngp_shard_ipc_open(nngp_ctx* c, const unsigned char* handles, int len_each) {
+  if (!c || !handles || len_each < (int)sizeof(hipIpcMemHandle_t)) return NNGP_ERR_ARG;
+  if (c->tG < 1) return fail_msg(c, NNGP_ERR_STATE, "shard_ipc_open: not a tile shard context");
+  if (c->peers_open) return fail_msg(c, NNGP_ERR_STATE, "shard_ipc_open: already open");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  for (int h = 0; h < c->tG; ++h) {
+    if (h == c->trank) continue;
+    hipIpcMemHandle_t hh;
+    std::memcpy(&hh, handles + (size_t)h * len_each, sizeof hh);
+    void* p = nullptr;
+    hipError_t e = hipIpcOpenMemHandle(&p, hh, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+      for (int q = 0; q < h; ++q)
+        if (q != c->trank && c->peer_gx[q]) { hipIpcCloseMemHandle(c->peer_gx[q]); c->peer_gx[q] = nullptr; }
+      return fail_hip(c, e, "hipIpcOpenMemHandle (granule buffer of another rank)");
+    }
+    c->peer_gx[h] = static_cast<double*>(p);
+  }
+  c->peers_open = true;
+  return NNGP_OK;
+}
+
 static int shard_call(nngp_ctx* c, int n_sweeps, int mask) {
+  if (c->engine == 1) return tile_shard_call(c, n_sweeps, mask);
   if (c->sp.G > 1 && !c->comm)
     return fail_msg(c, NNGP_ERR_STATE, "sharded sweep: no communicator (nngp_shard_comm_init) -- or use nngp_sweep_chains_group");
   if (shard_plan_check(c)) return fail_msg(c, NNGP_ERR_ARG, "sharded sweep: inconsistent shard plan");
@@ -1334,7 +1495,7 @@ int nngp_shard_comm_init(nngp_ctx* c, const unsigned char* id, int len) {
   if ((rc = set_device(c))) return rc;
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof u);
-  ncclResult_t e = ncclCommInitRank(&c->comm, c->sp.G, u, c->sp.rank);
+  ncclResult_t e = ncclCommInitRank(&c->comm, shard_ranks(c), u, shard_rank(c));
   if (e != ncclSuccess) {
     c->comm = nullptr;
     return fail_msg(c, NNGP_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(e));
@@ -1342,9 +1503,114 @@ int nngp_shard_comm_init(nngp_ctx* c, const unsigned char* id, int len) {
   return NNGP_OK;
 }
 
+// All ranks of a tile shard in one process: the ranks of each device run in
+// one launch (tiles [g0*Tl, g1*Tl)), the granules of ranks on other devices
+// go to their buffers through peer access; w of every rank's slots reaches the
+// others by device copies.
+static int tile_group_call(nngp_ctx** ctxs, int G, int n_sweeps, const double* beta0, const double* log_scale,
+                           const double* lnv, const uint64_t* seed, const uint64_t* counter_base) {
+  nngp_ctx* c0 = ctxs[0];
+  for (int g = 0; g < G; ++g) {
+    nngp_ctx* c = ctxs[g];
+    if (!c || c->engine != 1 || c->tG != G || c->trank != g || c->tTl != c0->tTl || c->n != c0->n || c->C != c0->C ||
+        c->tl.K != c0->tl.K || c->tl.T != c0->tl.T || !c->rmask_d)
+      return fail_msg(c, NNGP_ERR_ARG, "sweep_chains_group: ctxs[g] must be rank g of a G-rank tile shard of one graph");
+    for (int h = 0; h + 1 < g; ++h)
+      if (ctxs[h]->device == c->device && ctxs[g - 1]->device != c->device)
+        return fail_msg(c, NNGP_ERR_ARG, "sweep_chains_group: the ranks of one device must be contiguous");
+  }
+  if (n_sweeps == 0) return NNGP_OK;
+  const int Tl = c0->tTl, mask = (1 << c0->C) - 1;
+  int rc;
+  std::vector<hipEvent_t> ev(2 * G, nullptr);  // [g]: prologue of rank g done; [G + g]: launch of rank g's device done
+  auto cleanup = [&] {
+    for (auto e : ev) if (e) hipEventDestroy(e);
+  };
+#define GCHK(c, x)                                                     \
+  do {                                                                 \
+    hipError_t e_ = (x);                                               \
+    if (e_ != hipSuccess) { cleanup(); return fail_hip((c), e_, #x); } \
+  } while (0)
+  for (int g = 0; g < G; ++g) {
+    nngp_ctx* c = ctxs[g];
+    if ((rc = set_device(c))) { cleanup(); return rc; }
+    GCHK(c, hipEventCreateWithFlags(&ev[g], hipEventDisableTiming));
+    GCHK(c, hipEventCreateWithFlags(&ev[G + g], hipEventDisableTiming));
+    for (int k = 0; k < c->C; ++k)
+      if ((rc = sweep_prepare(c, k, beta0[k], log_scale[k], lnv[k], seed[k], counter_base[k]))) { cleanup(); return rc; }
+    if ((rc = upload_scalars(c))) { cleanup(); return rc; }
+    if ((rc = enqueue_sweep_body(c, n_sweeps, mask, nullptr, kPrologue))) { cleanup(); return rc; }
+    GCHK(c, launch_tile_call_bump(c->st, c->ctl_d));  // every rank's call id and timeout word
+    GCHK(c, hipEventRecord(ev[g], c->st));
+  }
+  std::vector<TileDev> devs(G);
+  for (int g = 0; g < G; ++g) devs[g] = tile_dev(ctxs[g]);
+  for (int g0 = 0; g0 < G;) {
+    int g1 = g0 + 1;
+    while (g1 < G && ctxs[g1]->device == ctxs[g0]->device) ++g1;
+    nngp_ctx* L = ctxs[g0];
+    set_device(L);
+    int cus = 0;
+    GCHK(L, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, L->device));
+    if ((g1 - g0) * Tl > cus) {
+      cleanup();
+      return fail_msg(L, NNGP_ERR_ARG, "sweep_chains_group: the tiles of the ranks on one device exceed its CUs "
+                                       "(they must all be resident; fewer tiles: NNGP_TILES)");
+    }
+    for (int h = 0; h < G; ++h)
+      if (ctxs[h]->device != L->device) {
+        hipError_t pe = hipDeviceEnablePeerAccess(ctxs[h]->device, 0);
+        if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) GCHK(L, pe);
+        (void)hipGetLastError();
+      }
+    for (int h = g0; h < g1; ++h) GCHK(L, hipStreamWaitEvent(L->st, ev[h], 0));
+    GCHK(L, hipMemcpyAsync(L->tdev_d, devs.data() + g0, sizeof(TileDev) * (g1 - g0), hipMemcpyHostToDevice, L->st));
+    TileShard sh = tile_shard_args(ctxs, G, g0, Tl);
+    TileLaunch a;
+    a.n_sweeps = n_sweeps;
+    a.chain_mask = mask;
+    a.z_in = nullptr;
+    GCHK(L, launch_sweep_tiles(L->st, devs[g0], a, L->tl.max_rows, L->tl.NT, L->tl.max_batches, L->tl.max_gslots, &sh,
+                               (g1 - g0) * Tl));
+    for (int h = g0; h < g1; ++h)
+      GCHK(L, hipMemcpyAsync(ctxs[h]->tmo_h, ctxs[h]->ctl_d + 1, sizeof(unsigned), hipMemcpyDeviceToHost, L->st));
+    for (int h = g0; h < g1; ++h) GCHK(L, hipEventRecord(ev[G + h], L->st));
+    g0 = g1;
+  }
+  // every rank's own slots of w to the others, then the epilogues
+  const TileLayout& TL = c0->tl;
+  for (int g = 0; g < G; ++g) {
+    nngp_ctx* c = ctxs[g];
+    set_device(c);
+    for (int h = 0; h < G; ++h) GCHK(c, hipStreamWaitEvent(c->st, ev[G + h], 0));
+    for (int h = 0; h < G; ++h) {
+      if (h == g) continue;
+      const size_t s0 = (size_t)TL.rank_slot0[h] * c->C, cnt = (size_t)(TL.rank_slot0[h + 1] - TL.rank_slot0[h]) * c->C;
+      GCHK(c, hipMemcpyAsync(c->w_slot_d + s0, ctxs[h]->w_slot_d + s0, cnt * sizeof(double), hipMemcpyDefault, c->st));
+    }
+    if ((rc = enqueue_sweep_body(c, n_sweeps, mask, nullptr, kEpilogue))) { cleanup(); return rc; }
+  }
+  for (int g = 0; g < G; ++g) {
+    set_device(ctxs[g]);
+    GCHK(ctxs[g], hipStreamSynchronize(ctxs[g]->st));
+  }
+#undef GCHK
+  cleanup();
+  for (int g = 0; g < G; ++g)
+    if ((rc = tile_timeout_check(ctxs[g]))) return rc;
+  return NNGP_OK;
+}
+
 int nngp_sweep_chains_group(nngp_ctx** ctxs, int G, int n_sweeps, const double* beta0, const double* log_scale,
                             const double* lnv, const uint64_t* seed, const uint64_t* counter_base) {
   if (!ctxs || G < 1 || n_sweeps < 0 || !beta0 || !log_scale || !lnv || !seed || !counter_base) return NNGP_ERR_ARG;
+  if (ctxs[0] && ctxs[0]->engine == 1) {
+    if (G > kTileRanksMax) return fail_msg(ctxs[0], NNGP_ERR_ARG, "sweep_chains_group: too many ranks");
+    // one rank: the plain tile sweep (no remote readers, no plan masks)
+    if (G == 1 && ctxs[0]->tG == 1)
+      return nngp_sweep_chains(ctxs[0], n_sweeps, beta0, log_scale, lnv, seed, counter_base);
+    return tile_group_call(ctxs, G, n_sweeps, beta0, log_scale, lnv, seed, counter_base);
+  }
   for (int g = 0; g < G; ++g) {
     nngp_ctx* c = ctxs[g];
     if (!c || !c->shard || c->sp.G != G || c->sp.rank != g || c->n != ctxs[0]->n || c->C != ctxs[0]->C ||
@@ -1428,7 +1694,7 @@ int nngp_sweep_timed(nngp_ctx* c, int n_sweeps, const double* beta0, const doubl
                      const double* lnv, const uint64_t* seed, const uint64_t* counter_base, double* ms,
                      double* kernel_ms) {
   if (!c || n_sweeps < 1 || !ms || !beta0 || !log_scale || !lnv || !seed || !counter_base) return NNGP_ERR_ARG;
-  if (c->shard) return fail_msg(c, NNGP_ERR_STATE, "sweep_timed: not available on shard contexts");
+  if (sharded_call(c)) return fail_msg(c, NNGP_ERR_STATE, "sweep_timed: not available on shard contexts");
   int rc;
   if ((rc = set_device(c))) return rc;
   for (int k = 0; k < c->C; ++k)

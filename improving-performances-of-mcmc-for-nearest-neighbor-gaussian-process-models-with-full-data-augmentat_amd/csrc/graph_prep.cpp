@@ -509,13 +509,16 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
 
 // ---------------------------------------------------------------- tile layout
 bool build_tile_layout(const int* nn, int n, int b, const int* colors, const double* locs, int d, int T,
-                       int NT, int RMAX, TileLayout& L, std::string& err) {
+                       int NT, int RMAX, TileLayout& L, std::string& err, int G) {
   L = TileLayout();
   L.n = n; L.b = b; L.NT = NT; L.RMAX = RMAX;
   if (NT < 64 || NT > 1024 || RMAX < 1 || (long long)NT * RMAX > (1 << 20)) { err = "tile layout: bad NT/RMAX"; return false; }
   if (T < 1) T = 1;
   if (T > n) T = n;
+  if (G < 1 || G > kMaxTileRanks || T % G != 0) { err = "tile layout: need 1 <= G <= 16 ranks dividing the tile count"; return false; }
   L.T = T;
+  L.G = G;
+  const int Tl = T / G;  // tiles per rank
   int K = 0;
   for (int i = 0; i < n; ++i) {
     if (colors[i] < 1) { err = "coloring must be 1-based positive"; return false; }
@@ -586,6 +589,9 @@ bool build_tile_layout(const int* nn, int n, int b, const int* colors, const dou
       slot_of[i] = x;
     }
   }
+  L.rank_slot0.assign(G + 1, 0);
+  for (int g = 0; g <= G; ++g) L.rank_slot0[g] = tc_ptr[(size_t)g * Tl * K];
+  if (G > 1) L.rmask.assign(n, 0u);
   L.slot_f0.assign(n, 0);
   L.batch_ptr.assign((size_t)T * K + 1, 0);
   L.gptr.assign((size_t)T * K + 1, 0);
@@ -680,6 +686,7 @@ bool build_tile_layout(const int* nn, int n, int b, const int* colors, const dou
         L.gsrc.push_back(gh[c][g + 2]);
         const int u = tile_of[L.compact_loc[x]];
         if (nbmark[u] != (int)pc) { nbmark[u] = (int)pc; L.nb.push_back(u); }
+        if (G > 1 && u / Tl != t / Tl) L.rmask[x] |= 1u << (t / Tl);
       }
       for (size_t q = gs0; q < L.gslot.size(); ++q) gidx[L.gslot[q]] = -1;
       L.gslot_ptr[pc + 1] = (int)L.gslot.size();

@@ -128,12 +128,20 @@ struct TileLayout {
   std::vector<int> gslot_ptr;        // T*K + 1
   int max_gslots = 0;                // max foreign slots of a (tile, colour)
   std::vector<int> nb_ptr, nb;       // T*K + 1, neighbour tiles of each (tile, colour)
+  // tile-sharded sweep over G ranks (G > 1): rank g runs tiles [g*T/G, (g+1)*T/G)
+  // and owns their slots [rank_slot0[g], rank_slot0[g+1]) (slot order is tile-major)
+  int G = 1;
+  std::vector<int> rank_slot0;       // G + 1
+  std::vector<uint32_t> rmask;       // n (G > 1): bit h = a tile of rank h != the owner's reads the slot's dw
 };
 
 // Fails (returns false, err set) when the layout does not fit the packed
 // formats; the caller checks the LDS budget (max_rows).
+// G > 1: the tiles of a G-rank tile shard (T a multiple of G, G <= kMaxTileRanks):
+// also the ranks' slot ranges and the remote-reader mask of every slot.
+constexpr int kMaxTileRanks = 16;
 bool build_tile_layout(const int* nn_rowmajor, int n, int b, const int* colors, const double* locs_colmajor,
-                       int d, int T, int NT, int RMAX, TileLayout& L, std::string& err);
+                       int d, int T, int NT, int RMAX, TileLayout& L, std::string& err, int G = 1);
 
 // Colour-sharded sweep over G ranks on top of a
 // SweepLayout (every rank builds the same layout from the same inputs):

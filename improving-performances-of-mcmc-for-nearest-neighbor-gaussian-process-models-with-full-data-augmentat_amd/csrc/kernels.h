@@ -153,6 +153,7 @@ struct TileDev {
   const int* erow;            // local row -> device row
   const int2* sinfo;          // per slot {obs_per_loc, f0 | exported}
   const int* slot_loc;        // per slot: location (normals)
+  const uint32_t* rmask;      // tile shard: per slot, ranks (other than the owner's) reading its dw, else null
   double2* dr;                // per slot x C {precision_diag, residuals_sum}
   double* w_slot;             // per slot x C
   double* dwx;                // per slot x C: 16-byte granules {dw, epoch, call id}
@@ -182,8 +183,23 @@ constexpr int tile_double_buffer(int C, int NT) { return C <= 2 ? 1 : 0; }
 constexpr int tile_rmax(int C, int NT) { return 4096 / NT; }
 // ghost-cell registers per thread: NT * GMAX ghost cells of a (tile, colour) per pass
 constexpr int tile_gmax(int NT) { return NT == 256 ? 4 : (NT == 512 ? 3 : 1); }
+// Tile-sharded sweep: the T tiles of the layout are split
+// over G ranks (rank h runs tiles [h*Tl, (h+1)*Tl)); a launch runs the tiles
+// [tile0, tile0 + grid) -- one rank's (a process per GPU) or every rank's
+// (the ranks of a group on one device).  A draw read by tiles of other ranks
+// is also stored into those ranks' granule buffers (peer memory over xGMI),
+// so every tile polls its own rank's buffer only.
+constexpr int kTileRanksMax = 16;
+struct TileShard {
+  int G = 1, Tl = 0, tile0 = 0, rank0 = 0;
+  const TileDev* devs = nullptr;     // device array: the TileDev of ranks rank0, rank0 + 1, ... of this launch
+  const unsigned* call = nullptr;    // call-id word of the launch (every rank tags with the same id)
+  double* gx[kTileRanksMax] = {};    // granule buffer of every rank (this process's mapping)
+};
 hipError_t launch_sweep_tiles(hipStream_t st, const TileDev& D, const TileLaunch& a, int max_rows, int NT,
-                              int max_batches, int max_gslots);
+                              int max_batches, int max_gslots, const TileShard* sh = nullptr, int grid = 0);
+// ctl[0] += 1 (call id), ctl[1] = 0 (timeout word): before every launch of a rank
+hipError_t launch_tile_call_bump(hipStream_t st, unsigned* ctl);
 // chain `chain`: cell/ghost values from Linv (device order) and precision_diag
 hipError_t launch_tile_refresh(hipStream_t st, const TileDev& D, int nbatches, int NT, const int* cell_src,
                                const int* gsrc, const double* linv, int chain);

@@ -1169,6 +1169,17 @@ __global__ void tile_call_bump_kernel(unsigned* ctl) {
   ctl[1] = 0u;   // timeout word
 }
 
+hipError_t launch_tile_call_bump(hipStream_t st, unsigned* ctl) {
+  hipLaunchKernelGGL(tile_call_bump_kernel, dim3(1), dim3(1), 0, st, ctl);
+  return hipGetLastError();
+}
+
+// granule cache policy: sc1 (device scope: the producer's write-through store,
+// the consumer's L2-bypassing poll, coherent across the XCDs); tile shard:
+// sc0|sc1 (system scope) for the stores into other ranks' buffers and the
+// polls, which see draws arriving from peer GPUs over xGMI
+constexpr int kGranAux = 16, kGranAuxSys = 17;
+
 // registers of one own batch: this thread's cells (f = t*R + j) and its draw
 // items u = t + k*NT < nslots*C (slot q = u / C, chain u % C: per-slot
 // records of consecutive items are consecutive, the loads coalesce).  Item
@@ -1178,6 +1189,7 @@ template <int C, int NT, int RMAX>
 struct TileBatchRegs {
   static constexpr int IMAX = (kTSlots * C + NT - 1) / NT;
   int R, ns, x0;
+  uint32_t rm[IMAX];          // tile shard: remote readers of the slot
   uint32_t pk[RMAX];
   double v[RMAX][C];
   int nobs[IMAX], flag[IMAX], loc[IMAX];
@@ -1186,7 +1198,7 @@ struct TileBatchRegs {
 };
 
 // the batch's per-slot records (the draw preparation waits for them)
-template <int C, int NT, int RMAX>
+template <int C, int NT, int RMAX, int SH>
 __device__ __forceinline__ void tile_load_items(const TileDev& D, const int4 B, TileBatchRegs<C, NT, RMAX>& b, int t) {
   b.ns = B.z; b.x0 = B.w;
 #pragma unroll
@@ -1199,6 +1211,7 @@ __device__ __forceinline__ void tile_load_items(const TileDev& D, const int4 B, 
       b.nobs[k] = si.x;
       b.flag[k] = si.y;
       b.loc[k] = D.slot_loc[b.x0 + q];
+      if (SH) b.rm[k] = D.rmask[b.x0 + q];
       const double2 dr = D.dr[xu];
       b.a0[k] = dr.x;
       b.a1[k] = dr.y;
@@ -1225,9 +1238,9 @@ __device__ __forceinline__ void tile_load_cells(const TileDev& D, const int4 B, 
   }
 }
 
-template <int C, int NT, int RMAX>
+template <int C, int NT, int RMAX, int SH>
 __device__ __forceinline__ void tile_load_batch(const TileDev& D, const int4 B, TileBatchRegs<C, NT, RMAX>& b, int t) {
-  tile_load_items<C, NT, RMAX>(D, B, b, t);
+  tile_load_items<C, NT, RMAX, SH>(D, B, b, t);
   tile_load_cells<C, NT, RMAX>(D, B, b, t);
 }
 
@@ -1296,6 +1309,7 @@ struct TileState {
   __amdgpu_buffer_rsrc_t gran;
   unsigned call;
   unsigned* tmo;
+  int G;                            // tile shard: ranks (1: single GPU)
   bool timed_out;
   int T, t, lane, wv, K, nph, ph;
   unsigned long long tp[8], t_prev;
@@ -1339,8 +1353,8 @@ __device__ __forceinline__ void seg_scan_step(double (&v)[C], int& f) {
 // one own batch of colour c (epoch): products -> slot totals -> draws ->
 // scatter.  LDS and registers only, plus the draws' stores: no global load
 // (a load here would wait behind the next batch's prefetch, vmcnt is in order)
-template <int C, int NT, int RMAX, int PROBE>
-__device__ __forceinline__ void tile_own_draw(const TileDev& D, const TileLaunch& a, TileState& S,
+template <int C, int NT, int RMAX, int PROBE, int SH>
+__device__ __forceinline__ void tile_own_draw(const TileDev& D, const TileLaunch& a, const TileShard& sh, TileState& S,
                                               TileBatchRegs<C, NT, RMAX>& b, unsigned epoch) {
   constexpr int IMAX = TileBatchRegs<C, NT, RMAX>::IMAX;
   const int t = S.t, lane = S.lane, wv = S.wv;
@@ -1438,7 +1452,16 @@ __device__ __forceinline__ void tile_own_draw(const TileDev& D, const TileLaunch
         // tag word also checks the payload, so a torn read (new tag, old dw --
         // not observed on gfx950, not architecturally excluded) is not taken
         g.x = (unsigned)uu; g.y = (unsigned)(uu >> 32); g.z = epoch; g.w = S.call ^ g.x ^ g.y;
-        __builtin_amdgcn_raw_buffer_store_b128(g, S.gran, (int)(xu * 16), 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(g, S.gran, (int)(xu * 16), 0, SH ? kGranAuxSys : kGranAux);
+        if (SH) {
+          // the same granule into the buffer of every other rank with a reader
+#pragma unroll
+          for (int h = 0; h < kTileRanksMax; ++h)
+            if (h < S.G && ((b.rm[k] >> h) & 1u))
+              __builtin_amdgcn_raw_buffer_store_b128(
+                  g, __builtin_amdgcn_make_buffer_rsrc(sh.gx[h], 0, 0x7FFFFFFF, 0x00020000), (int)(xu * 16), 0,
+                  kGranAuxSys);
+        }
       }
     }
   }
@@ -1474,8 +1497,8 @@ __device__ __forceinline__ void tile_own_scatter(TileState& S, const TileBatchRe
 // the normals pregenerated by a separate kernel -- no Philox here,
 // 132 instead of 255 VGPRs at 1 chain --, double buffering at 3 chains, an L2
 // prefetch of the next stream during the own work, other load orders.)
-template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE>
-__device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a, TileState& S, int ph,
+template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE, int SH>
+__device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a, const TileShard& sh, TileState& S, int ph,
                                            TileBatchRegs<C, NT, RMAX>& cur, TileBatchRegs<C, NT, RMAX>& nxt,
                                            TileGhostRegs<C, GMAX>& gr, TileGhostRegs<C, GMAX>& grn) {
   const int K = S.K, t = S.t;
@@ -1497,7 +1520,7 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
   if (DB) {
     // the next colour's first batch (and ghost chunk): their HBM stream
     // overlaps this colour's work (two register sets)
-    if (more) tile_load_batch<C, NT, RMAX>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
+    if (more) tile_load_batch<C, NT, RMAX, SH>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
     if (has_next && gn1 > gn0) tile_load_ghosts<C, NT, GMAX>(D, gn0, gn1, grn, t);
   }
   // ---- 1. own batches.  One register set (!DB): after the draw of the last
@@ -1510,15 +1533,15 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
   for (int bi = bfirst; bi < bend; ++bi) {
     if (bi != bfirst) {  // rare: a colour with more than one batch in this tile
       __syncthreads();   // acc_s is indexed by slot-in-batch: every wave is done with the last batch
-      tile_load_batch<C, NT, RMAX>(D, S.batch_s[bi], cur, t);
+      tile_load_batch<C, NT, RMAX, SH>(D, S.batch_s[bi], cur, t);
       tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, s, cur, t);
     }
-    tile_own_draw<C, NT, RMAX, PROBE>(D, a, S, cur, epoch);
+    tile_own_draw<C, NT, RMAX, PROBE, SH>(D, a, sh, S, cur, epoch);
     const int R = cur.R;
     if (!DB && bi + 1 == bend) {
-      if (more) tile_load_items<C, NT, RMAX>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
+      if (more) tile_load_items<C, NT, RMAX, SH>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
       if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
-      if (pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * C + t % C) * 16), 0, 16);
+      if (pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * C + t % C) * 16), 0, SH ? kGranAuxSys : kGranAux);
     }
     tile_own_scatter<C, NT, RMAX, PROBE>(S, cur, R);
   }
@@ -1527,14 +1550,14 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
   // draw scalars, then (two register sets) the first poll
   if (!DB) {
     if (bend == bfirst) {  // no own batch of this colour in the tile
-      if (more) tile_load_items<C, NT, RMAX>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
+      if (more) tile_load_items<C, NT, RMAX, SH>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
       if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
-      if (pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * C + t % C) * 16), 0, 16);
+      if (pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * C + t % C) * 16), 0, SH ? kGranAuxSys : kGranAux);
     }
     if (more) tile_load_cells<C, NT, RMAX>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
   }
   if (more) tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, sn, nxt, t);
-  if (DB && pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * C + t % C) * 16), 0, 16);
+  if (DB && pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * C + t % C) * 16), 0, SH ? kGranAuxSys : kGranAux);
   TSTAMP(S, 5);
   TLSTAMP(S, 4);
   // ---- 3. hand-off: the granule of each (foreign slot, chain) of this colour
@@ -1547,7 +1570,7 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
       const int x = u0 == 0 ? gsl_pref : D.gslot[gs0 + u / C];
       const int ch = u % C;
       const int off = (int)(((size_t)x * C + ch) * 16);
-      u32x4_t g = u0 == 0 ? gfirst : __builtin_amdgcn_raw_buffer_load_b128(S.gran, off, 0, 16);
+      u32x4_t g = u0 == 0 ? gfirst : __builtin_amdgcn_raw_buffer_load_b128(S.gran, off, 0, SH ? kGranAuxSys : kGranAux);
       double dw = 0.0;
       for (unsigned spins = 0;; ++spins) {
         if (g.z == epoch && (g.w ^ g.x ^ g.y) == S.call) {
@@ -1555,13 +1578,16 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
           if (PROBE == 2) atomicMax(S.spin_s, spins);
           break;
         }
-        if (S.timed_out || spins > (1u << 20)) {
+        // bounded wait (about a second per poll); once any tile of the launch
+        // has given up (timeout word), the others stop waiting within ~1k polls
+        if (S.timed_out || spins > (1u << 20) ||
+            ((spins & 1023u) == 1023u && __hip_atomic_load(S.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
           if (!S.timed_out) __hip_atomic_store(S.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           S.timed_out = true;
           break;
         }
         __builtin_amdgcn_s_sleep(1);
-        g = __builtin_amdgcn_raw_buffer_load_b128(S.gran, off, 0, 16);
+        g = __builtin_amdgcn_raw_buffer_load_b128(S.gran, off, 0, SH ? kGranAuxSys : kGranAux);
       }
       S.gdw_s[u] = dw;
     }
@@ -1587,13 +1613,18 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
   TLSTAMP(S, 3);
 }
 
-template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE>
-__global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D, TileLaunch a) {
+template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE, int SH>
+__global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D0, TileLaunch a, TileShard sh) {
   using BR = TileBatchRegs<C, NT, RMAX>;
   constexpr int NW = NT / 64;
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  // tile shard: global tile index, its rank, that rank's buffers
+  const int Tg = SH ? sh.tile0 + (int)blockIdx.x : (int)blockIdx.x;
+  const int rk = SH ? Tg / sh.Tl : 0;
+  const TileDev D = SH ? sh.devs[rk - sh.rank0] : D0;
   TileState S;
-  S.T = blockIdx.x; S.t = threadIdx.x; S.lane = S.t & 63; S.wv = S.t >> 6; S.K = D.K;
+  S.G = SH ? sh.G : 1;
+  S.T = Tg; S.t = threadIdx.x; S.lane = S.t & 63; S.wv = S.t >> 6; S.K = D.K;
   S.nph = a.n_sweeps * D.K;
   S.timed_out = false;
   for (int k = 0; k < 8; ++k) S.tp[k] = 0;
@@ -1633,14 +1664,14 @@ __global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D, TileLaunch a
     S.seed_s[2 * t] = D.scal[t].seed;
     S.seed_s[2 * t + 1] = D.scal[t].counter_base;
   }
-  S.call = D.ctl[0];
+  S.call = SH ? *sh.call : D.ctl[0];
   S.tmo = D.ctl + 1;
-  S.gran = __builtin_amdgcn_make_buffer_rsrc(D.dwx, 0, 0x7FFFFFFF, 0x00020000);
+  S.gran = __builtin_amdgcn_make_buffer_rsrc(SH ? sh.gx[rk] : D.dwx, 0, 0x7FFFFFFF, 0x00020000);
   __syncthreads();
   BR A, B;  // batch register sets: the current colour's and (DB) the next one's
   TileGhostRegs<C, GMAX> GA, GB;
   if (S.nph > 0 && S.bptr_s[0] < S.bptr_s[1]) {
-    tile_load_batch<C, NT, RMAX>(D, S.batch_s[S.bptr_s[0]], A, t);
+    tile_load_batch<C, NT, RMAX, SH>(D, S.batch_s[S.bptr_s[0]], A, t);
     tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, 0, A, t);
   }
   if (DB && S.nph > 0 && S.gptr_s[0] < S.gptr_s[1]) tile_load_ghosts<C, NT, GMAX>(D, S.gptr_s[0], S.gptr_s[1], GA, t);
@@ -1648,11 +1679,11 @@ __global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D, TileLaunch a
   TSTAMP(S, 7);
   if (DB) {
     for (int ph = 0; ph < S.nph; ph += 2) {
-      tile_phase<C, NT, RMAX, GMAX, DB, PROBE>(D, a, S, ph, A, B, GA, GB);
-      if (ph + 1 < S.nph) tile_phase<C, NT, RMAX, GMAX, DB, PROBE>(D, a, S, ph + 1, B, A, GB, GA);
+      tile_phase<C, NT, RMAX, GMAX, DB, PROBE, SH>(D, a, sh, S, ph, A, B, GA, GB);
+      if (ph + 1 < S.nph) tile_phase<C, NT, RMAX, GMAX, DB, PROBE, SH>(D, a, sh, S, ph + 1, B, A, GB, GA);
     }
   } else {
-    for (int ph = 0; ph < S.nph; ++ph) tile_phase<C, NT, RMAX, GMAX, DB, PROBE>(D, a, S, ph, A, A, GA, GA);
+    for (int ph = 0; ph < S.nph; ++ph) tile_phase<C, NT, RMAX, GMAX, DB, PROBE, SH>(D, a, sh, S, ph, A, A, GA, GA);
   }
   if (PROBE == 1 && t == 0) {
     unsigned long long* o = D.dbg + (size_t)T * 8;
@@ -1661,52 +1692,69 @@ __global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D, TileLaunch a
 }
 #undef TSTAMP
 
-template <int C, int NT, int PROBE>
-static hipError_t launch_tiles_c(hipStream_t st, const TileDev& D, const TileLaunch& a, int lds) {
+// sh == nullptr: one GPU, the call-id bump and the whole grid of tiles here;
+// else the caller bumped the call ids and `grid` tiles from sh->tile0 run
+template <int C, int NT, int PROBE, int SH>
+static hipError_t launch_tiles_c(hipStream_t st, const TileDev& D, const TileLaunch& a, int lds, const TileShard* sh,
+                                 int grid) {
   constexpr int RMAX = tile_rmax(C, NT);
   constexpr int DB = tile_double_buffer(C, NT);
   constexpr int GMAX = tile_gmax(NT);
-  auto k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE>;
+  auto k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE, SH>;
   lds = lds < kTSpreadLds ? kTSpreadLds : lds;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(tile_call_bump_kernel, dim3(1), dim3(1), 0, st, D.ctl);
-  hipLaunchKernelGGL(k, dim3(D.T), dim3(NT), lds, st, D, a);
+  if constexpr (SH) {
+    hipLaunchKernelGGL(k, dim3(grid), dim3(NT), lds, st, D, a, *sh);
+  } else {
+    hipLaunchKernelGGL(tile_call_bump_kernel, dim3(1), dim3(1), 0, st, D.ctl);
+    hipLaunchKernelGGL(k, dim3(D.T), dim3(NT), lds, st, D, a, TileShard());
+  }
   return hipGetLastError();
 }
 
 template <int NT>
-static hipError_t launch_tiles_nt(hipStream_t st, const TileDev& D, const TileLaunch& a, int lds) {
+static hipError_t launch_tiles_nt(hipStream_t st, const TileDev& D, const TileLaunch& a, int lds, const TileShard* sh,
+                                  int grid) {
+  if (sh) {
+    switch (D.C) {
+      case 1: return launch_tiles_c<1, NT, 0, 1>(st, D, a, lds, sh, grid);
+      case 2: return launch_tiles_c<2, NT, 0, 1>(st, D, a, lds, sh, grid);
+      case 3: return launch_tiles_c<3, NT, 0, 1>(st, D, a, lds, sh, grid);
+      case 4: return launch_tiles_c<4, NT, 0, 1>(st, D, a, lds, sh, grid);
+      default: return hipErrorInvalidValue;
+    }
+  }
   if (D.dbg && D.probe == 1) {
     switch (D.C) {
-      case 1: return launch_tiles_c<1, NT, 1>(st, D, a, lds);
-      case 3: return launch_tiles_c<3, NT, 1>(st, D, a, lds);
+      case 1: return launch_tiles_c<1, NT, 1, 0>(st, D, a, lds, nullptr, 0);
+      case 3: return launch_tiles_c<3, NT, 1, 0>(st, D, a, lds, nullptr, 0);
       default: break;
     }
   }
   if (D.dbg && D.probe == 2) {
     switch (D.C) {
-      case 1: return launch_tiles_c<1, NT, 2>(st, D, a, lds);
-      case 3: return launch_tiles_c<3, NT, 2>(st, D, a, lds);
+      case 1: return launch_tiles_c<1, NT, 2, 0>(st, D, a, lds, nullptr, 0);
+      case 3: return launch_tiles_c<3, NT, 2, 0>(st, D, a, lds, nullptr, 0);
       default: break;
     }
   }
   switch (D.C) {
-    case 1: return launch_tiles_c<1, NT, 0>(st, D, a, lds);
-    case 2: return launch_tiles_c<2, NT, 0>(st, D, a, lds);
-    case 3: return launch_tiles_c<3, NT, 0>(st, D, a, lds);
-    case 4: return launch_tiles_c<4, NT, 0>(st, D, a, lds);
+    case 1: return launch_tiles_c<1, NT, 0, 0>(st, D, a, lds, nullptr, 0);
+    case 2: return launch_tiles_c<2, NT, 0, 0>(st, D, a, lds, nullptr, 0);
+    case 3: return launch_tiles_c<3, NT, 0, 0>(st, D, a, lds, nullptr, 0);
+    case 4: return launch_tiles_c<4, NT, 0, 0>(st, D, a, lds, nullptr, 0);
     default: return hipErrorInvalidValue;
   }
 }
 
 hipError_t launch_sweep_tiles(hipStream_t st, const TileDev& D, const TileLaunch& a, int max_rows, int NT,
-                              int max_batches, int max_gslots) {
+                              int max_batches, int max_gslots, const TileShard* sh, int grid) {
   const int lds = tile_lds_bytes(max_rows, D.C, NT, D.K, max_batches, max_gslots);
   switch (NT) {
-    case 256: return launch_tiles_nt<256>(st, D, a, lds);
-    case 512: return launch_tiles_nt<512>(st, D, a, lds);
-    case 1024: return launch_tiles_nt<1024>(st, D, a, lds);
+    case 256: return launch_tiles_nt<256>(st, D, a, lds, sh, grid);
+    case 512: return launch_tiles_nt<512>(st, D, a, lds, sh, grid);
+    case 1024: return launch_tiles_nt<1024>(st, D, a, lds, sh, grid);
     default: return hipErrorInvalidValue;
   }
 }

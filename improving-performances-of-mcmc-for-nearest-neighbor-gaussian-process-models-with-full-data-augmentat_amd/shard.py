@@ -1,5 +1,13 @@
-"""Colour-sharded chromatic sweep: ONE set of chains swept by several GPUs
+"""Sharded chromatic sweep: ONE set of chains swept by several GPUs
 (DESIGN.md §6).
+
+Two engines behind the same interface (nngp_ctx_info's sweep_engine):
+ - tile shard (default when the tile layout fits): the persistent tile sweep
+   with its tiles split over the ranks; the draws other ranks' tiles read are
+   written straight into their granule buffers (peer memory over xGMI, HIP
+   IPC), one launch per call, then one RCCL broadcast of every rank's slots;
+ - colour shard (NNGP_ENGINE=colors, or when the tiles do not fit): one
+   launch per colour and an RCCL all-gather of the colour's values.
 
 The reference sweeps a colour class at a time (Scripts/mcmc_nngp_update_Gaussian.R:261-275);
 the locations of one class are conditionally independent, so each rank (one
@@ -25,13 +33,13 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import SHARD_ID_BYTES, check, lib
+from ._lib import IPC_HANDLE_BYTES, SHARD_ID_BYTES, check, lib
 from .context import ChainContext
 
 
 class ShardContext(ChainContext):
-    """Rank ``rank`` of an ``n_ranks``-way colour-sharded context (the
-    colour-launch sweep engine).  Same interface as ChainContext."""
+    """Rank ``rank`` of an ``n_ranks``-way sharded context (tile shard, or
+    colour shard with NNGP_ENGINE=colors).  Same interface as ChainContext."""
 
     def __init__(self, locs, NNarray, coloring, locs_match, observed_field, n_ranks: int, rank: int,
                  device: int = -1, n_chains: int = 1):
@@ -43,6 +51,21 @@ class ShardContext(ChainContext):
         """Collective over the ranks: the RCCL communicator of the shard."""
         assert len(uid) >= SHARD_ID_BYTES
         self._chk(lib.nngp_shard_comm_init(self._h, bytes(uid), len(uid)))
+
+    @property
+    def tile_shard(self) -> bool:
+        return self.info["sweep_engine"] == 1
+
+    def ipc_handle(self) -> bytes:
+        """Tile shard: the HIP IPC handle of this rank's granule buffer."""
+        buf = C.create_string_buffer(IPC_HANDLE_BYTES)
+        self._chk(lib.nngp_shard_ipc_handle(self._h, buf, IPC_HANDLE_BYTES))
+        return buf.raw
+
+    def ipc_open(self, handles) -> None:
+        """Tile shard: map the other ranks' granule buffers (handles in rank order)."""
+        assert len(handles) == self.n_ranks and all(len(h) == IPC_HANDLE_BYTES for h in handles)
+        self._chk(lib.nngp_shard_ipc_open(self._h, b"".join(handles), IPC_HANDLE_BYTES))
 
 
 def shard_unique_id() -> bytes:
@@ -60,8 +83,14 @@ def broadcast_unique_id(dist) -> bytes:
 
 
 def init_shard_comm(ctx: ShardContext, dist) -> None:
+    """Collective over the torch.distributed group: the RCCL communicator and,
+    for a tile shard, the exchange of the granule-buffer IPC handles."""
     if ctx.n_ranks > 1:
         ctx.comm_init(broadcast_unique_id(dist))
+        if ctx.tile_shard:
+            handles = [None] * ctx.n_ranks
+            dist.all_gather_object(handles, ctx.ipc_handle())
+            ctx.ipc_open(handles)
 
 
 def sweep_chains_group(ctxs, n_sweeps: int, beta0, log_scale, log_noise_variance, seed, counter_base) -> None:

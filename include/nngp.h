@@ -50,8 +50,9 @@
 extern "C" {
 #endif
 
-#define NNGP_ABI_VERSION 6
+#define NNGP_ABI_VERSION 7
 #define NNGP_SHARD_ID_BYTES 128 /* RCCL unique id */
+#define NNGP_IPC_HANDLE_BYTES 64 /* HIP IPC handle of a tile shard's granule buffer */
 
 typedef enum {
   NNGP_OK = 0,
@@ -97,11 +98,13 @@ typedef struct {
   int n_tiles;       /* tiles (persistent workgroups) of the tile engine */
   int tile_rows_max; /* max local rows (own + foreign) of a tile: its LDS-resident r */
   long long n_ghost_cells; /* foreign-member cells the tiles (or shard ranks) apply after a hand-off */
-  int n_ranks;       /* shard contexts: ranks of the colour-sharded sweep (0: not sharded) */
+  int n_ranks;       /* shard contexts: ranks of the sharded sweep (0: not sharded);
+                        sweep_engine 0: colour shard, 1: tile shard */
   int rank;          /* shard contexts: this context's rank */
   long long shard_owned;          /* locations swept by this rank */
   long long shard_needed_rows;    /* rows of B its columns touch (its r halo included) */
-  long long shard_exchange_slots; /* slots of all colours' exchange regions (padded) */
+  long long shard_exchange_slots; /* colour shard: slots of all colours' exchange regions (padded);
+                                     tile shard: locations whose draws other ranks read */
   int tile_ghost_pass;       /* tile engine: ghost cells a (tile, colour) applies per register pass */
   int tile_ghost_cells_max;  /* tile engine: most ghost cells of one (tile, colour) */
 } nngp_info;
@@ -222,10 +225,26 @@ int nngp_shard_unique_id(unsigned char* id, int len);
 /* collective over the n_ranks contexts: RCCL communicator of the shard */
 int nngp_shard_comm_init(nngp_ctx* ctx, const unsigned char* id, int len);
 /* all n_ranks shard contexts in ONE process (ctxs[g] = rank g; any devices):
- * nngp_sweep_chains with the exchange done by device copies between them */
+ * nngp_sweep_chains with the exchange done by device copies between them.
+ * Tile shards: the ranks of one device run in one launch (their tiles must fit
+ * the device's CUs together), ranks on one device contiguous. */
 int nngp_sweep_chains_group(nngp_ctx** ctxs, int n_ranks, int n_sweeps, const double* beta0,
                             const double* log_scale, const double* log_noise_variance,
                             const uint64_t* seed, const uint64_t* counter_base);
+
+/* Tile shard (sweep_engine 1 on a shard context, the default when the tile
+ * layout fits): the tile-resident sweep with its tiles split over the ranks
+ * (rank g runs tiles [g*T/G, (g+1)*T/G) on its GPU).  A draw read by a tile
+ * of another rank is written into that rank's granule buffer (peer memory
+ * over xGMI) by the producing tile, so the hand-offs stay inside the one
+ * persistent launch per call; after it, every rank's own slots reach the
+ * others (RCCL broadcasts).  Before the first sweep, after
+ * nngp_shard_comm_init: every rank exports its buffer's handle, the handles
+ * are exchanged out of band (all-gather), and every rank opens the others'.
+ * NNGP_ENGINE=colors at creation selects the colour shard instead. */
+int nngp_shard_ipc_handle(nngp_ctx* ctx, unsigned char* handle, int len);
+/* handles: n_ranks x len_each bytes, rank order (this rank's entry ignored) */
+int nngp_shard_ipc_open(nngp_ctx* ctx, const unsigned char* handles, int len_each);
 
 /* ---------- measurement ---------- */
 /* nngp_sweep_chains bracketed by HIP events on the context's stream;

@@ -93,6 +93,8 @@ nngp_device_normals <- function(device, seed, sweep, n)
 
 nngp_shard_unique_id <- function() .Call(C_nngp_shard_unique_id)
 nngp_shard_comm_init <- function(ctx, id) invisible(.Call(C_nngp_shard_comm_init, ctx, id))
+nngp_shard_ipc_handle <- function(ctx) .Call(C_nngp_shard_ipc_handle, ctx)
+nngp_shard_ipc_open <- function(ctx, handles) invisible(.Call(C_nngp_shard_ipc_open, ctx, handles))
 nngp_sweep_chains_group <- function(ctxs, n_sweeps, beta_0, log_scale, log_noise_variance, seed, counter_base)
   invisible(.Call(C_nngp_sweep_chains_group, ctxs, as.integer(n_sweeps), as.double(beta_0), as.double(log_scale),
                   as.double(log_noise_variance), as.double(seed), as.double(counter_base)))

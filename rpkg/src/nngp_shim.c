@@ -354,7 +354,7 @@ SEXP C_nngp_device_normals(SEXP device, SEXP seed, SEXP sweep, SEXP n) {
   return z;
 }
 
-/* ---------- colour-sharded sweep ---------- */
+/* ---------- sharded sweep (colour shard / tile shard) ---------- */
 SEXP C_nngp_shard_unique_id(void) {
   SEXP id = PROTECT(Rf_allocVector(RAWSXP, NNGP_SHARD_ID_BYTES));
   check(nngp_shard_unique_id(RAW(id), NNGP_SHARD_ID_BYTES), NULL);
@@ -380,6 +380,30 @@ SEXP C_nngp_sweep_chains_group(SEXP ctxs, SEXP n_sweeps, SEXP beta0, SEXP log_sc
   to_u64(seed, s, k);
   to_u64(counter_base, cb, k);
   check(nngp_sweep_chains_group(cs, G, as_int(n_sweeps), REAL(beta0), REAL(log_scale), REAL(lnv), s, cb), cs[0]);
+  return R_NilValue;
+}
+
+/* tile shard: HIP IPC handle of this rank's granule buffer (a raw vector the
+   ranks exchange out of band), and the mapping of the others' (list of raws) */
+SEXP C_nngp_shard_ipc_handle(SEXP p) {
+  nngp_ctx* c = get_ctx(p);
+  SEXP h = PROTECT(Rf_allocVector(RAWSXP, NNGP_IPC_HANDLE_BYTES));
+  check(nngp_shard_ipc_handle(c, RAW(h), NNGP_IPC_HANDLE_BYTES), c);
+  UNPROTECT(1);
+  return h;
+}
+
+SEXP C_nngp_shard_ipc_open(SEXP p, SEXP handles) {
+  nngp_ctx* c = get_ctx(p);
+  const int G = (int)XLENGTH(handles);
+  if (G < 1 || G > 16) Rf_error("nngp: 1..16 ranks in a tile shard");
+  unsigned char buf[16 * NNGP_IPC_HANDLE_BYTES];
+  for (int g = 0; g < G; ++g) {
+    SEXP h = VECTOR_ELT(handles, g);
+    if (TYPEOF(h) != RAWSXP || XLENGTH(h) != NNGP_IPC_HANDLE_BYTES) Rf_error("nngp: IPC handles must be raw(64)");
+    memcpy(buf + (size_t)g * NNGP_IPC_HANDLE_BYTES, RAW(h), NNGP_IPC_HANDLE_BYTES);
+  }
+  check(nngp_shard_ipc_open(c, buf, NNGP_IPC_HANDLE_BYTES), c);
   return R_NilValue;
 }
 
@@ -424,6 +448,8 @@ static const R_CallMethodDef call_methods[] = {
     E(C_nngp_shard_unique_id, 0),
     E(C_nngp_shard_comm_init, 2),
     E(C_nngp_sweep_chains_group, 7),
+    E(C_nngp_shard_ipc_handle, 1),
+    E(C_nngp_shard_ipc_open, 2),
     {NULL, NULL, 0}};
 #undef E
 

@@ -7,7 +7,11 @@
 // the published dw -- with each tile's r in its own local-row array, so it
 // checks the layout (local rows, batches, stream positions, start/end flags,
 // ghost cells, exported flags, neighbour lists) and the algorithm together.
-// Usage: tile_sweep_check <n> <m> <tiles> <chains> <seed>  (prints "ok <stats>")
+// With G > 1 (a tile shard): the tiles of rank g = [g*T/G, (g+1)*T/G), one
+// granule buffer per rank, poisoned (NaN) before each colour: a draw reaches
+// a reader of another rank only through the remote puts of the plan (rmask),
+// which must be exactly the set of reader ranks; rank slot ranges checked.
+// Usage: tile_sweep_check <n> <m> <tiles> <chains> <seed> [NT RMAX G]  (prints "ok <stats>")
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -37,6 +41,7 @@ int main(int argc, char** argv) {
   const int seed = argc > 5 ? std::atoi(argv[5]) : 1;
   const int NT = argc > 6 ? std::atoi(argv[6]) : 256;
   const int RMAX = argc > 7 ? std::atoi(argv[7]) : 16;
+  const int G = argc > 8 ? std::atoi(argv[8]) : 1;
   const int d = 2, b = m + 1, sweeps = 3;
   std::mt19937_64 g(seed);
   std::uniform_real_distribution<double> U(0, 1);
@@ -52,7 +57,7 @@ int main(int argc, char** argv) {
   const int K = greedy_coloring(nn.data(), n, b, col);
   TileLayout L;
   std::string err;
-  if (!build_tile_layout(nn.data(), n, b, col.data(), locs.data(), d, T, NT, RMAX, L, err)) {
+  if (!build_tile_layout(nn.data(), n, b, col.data(), locs.data(), d, T, NT, RMAX, L, err, G)) {
     std::printf("FAIL build: %s\n", err.c_str());
     return 1;
   }
@@ -152,7 +157,31 @@ int main(int argc, char** argv) {
       REQUIRE((int)seen.size() == L.erow_ptr[t + 1] - L.erow_ptr[t]);
       for (int r = L.tile_row0[t]; r < L.tile_row0[t + 1]; ++r) REQUIRE(L.erow[L.erow_ptr[t] + r - L.tile_row0[t]] == r);
     }
+    // tile shard: rank slot ranges = the slots of the rank's tiles; rmask = the
+    // ranks (other than the owner's) of the tiles with a ghost cell of the slot
+    REQUIRE(L.G == G && (int)L.rank_slot0.size() == G + 1 && L.rank_slot0[0] == 0 && L.rank_slot0[G] == n);
+    const int Tl = L.T / G;
+    for (int t = 0; t < L.T; ++t)
+      for (int bi = L.batch_ptr[(size_t)t * K]; bi < L.batch_ptr[(size_t)t * K + K]; ++bi) {
+        const TileBatch B = L.batch[bi];
+        REQUIRE(B.slot0 >= L.rank_slot0[t / Tl] && B.slot0 + B.nslots <= L.rank_slot0[t / Tl + 1]);
+      }
+    if (G > 1) {
+      std::vector<uint32_t> want(n, 0u);
+      for (int t = 0; t < L.T; ++t)
+        for (int pc = t * K; pc < t * K + K; ++pc)
+          for (int q = L.gslot_ptr[pc]; q < L.gslot_ptr[pc + 1]; ++q) {
+            const int x = L.gslot[q];
+            int ro = 0;
+            while (L.rank_slot0[ro + 1] <= x) ++ro;
+            if (ro != t / Tl) want[x] |= 1u << (t / Tl);
+          }
+      REQUIRE(L.rmask == want);
+    }
   }
+  const int Tl = L.T / G;
+  std::vector<std::vector<double>> gbuf(G, std::vector<double>((size_t)n * C, 0.0));  // per-rank granule buffers
+  long long remote_puts = 0;
   std::vector<double> f0s(NT);
   long long ghosts_applied = 0;
   for (int s = 0; s < sweeps; ++s) {
@@ -174,6 +203,7 @@ int main(int argc, char** argv) {
       }
     }
     for (int c = 0; c < K; ++c) {
+      for (auto& gb : gbuf) std::fill(gb.begin(), gb.end(), std::nan(""));
       for (int t = 0; t < L.T; ++t) {
         const int pc = t * K + c;
         std::vector<double>& r_s = rt[t];
@@ -230,7 +260,15 @@ int main(int argc, char** argv) {
               const double dw = wn - wv;
               w[(size_t)x * C + ch] = wn;
               acc_s[(size_t)q * C + ch] = dw;
-              if (L.slot_f0[x] & kSlotExported) dwx[(size_t)x * C + ch] = dw;
+              if (L.slot_f0[x] & kSlotExported) {
+                dwx[(size_t)x * C + ch] = dw;
+                gbuf[t / Tl][(size_t)x * C + ch] = dw;  // own rank's buffer
+                for (int h = 0; h < G; ++h)
+                  if (G > 1 && ((L.rmask[x] >> h) & 1u)) {
+                    gbuf[h][(size_t)x * C + ch] = dw;  // remote put
+                    ++remote_puts;
+                  }
+              }
             }
           }
           for (size_t e = B.off; e < (size_t)B.off + (size_t)B.R * NT; ++e) {
@@ -255,7 +293,11 @@ int main(int argc, char** argv) {
           int owner = 0;
           while (L.tile_row0[owner + 1] <= row) ++owner;
           REQUIRE(owner != t && nbs.count(owner));
-          for (int ch = 0; ch < C; ++ch) rt[t][(size_t)lr * C + ch] += gval[ch * ng + gi] * dwx[(size_t)x * C + ch];
+          for (int ch = 0; ch < C; ++ch) {
+            const double dwv = gbuf[t / Tl][(size_t)x * C + ch];  // the reader polls its own rank's buffer
+            REQUIRE(!std::isnan(dwv) && dwv == dwx[(size_t)x * C + ch]);
+            rt[t][(size_t)lr * C + ch] += gval[ch * ng + gi] * dwv;
+          }
           ++ghosts_applied;
         }
       }
@@ -268,7 +310,7 @@ int main(int argc, char** argv) {
       maxrel = std::max(maxrel, std::fabs(a - r) / std::max(1.0, std::fabs(r)));
     }
   if (!(maxrel < 1e-11)) { std::printf("FAIL maxrel %.3e\n", maxrel); return 1; }
-  std::printf("ok K=%d T=%d max_rows=%d batches=%zu cells=%zu ghosts=%zu nb=%zu maxrel=%.2e\n", K, L.T, L.max_rows,
-              L.batch.size(), ncell, ng, L.nb.size(), maxrel);
+  std::printf("ok K=%d T=%d G=%d max_rows=%d batches=%zu cells=%zu ghosts=%zu nb=%zu remote_puts=%lld maxrel=%.2e\n",
+              K, L.T, G, L.max_rows, L.batch.size(), ncell, ng, L.nb.size(), remote_puts, maxrel);
   return 0;
 }

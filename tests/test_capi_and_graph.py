@@ -20,7 +20,7 @@ def test_header_symbols_exported(P):
     lib = C.CDLL(str(_lib.LIB_PATH))
     for s in sorted(declared):
         assert hasattr(lib, s), s
-    assert P.lib.nngp_abi_version() == 6
+    assert P.lib.nngp_abi_version() == 7
 
 
 def test_library_has_gfx950_code_object():
@@ -160,6 +160,24 @@ def test_tile_sweep_emulation(tile_check_exe, n, m, tiles, chains, seed, nt, rma
     out = subprocess.run([str(tile_check_exe), str(n), str(m), str(tiles), str(chains), str(seed), str(nt),
                           str(rmax)], capture_output=True, text=True)
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
+
+
+@pytest.mark.parametrize("n,m,tiles,G,chains,seed", [
+    (3000, 10, 16, 2, 1, 1), (5000, 15, 24, 8, 3, 2), (2000, 8, 12, 3, 2, 3), (400, 5, 16, 16, 1, 4),
+    (60000, 15, 64, 8, 1, 5), (8, 2, 8, 8, 1, 6)])
+def test_tile_shard_plan_emulation(tile_check_exe, n, m, tiles, G, chains, seed):
+    """Tile shard: the emulation with one granule buffer per
+    rank, poisoned before every colour, so a ghost cell of another rank's
+    slot only sees the draw through the plan's remote puts; the remote-reader
+    masks must equal the brute-force set of reader ranks, and the ranks' slot
+    ranges hold exactly their tiles' slots.  Same 1e-11 bar against the
+    serial sweep."""
+    import subprocess
+
+    out = subprocess.run([str(tile_check_exe), str(n), str(m), str(tiles), str(chains), str(seed), "256", "16",
+                          str(G)], capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
+    assert G == 1 or int(out.stdout.split("remote_puts=")[1].split()[0]) > 0 or n < 16
 
 
 @pytest.mark.parametrize("n,m,G,sweeps,seed", [(3000, 10, 2, 2, 1), (5000, 15, 3, 2, 2), (2000, 5, 8, 2, 3),

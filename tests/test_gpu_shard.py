@@ -1,10 +1,15 @@
-"""Colour-sharded sweep on the GPU, through the C ABI.
-
-All ranks of a shard run in this one process on device 0
-(nngp_sweep_chains_group: the exchange of each colour is a device copy of the
-other ranks' segments instead of the RCCL all-gather).  The per-rank kernels,
-the plan and the exchange layout are the ones the RCCL path uses; the
-multi-process RCCL transport itself needs one GPU per rank (8-GPU node).
+"""Sharded sweep on the GPU, through the C ABI,
+for both shard engines (every test runs twice):
+ - tiles: the tile shard -- the ranks' tiles run in ONE launch on device 0
+   (each rank with its own context, buffers and granule buffer; a draw read
+   by another rank's tile reaches it only through the remote put into that
+   rank's buffer, exactly as across GPUs), then device copies of every
+   rank's slots instead of the RCCL broadcasts.  NNGP_TILES fixes the tile
+   count, so 1 rank and G ranks share one layout;
+ - colors: the colour shard -- the exchange of each colour is a device copy
+   of the other ranks' segments instead of the RCCL all-gather.
+The per-rank kernels and plans are the ones the multi-process path uses; the
+multi-process transport itself needs one GPU per rank (8-GPU node).
 
 Bars: every rank's field == the 1-rank shard field, bitwise (the ranks apply
 the same updates in the same order); the 1-rank shard vs the oracle's
@@ -19,6 +24,13 @@ from conftest import make_problem
 pytestmark = pytest.mark.gpu
 
 CP = [1.0, 0.08, 0.0]
+
+
+@pytest.fixture(autouse=True, params=["tiles", "colors"])
+def engine(request, monkeypatch):
+    monkeypatch.setenv("NNGP_ENGINE", request.param)
+    monkeypatch.setenv("NNGP_TILES", "120")  # divisible by every G below; <= the CUs of one device
+    return request.param
 
 
 def _shards(P, prob, G, C, fields, b0):
@@ -45,7 +57,7 @@ def _fields(ctx, C):
 
 @pytest.mark.parametrize("n,m,G,C", [(6000, 10, 2, 1), (6000, 10, 3, 3), (20000, 15, 8, 1), (3000, 5, 5, 2),
                                      (40, 3, 4, 1)])
-def test_group_shard_equals_single_rank_bitwise(P, n, m, G, C):
+def test_group_shard_equals_single_rank_bitwise(P, engine, n, m, G, C):
     prob = make_problem(P, n, m, seed=n + G)
     rng = np.random.default_rng(G)
     fields = [rng.normal(size=n) for _ in range(C)]
@@ -57,7 +69,10 @@ def test_group_shard_equals_single_rank_bitwise(P, n, m, G, C):
     want = _fields(ref, C)
     ctxs = _shards(P, prob, G, C, fields, b0)
     info = ctxs[0].info
-    assert info["n_ranks"] == G and info["sweep_engine"] == 0
+    assert info["n_ranks"] == G and info["sweep_engine"] == (1 if engine == "tiles" else 0)
+    if engine == "tiles":
+        assert info["n_tiles"] == min(120, n) and ref.info["n_tiles"] == info["n_tiles"]
+        assert G == 1 or n < 100 or info["shard_exchange_slots"] > 0
     assert sum(c.info["shard_owned"] for c in ctxs) == n
     P.sweep_chains_group(ctxs, 3, *args)
     for g, ctx in enumerate(ctxs):
