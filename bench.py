@@ -14,9 +14,12 @@ chains of a GPU share one context and sweep in the same kernels
 runs the reference's per-iteration call shape: n_chromatic = 10 sweeps per
 call (r = B w refresh + 10 sweeps).  A single-chain context is timed too
 ("single_chain" in config).
-Multi-GPU: every rank runs its own chains on its own synthetic field (the
-reference's chain-level parallelism, mclapply -> ranks): weak scaling, no
-data-path collective (DESIGN.md "Multi-GPU").
+Multi-GPU (N > 1): the tile-sharded sweep of ONE field whose
+size grows with N (n = N x 1e6; every GPU keeps the tile geometry of the
+n=1e6 headline): weak scaling, value = chain-sweeps/s x n/1e6.  A small
+cross-GPU parity check (N-rank shard == one GPU, bitwise) runs first and is
+reported.  --multi shard-strong keeps n fixed; --multi replicas runs
+independent chains per GPU (the reference's mclapply -> ranks).
 """
 from __future__ import annotations
 
@@ -219,67 +222,145 @@ def timed_region(run, steps, warmup, dist=None, sync=lambda: None):
     return el, ctr
 
 
-def shard_main(P, args, world, rank, local_rank, dist):
-    """--shard: the colour-sharded sweep.  Every rank builds the
-    same workload (same seed) and sweeps its spatial block of every colour; a
-    step = one sweep of every chain of the ONE shared set of chains, so value
-    = chain-sweeps/s of the whole job (strong scaling)."""
+def shard_parity_check(P, args, world, rank, local_rank, dist):
+    """Cross-GPU parity at a small size, run by every rank before the sharded
+    measurement: the world-rank tile shard (IPC granule puts over xGMI, RCCL
+    broadcasts) against this GPU alone with the same tiles, bitwise after 3
+    sweeps of 2 chains; -> True on every rank iff every rank matched."""
     import torch
 
-    from nngp_amd.shard import ShardContext, init_shard_comm
+    from nngp_amd.shard import ShardContext, _agreed, init_shard_comm
+
+    n, m, C = 20000, 10, 2
+    rng = np.random.default_rng(99)
+    locs = rng.uniform(size=(n, 2))
+    locs = locs[P.order_maxmin(locs) - 1]
+    NN = P.find_ordered_nn(locs, m)
+    col = P.naive_greedy_coloring(NN)
+    lm = np.arange(1, n + 1, dtype=np.int32)
+    y = rng.normal(size=n)
+    fields = [rng.normal(size=n) for _ in range(C)]
+    args_c = ([0.1, 0.2], [0.0, 0.1], [-0.5, -0.3], [5, 6], [0, 0])
+    old = os.environ.get("NNGP_TILES")
+    os.environ["NNGP_TILES"] = str(16 * world)  # the same tiles on one GPU and over the ranks
+    try:
+        res = []
+        for shard in (False, True):
+            # every step that may fail on one rank is agreed before the next
+            # collective (a rank never waits for a peer that has given up)
+            ctx = _agreed(dist, lambda: (
+                ShardContext(locs, NN, col, lm, y, n_ranks=world, rank=rank, device=local_rank, n_chains=C)
+                if shard else P.ChainContext(locs, NN, col, lm, y, device=local_rank, n_chains=C)))
+            if shard:
+                init_shard_comm(ctx, dist)
+            for k in range(C):
+                ctx.select(k)
+                ctx.factor(0, "exponential_isotropic", [1.0, 0.1, 0.0])
+                ctx.set_field(fields[k])
+                ctx.set_mu(None, args_c[0][k])
+            ctx.sweep_chains(3, *args_c)
+            out = []
+            for k in range(C):
+                ctx.select(k)
+                out.append(ctx.get_field())
+            res.append((out, ctx.info))
+            ctx.close()
+    finally:
+        if old is None:
+            os.environ.pop("NNGP_TILES", None)
+        else:
+            os.environ["NNGP_TILES"] = old
+    ok = all(np.array_equal(a, b) for a, b in zip(res[0][0], res[1][0])) and res[1][1]["sweep_engine"] == 1
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item()), {"n": n, "m": m, "chains": C, "sweeps": 3, "tiles": 16 * world,
+                            "exchange_slots_rank0": res[1][1]["shard_exchange_slots"]}
+
+
+def shard_main(P, args, world, rank, local_rank, dist, scaling):
+    """The sharded sweep of ONE set of chains over the world GPUs (DESIGN.md
+    §6; tile shard by default, colour shard with NNGP_ENGINE=colors).  Every
+    rank builds the same workload (same seed).  scaling "weak": n = world x
+    --n (every GPU keeps the tiles of an n=--n field: 256 tiles of ~3.9k
+    locations at 1e6); "strong": n = --n split over the GPUs.  A step = one
+    sweep of every chain; value = chain-sweeps/s x n / 1e6, i.e. sweeps of
+    1e6-location fields per second (a sweep of the 8e6-location field counts 8)."""
+    import torch
+
+    from nngp_amd.shard import ShardContext, _agreed, init_shard_comm
 
     covfun, cp, C, nc = args.covfun, [1.0, args.range, 0.0], args.chains, args.n_chromatic
-    log(f"shard setup n={args.n} m={args.m} {covfun} chains={C} world={world}", rank)
-    wl = make_workload(P, args.n, args.m, covfun, cp, seed=1000, device=local_rank, chains=C)
-    ctx = ShardContext(wl["locs"], wl["NN"], wl["col"], wl["lm"], wl["y"], n_ranks=world, rank=rank,
-                       device=local_rank, n_chains=C)
-    init_shard_comm(ctx, dist)
-    rng = np.random.default_rng(7)
-    for k in range(C):
-        ctx.select(k)
-        ctx.factor(0, covfun, cp)
-        ctx.set_field(wl["beta0"] + wl["w"] + 0.1 * rng.normal(size=len(wl["y"])))
-        ctx.set_mu(None, wl["beta0"])
-    ctx.select(0)
-    info = ctx.info
-    b0, ls, lnv = wl["beta0"], wl["log_scale"], wl["log_noise_variance"]
-    seeds = [77 + k for k in range(C)]
+    n = args.n * world if scaling == "weak" else args.n
+    t_par = time.time()
+    parity, pinfo = shard_parity_check(P, args, world, rank, local_rank, dist) if world > 1 else (None, None)
+    log(f"cross-GPU parity check ({time.time() - t_par:.1f}s): {parity}", rank)
+    if world > 1 and not parity:
+        raise RuntimeError("sharded sweep differs from one GPU on the parity check")
+    log(f"shard setup n={n} m={args.m} {covfun} chains={C} world={world} scaling={scaling}", rank)
+    agree = (lambda f: _agreed(dist, f)) if world > 1 else (lambda f: f())
+    wl = agree(lambda: make_workload(P, n, args.m, covfun, cp, seed=1000, device=local_rank, chains=C))
+    ctx = agree(lambda: ShardContext(wl["locs"], wl["NN"], wl["col"], wl["lm"], wl["y"], n_ranks=world, rank=rank,
+                                     device=local_rank, n_chains=C))
+    try:
+        init_shard_comm(ctx, dist)
+        rng = np.random.default_rng(7)
 
-    def run(nsw, base):
-        done = 0
-        while done < nsw:
-            s = min(nc, nsw - done)
-            ctx.sweep_chains(s, [b0] * C, [ls] * C, [lnv] * C, seeds, [base + done] * C)
-            done += s
-        return base + done
+        def prep():
+            for k in range(C):
+                ctx.select(k)
+                ctx.factor(0, covfun, cp)
+                ctx.set_field(wl["beta0"] + wl["w"] + 0.1 * rng.normal(size=len(wl["y"])))
+                ctx.set_mu(None, wl["beta0"])
+            ctx.select(0)
 
-    sync = (lambda: torch.cuda.synchronize(local_rank)) if torch.cuda.is_available() else (lambda: None)
-    elapsed, _ = timed_region(run, args.steps, args.warmup, dist, sync)
-    n, nnz = args.n, info["nnz"]
+        agree(prep)
+        info = ctx.info
+        b0, ls, lnv = wl["beta0"], wl["log_scale"], wl["log_noise_variance"]
+        seeds = [77 + k for k in range(C)]
+
+        def run(nsw, base):
+            done = 0
+            while done < nsw:
+                s = min(nc, nsw - done)
+                ctx.sweep_chains(s, [b0] * C, [ls] * C, [lnv] * C, seeds, [base + done] * C)
+                done += s
+            return base + done
+
+        sync = (lambda: torch.cuda.synchronize(local_rank)) if torch.cuda.is_available() else (lambda: None)
+        log(f"graph prep {wl['t_graph']:.1f}s colours={info['n_colors']} engine={info['sweep_engine']} "
+            f"tiles={info['n_tiles']} owned={info['shard_owned']} exchange_slots={info['shard_exchange_slots']}", rank)
+        elapsed, _ = timed_region(run, args.steps, args.warmup, dist, sync)
+    finally:
+        ctx.close()
+    nnz = info["nnz"]
+    tiles = info["sweep_engine"] == 1
     bytes_sweep = C * (8 * nnz + 40 * n) + 4 * nnz
     achieved = bytes_sweep * args.steps / elapsed / 1e9 / world  # per GPU, whole sharded call (wall clock)
+    how = ("tile shard: the tiles of all GPUs in one persistent launch per GPU and call, cross-GPU hand-offs "
+           "as 16-B granules stored into the reader GPU's buffer over xGMI (HIP IPC), RCCL broadcast of each "
+           "rank's slots per call" if tiles else "colour shard: one launch per colour, RCCL all-gather per colour")
     out = {"metric": "full-field Gibbs sweeps/sec at n=1e6, m=15; achieved HBM GB/s vs roofline",
-           "value": args.steps * C / elapsed, "unit": "sweeps/s", "n_gpus": world, "steps": args.steps,
-           "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
-           "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+           "value": args.steps * C * (n / 1e6) / elapsed, "unit": "sweeps/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
+           "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f64",
            "data": "synthetic (U[0,1]^2 locations, exact max-min order, field drawn from the Vecchia prior)",
-           "config": {"workload": (f"colour-sharded chromatic sweep n={n} m={args.m} {covfun} range={args.range}, "
-                                   f"{C} chains swept by all {world} GPUs (value = chain-sweeps/s)"),
+           "config": {"workload": (f"sharded chromatic sweep of ONE field n={n} m={args.m} {covfun} "
+                                   f"range={args.range}, {C} chains swept by all {world} GPUs "
+                                   f"(value = chain-sweeps/s x n/1e6)"),
                       "n": n, "m": args.m, "n_colors": info["n_colors"], "nnz": nnz, "chains": C,
-                      "n_chromatic_per_call": nc, "sweep_engine": "colours (sharded)",
-                      "owned_rank0": info["shard_owned"], "needed_rows_rank0": info["shard_needed_rows"],
-                      "ghost_cells_rank0": info["n_ghost_cells"],
-                      "parallelism": f"colour classes sharded over {world} GPUs, RCCL all-gather per colour"},
+                      "chain_sweeps_per_s": args.steps * C / elapsed,
+                      "n_chromatic_per_call": nc, "sweep_engine": "tile shard" if tiles else "colour shard",
+                      "n_tiles": info["n_tiles"], "owned_rank0": info["shard_owned"],
+                      "needed_rows_rank0": info["shard_needed_rows"],
+                      "exchange_slots": info["shard_exchange_slots"],
+                      "parity_check": {"bitwise_equal_to_one_gpu": parity, **(pinfo or {})},
+                      "parallelism": f"{how}; {world} GPUs"},
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                        "kernel": "whole sharded call per GPU (wall clock: sweep launches + all-gathers)",
+                        "kernel": "whole sharded call per GPU (wall clock)",
                         "algorithmic_bytes_per_sweep": bytes_sweep},
            "cpu_baseline": None}
-    ctx.close()
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if dist:
-        dist.destroy_process_group()
+    return out
 
 
 def main():
@@ -299,14 +380,19 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--mcmc-iters", type=int, default=10,
                     help="timed MCMC iterations for the secondary metric (0: skip)")
-    ap.add_argument("--shard", action="store_true",
-                    help="colour-sharded sweep of ONE set of chains over the N GPUs (RCCL all-gather per colour; "
-                         "strong scaling) instead of independent chains per GPU")
+    ap.add_argument("--multi", choices=["shard-weak", "shard-strong", "replicas"], default="shard-weak",
+                    help="N > 1: the sharded sweep of ONE field over the N GPUs with n = N x --n (shard-weak, "
+                         "default) or n = --n (shard-strong), or independent chains per GPU (replicas)")
+    ap.add_argument("--shard", action="store_true", help="the sharded sweep even at N = 1 (strong)")
+    ap.add_argument("--no-fallback", action="store_true",
+                    help="exit with an error when the sharded sweep fails instead of measuring replicas")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("NNGP_BENCH_DEVICE"):  # test hook: every rank on this device
+        local_rank = int(os.environ["NNGP_BENCH_DEVICE"])
     import torch
 
     dist = None
@@ -319,8 +405,33 @@ def main():
     P = _pkgload.load()
     covfun = args.covfun
     cp = [1.0, args.range, 0.0]
-    if args.shard:
-        return shard_main(P, args, world, rank, local_rank, dist)
+    note = None
+    if args.shard or (world > 1 and args.multi != "replicas"):
+        scaling = "weak" if (world > 1 and args.multi == "shard-weak") else "strong"
+        try:
+            out = shard_main(P, args, world, rank, local_rank, dist, scaling)
+        except Exception as e:  # noqa: BLE001 -- reported in the JSON line, then the replicas measurement
+            out = None
+            note = f"sharded sweep failed on rank {rank}: {type(e).__name__}: {e}"
+            log(note, 0)
+        if world > 1:
+            import torch as _t
+
+            ok = _t.tensor([0 if out is None else 1], dtype=_t.int32)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if not ok.item() and note is None:
+                note = "sharded sweep failed on another rank"
+                out = None
+        if out is not None:
+            if rank == 0:
+                print(json.dumps(out), flush=True)
+            if dist:
+                dist.destroy_process_group()
+            return
+        if args.no_fallback:
+            if dist:
+                dist.destroy_process_group()
+            raise SystemExit(f"bench: {note}")
     log(f"setup n={args.n} m={args.m} {covfun} chains={args.chains} world={world}", rank)
     wl = make_workload(P, args.n, args.m, covfun, cp, seed=1000 + rank, device=local_rank, chains=args.chains)
     C = args.chains
@@ -423,7 +534,8 @@ def main():
                       "n_tiles": info["n_tiles"], "tile_rows_max": info["tile_rows_max"],
                       "n_ghost_cells": info["n_ghost_cells"],
                       "single_chain": single,
-                      "parallelism": f"chains {C} per GPU x {world} GPUs (independent)"},
+                      "parallelism": f"chains {C} per GPU x {world} GPUs (independent)",
+                      "multi_gpu_note": note},
            "roofline": roofline, "cpu_baseline": cpu, "secondary": mcmc}
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -82,15 +82,33 @@ def broadcast_unique_id(dist) -> bytes:
     return obj[0]
 
 
+def _agreed(dist, fn):
+    """fn() on every rank, then agreement over the group: if it raised on any
+    rank, every rank raises (no rank goes on to a step its peers never reach)."""
+    res, err = None, None
+    try:
+        res = fn()
+    except Exception as e:  # noqa: BLE001 -- re-raised below on every rank
+        err = f"{type(e).__name__}: {e}"
+    errs = [None] * dist.get_world_size()
+    dist.all_gather_object(errs, err)
+    bad = [(r, e) for r, e in enumerate(errs) if e is not None]
+    if bad:
+        raise RuntimeError("shard setup failed: " + "; ".join(f"rank {r}: {e}" for r, e in bad))
+    return res
+
+
 def init_shard_comm(ctx: ShardContext, dist) -> None:
     """Collective over the torch.distributed group: the RCCL communicator and,
-    for a tile shard, the exchange of the granule-buffer IPC handles."""
+    for a tile shard, the exchange of the granule-buffer IPC handles (every
+    step agreed by all ranks before the next)."""
     if ctx.n_ranks > 1:
-        ctx.comm_init(broadcast_unique_id(dist))
+        uid = broadcast_unique_id(dist)
+        _agreed(dist, lambda: ctx.comm_init(uid))
         if ctx.tile_shard:
             handles = [None] * ctx.n_ranks
-            dist.all_gather_object(handles, ctx.ipc_handle())
-            ctx.ipc_open(handles)
+            dist.all_gather_object(handles, _agreed(dist, ctx.ipc_handle))
+            _agreed(dist, lambda: ctx.ipc_open(handles))
 
 
 def sweep_chains_group(ctxs, n_sweeps: int, beta0, log_scale, log_noise_variance, seed, counter_base) -> None:

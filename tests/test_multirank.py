@@ -89,3 +89,71 @@ def test_shard_unique_id_broadcast_two_ranks():
         p.join(timeout=30)
         assert p.exitcode == 0
     assert out[0] == out[1] == bytes(range(128))
+
+
+class _FakeTileShard:
+    """Stands in for a tile-shard ShardContext (the IPC and RCCL calls need a
+    GPU): records what init_shard_comm hands it."""
+
+    def __init__(self, rank, fail_open=False):
+        self.n_ranks, self.rank, self.tile_shard, self.fail_open = 2, rank, True, fail_open
+        self.uid = self.opened = None
+
+    def comm_init(self, uid):
+        self.uid = uid
+
+    def ipc_handle(self):
+        return bytes([self.rank + 1]) * 64
+
+    def ipc_open(self, handles):
+        if self.fail_open:
+            raise RuntimeError("hipIpcOpenMemHandle: invalid argument")
+        self.opened = list(handles)
+
+
+def _init_worker(rank, world, port, q, fail_rank):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path.insert(0, str(ROOT))
+    import _pkgload
+
+    _pkgload.load()
+    import nngp_amd.shard as S
+
+    S.shard_unique_id = lambda: bytes(range(128))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ctx = _FakeTileShard(rank, fail_open=(rank == fail_rank))
+    try:
+        S.init_shard_comm(ctx, dist)
+        q.put((rank, "ok", ctx.uid, ctx.opened))
+    except RuntimeError as e:
+        q.put((rank, "raised", str(e), None))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("fail_rank", [-1, 1])
+def test_tile_shard_init_two_ranks(fail_rank):
+    """Tile-shard bootstrap over gloo: the RCCL id from rank 0, then the IPC
+    handles of the granule buffers in rank order on every rank; a failure on
+    one rank (here rank 1's ipc_open) raises on EVERY rank, so no rank goes on
+    to a sweep whose peers never come."""
+    world, port = 2, 30500 + os.getpid() % 1000 + (fail_rank + 1) * 7
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_init_worker, args=(r, world, port, q, fail_rank)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {r: (st, a, b) for r, st, a, b in (q.get(timeout=100) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    if fail_rank < 0:
+        for r in range(world):
+            st, uid, opened = out[r]
+            assert st == "ok" and uid == bytes(range(128))
+            assert opened == [bytes([1]) * 64, bytes([2]) * 64]
+    else:
+        for r in range(world):
+            st, msg, _ = out[r]
+            assert st == "raised" and "rank 1" in msg and "hipIpcOpenMemHandle" in msg
