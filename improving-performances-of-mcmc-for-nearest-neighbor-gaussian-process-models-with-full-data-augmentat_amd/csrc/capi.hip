@@ -117,6 +117,8 @@ struct nngp_ctx {
   int* erow_ptr_d = nullptr;
   int* erow_d = nullptr;
   double* dwx_d = nullptr;        // n x C granules of 16 B
+  bool rglobal = false;           // tiles keep r in global memory (rg_d) instead of LDS
+  double* rg_d = nullptr;         // sum of the tiles' local rows x C
   unsigned* ctl_d = nullptr;      // [0] call id, [1] timeout word
   unsigned* tmo_h = nullptr;      // pinned copy of the timeout word after each launch
   unsigned long long* tdbg_d = nullptr;  // NNGP_PROBE=9: per-tile phase times, =2: per-phase timeline
@@ -235,6 +237,7 @@ TileDev tile_dev(nngp_ctx* c) {
   D.w_slot = c->w_slot_d;
   D.dwx = c->dwx_d;
   D.r = c->r_d;
+  D.rg = c->rg_d;
   D.scal = c->scal_d;
   D.ctl = c->ctl_d;
   D.dbg = c->tdbg_d;
@@ -362,6 +365,7 @@ void nngp_ctx_destroy(nngp_ctx* c) {
     for (int h = 0; h < c->tG; ++h)
       if (h != c->trank && c->peer_gx[h]) hipIpcCloseMemHandle(c->peer_gx[h]);
   ptrs.push_back(c->rmask_d);
+  ptrs.push_back(c->rg_d);
   ptrs.push_back(c->tdev_d);
   for (int k = 0; k < kMaxChains; ++k) {
     ChainState& s = c->ch[k];
@@ -462,10 +466,23 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       bool ok = cus > 0 && T <= n &&
                 build_tile_layout(nn.data(), n, b, coloring, locs, d, T, NT, tile_rmax(n_chains, NT), c->tl, terr, G);
       const int need = ok ? tile_lds_bytes(c->tl.max_rows, n_chains, NT, c->tl.K, c->tl.max_batches, c->tl.max_gslots) : 0;
-      if (ok && need > lds_max) {
-        ok = false;
-        terr = "tile layout needs " + std::to_string(need) +
-               " B of LDS per tile (device: " + std::to_string(lds_max) + ")";
+      // NNGP_TILE_R=global: the tiles' r in global memory (kernels.hip RG),
+      // one GPU, for layouts beyond the LDS.  Opt-in: at n = 1e7, m = 20 (one
+      // chain) it measured 362 chain-sweeps/s (26.4 ms per 10-sweep launch,
+      // 1024 threads: 341) against the colour engine's 449 -- five serial
+      // batches per phase, each behind dependent global round trips -- so the
+      // colour engine stays the default there
+      const char* trg = std::getenv("NNGP_TILE_R");
+      const bool force_rg = trg && std::string(trg) == "global";
+      if (ok && (need > lds_max || force_rg)) {
+        const int need_rg = tile_lds_bytes(0, n_chains, NT, c->tl.K, c->tl.max_batches, c->tl.max_gslots);
+        if (force_rg && shard_G == 0 && (NT == 512 || NT == 1024) && need_rg <= lds_max) {
+          c->rglobal = true;
+        } else {
+          ok = false;
+          terr = "tile layout needs " + std::to_string(need) +
+                 " B of LDS per tile (device: " + std::to_string(lds_max) + ")";
+        }
       }
       if (ok) {
         c->engine = 1;
@@ -597,6 +614,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     CK(dalloc(&c->erow_ptr_d, TL.erow_ptr.size()));
     CK(dalloc(&c->erow_d, TL.erow.size()));
     CK(dalloc(&c->dwx_d, (size_t)n * C * 2));
+    if (c->rglobal) CK(dalloc(&c->rg_d, TL.erow.size() * C));
     CK(dalloc(&c->ctl_d, 4));
     CK(hipHostMalloc((void**)&c->tmo_h, sizeof(unsigned), hipHostMallocDefault));
     *c->tmo_h = 0;
@@ -814,6 +832,7 @@ int nngp_ctx_info(const nngp_ctx* c, nngp_info* info) {
   }
   info->tile_ghost_pass = c->engine == 1 ? c->tl.NT * tile_gmax(c->tl.NT) : 0;
   info->tile_ghost_cells_max = 0;
+  info->tile_r_global = c->rglobal ? 1 : 0;
   if (c->engine == 1)
     for (size_t i = 0; i + 1 < c->tl.gptr.size(); ++i)
       info->tile_ghost_cells_max = std::max(info->tile_ghost_cells_max, c->tl.gptr[i + 1] - c->tl.gptr[i]);

@@ -158,6 +158,7 @@ struct TileDev {
   double* w_slot;             // per slot x C
   double* dwx;                // per slot x C: 16-byte granules {dw, epoch, call id}
   const double* r;            // device rows x C (r = B w at call start)
+  double* rg;                 // tiles with r in global memory: local rows x C (null: r in LDS)
   const SweepScalars* scal;   // C
   unsigned* ctl;              // [0] call id (bumped on the device before every launch), [1] timeout word
   unsigned long long* dbg;    // NNGP_PROBE=9 / 2: per-tile phase times / per-phase timeline, else null

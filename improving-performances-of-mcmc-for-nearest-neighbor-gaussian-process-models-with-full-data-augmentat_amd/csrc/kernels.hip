@@ -1613,7 +1613,12 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
   TLSTAMP(S, 3);
 }
 
-template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE, int SH>
+// RG: the tile's r in global memory (D.rg, the tile's local rows at
+// erow_ptr[tile] x C) instead of LDS -- layouts whose tiles do not fit a CU's
+// LDS (n = 1e7 on one GPU).  A row takes at most one update per colour (one
+// member per colour), so the scatter and the ghost adds stay plain
+// read-modify-writes; the phase barriers order them for the workgroup.
+template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE, int SH, int RG>
 __global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D0, TileLaunch a, TileShard sh) {
   using BR = TileBatchRegs<C, NT, RMAX>;
   constexpr int NW = NT / 64;
@@ -1632,8 +1637,8 @@ __global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D0, TileLaunch 
   const int T = S.T, t = S.t, K = D.K;
   const int row0 = D.erow_ptr[T], nrows = D.erow_ptr[T + 1] - row0;
   const int b_lo = D.batch_ptr[T * K], nbt = D.batch_ptr[T * K + K] - b_lo;
-  S.r_s = smem;
-  S.acc_s = smem + ((nrows * C + 1) / 2) * 2;   // kTSlots x C: slot totals, then dw
+  S.r_s = RG ? D.rg + (size_t)row0 * C : smem;
+  S.acc_s = RG ? smem : smem + ((nrows * C + 1) / 2) * 2;  // kTSlots x C: slot totals, then dw
   S.wsum = S.acc_s + kTSlots * C;                // NW x C: segmented wave totals
   S.sc_s = S.wsum + NW * C;                      // C x {inv_s2, inv_t2}
   S.seed_s = reinterpret_cast<unsigned long long*>(S.sc_s + 2 * C);
@@ -1694,13 +1699,13 @@ __global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D0, TileLaunch 
 
 // sh == nullptr: one GPU, the call-id bump and the whole grid of tiles here;
 // else the caller bumped the call ids and `grid` tiles from sh->tile0 run
-template <int C, int NT, int PROBE, int SH>
+template <int C, int NT, int PROBE, int SH, int RG = 0>
 static hipError_t launch_tiles_c(hipStream_t st, const TileDev& D, const TileLaunch& a, int lds, const TileShard* sh,
                                  int grid) {
   constexpr int RMAX = tile_rmax(C, NT);
   constexpr int DB = tile_double_buffer(C, NT);
   constexpr int GMAX = tile_gmax(NT);
-  auto k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE, SH>;
+  auto k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE, SH, RG>;
   lds = lds < kTSpreadLds ? kTSpreadLds : lds;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return e;
@@ -1716,6 +1721,19 @@ static hipError_t launch_tiles_c(hipStream_t st, const TileDev& D, const TileLau
 template <int NT>
 static hipError_t launch_tiles_nt(hipStream_t st, const TileDev& D, const TileLaunch& a, int lds, const TileShard* sh,
                                   int grid) {
+  if (D.rg) {  // r in global memory: 512- or 1024-thread tiles, one GPU
+    if constexpr (NT == 512 || NT == 1024) {
+      if (sh) return hipErrorInvalidValue;
+      switch (D.C) {
+        case 1: return launch_tiles_c<1, NT, 0, 0, 1>(st, D, a, lds, nullptr, 0);
+        case 2: return launch_tiles_c<2, NT, 0, 0, 1>(st, D, a, lds, nullptr, 0);
+        case 3: return launch_tiles_c<3, NT, 0, 0, 1>(st, D, a, lds, nullptr, 0);
+        case 4: return launch_tiles_c<4, NT, 0, 0, 1>(st, D, a, lds, nullptr, 0);
+        default: return hipErrorInvalidValue;
+      }
+    }
+    return hipErrorInvalidValue;
+  }
   if (sh) {
     switch (D.C) {
       case 1: return launch_tiles_c<1, NT, 0, 1>(st, D, a, lds, sh, grid);
@@ -1750,7 +1768,7 @@ static hipError_t launch_tiles_nt(hipStream_t st, const TileDev& D, const TileLa
 
 hipError_t launch_sweep_tiles(hipStream_t st, const TileDev& D, const TileLaunch& a, int max_rows, int NT,
                               int max_batches, int max_gslots, const TileShard* sh, int grid) {
-  const int lds = tile_lds_bytes(max_rows, D.C, NT, D.K, max_batches, max_gslots);
+  const int lds = tile_lds_bytes(D.rg ? 0 : max_rows, D.C, NT, D.K, max_batches, max_gslots);
   switch (NT) {
     case 256: return launch_tiles_nt<256>(st, D, a, lds, sh, grid);
     case 512: return launch_tiles_nt<512>(st, D, a, lds, sh, grid);

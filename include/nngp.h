@@ -96,7 +96,7 @@ typedef struct {
   int n_chunks;    /* sweep chunks (wavefront tasks per chain and sweep) */
   int sweep_engine;  /* 0: one launch per colour, 1: tile-resident persistent sweep */
   int n_tiles;       /* tiles (persistent workgroups) of the tile engine */
-  int tile_rows_max; /* max local rows (own + foreign) of a tile: its LDS-resident r */
+  int tile_rows_max; /* max local rows (own + foreign) of a tile: its resident r */
   long long n_ghost_cells; /* foreign-member cells the tiles (or shard ranks) apply after a hand-off */
   int n_ranks;       /* shard contexts: ranks of the sharded sweep (0: not sharded);
                         sweep_engine 0: colour shard, 1: tile shard */
@@ -107,6 +107,7 @@ typedef struct {
                                      tile shard: locations whose draws other ranks read */
   int tile_ghost_pass;       /* tile engine: ghost cells a (tile, colour) applies per register pass */
   int tile_ghost_cells_max;  /* tile engine: most ghost cells of one (tile, colour) */
+  int tile_r_global;         /* tile engine: 1 = the tiles' r in global memory (layout beyond the LDS) */
 } nngp_info;
 
 /* ---------- library ---------- */
