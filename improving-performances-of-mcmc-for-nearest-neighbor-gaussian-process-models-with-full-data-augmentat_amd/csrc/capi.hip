@@ -40,9 +40,16 @@ struct ChainState {
   bool have_factor[2] = {false, false};
   bool have_field = false, have_mu = false, mu_is_const = true;
   double mu_beta0 = 0.0;
+  // generations of the field and of the two factor slots (bumped on every
+  // write) and the last row-statistics passes (nngp_loglik) they produced:
+  // nngp_beta0_stats reuses a pass over the current factor and field
+  uint64_t fgen = 1, lgen[2] = {1, 1};
+  struct RowStats { uint64_t lg = 0, fg = 0; double shift = 0.0, r[4] = {0, 0, 0, 0}; } rs[2];
+  int rs_next = 0;
 };
 
 struct nngp_ctx {
+  uint64_t gen = 1;  // generation counter of ChainState::fgen / lgen
   int device = 0;
   hipStream_t st = nullptr;
   int n = 0, d = 0, b = 0, n_obs = 0, ds = 2;
@@ -890,6 +897,7 @@ int nngp_factor(nngp_ctx* c, int which, int covfun, const double* cp, int ncp) {
   HIPCHK(c, launch_scale_coords(c->st, covfun, cp, ncp, c->locs_d, c->n, c->d, c->sc_d, use_ds));
   const int big = INT_MAX;
   HIPCHK(c, hipMemcpyAsync(c->fail_d, &big, sizeof(int), hipMemcpyHostToDevice, c->st));
+  S.lgen[which] = ++c->gen;
   HIPCHK(c, launch_factor(c->st, fam, var, nug, nu, c->sc_d, use_ds, c->nn_d, c->n, c->b, S.linv_d[which], c->fail_d));
   int fail = 0;
   HIPCHK(c, hipMemcpyAsync(&fail, c->fail_d, sizeof(int), hipMemcpyDeviceToHost, c->st));
@@ -927,6 +935,7 @@ int nngp_set_linv(nngp_ctx* c, int which, const double* Linv) {
   std::vector<double> rm((size_t)c->n * c->b);
   for (int i = 0; i < c->n; ++i)
     for (int j = 0; j < c->b; ++j) rm[(size_t)c->dpos[i] * c->b + j] = Linv[i + (size_t)j * c->n];
+  S.lgen[which] = ++c->gen;
   HIPCHK(c, hipMemcpyAsync(S.linv_d[which], rm.data(), rm.size() * sizeof(double), hipMemcpyHostToDevice, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
   S.have_factor[which] = true;
@@ -942,6 +951,7 @@ int nngp_accept_factor(nngp_ctx* c) {
   if ((rc = set_device(c))) return rc;
   std::swap(S.linv_d[0], S.linv_d[1]);
   std::swap(S.have_factor[0], S.have_factor[1]);
+  std::swap(S.lgen[0], S.lgen[1]);
   // captured sweep graphs read the current factor through linv_cur_d: they stay valid
   return refresh_sweep_values(c, c->cur);
 }
@@ -982,6 +992,7 @@ int nngp_set_field(nngp_ctx* c, const double* field) {
   int rc;
   if ((rc = set_device(c))) return rc;
   ChainState& S = c->ch[c->cur];
+  S.fgen = ++c->gen;
   if ((rc = upload_field(c, field, S.field_d))) return rc;
   S.have_field = true;
   return NNGP_OK;
@@ -1082,6 +1093,12 @@ int nngp_loglik(nngp_ctx* c, int which, double beta0, double log_scale, double* 
   double r[4];
   if ((rc = fetch4(c, nb, r))) return rc;
   *ll = r[0] - c->n * 0.5 * log_scale - 0.5 * r[1] / std::exp(log_scale);
+  ChainState::RowStats& e = S.rs[S.rs_next];
+  S.rs_next ^= 1;
+  e.lg = S.lgen[which];
+  e.fg = S.fgen;
+  e.shift = beta0;
+  for (int k = 0; k < 4; ++k) e.r[k] = r[k];
   return NNGP_OK;
 }
 
@@ -1108,6 +1125,12 @@ static int sweep_prepare(nngp_ctx* c, int k, double beta0, double log_scale, dou
   sc.seed = seed;
   sc.counter_base = counter_base;
   return NNGP_OK;
+}
+
+// a sweep call rewrites the fields of the chains in mask (row-statistics cache)
+static void fields_written(nngp_ctx* c, int mask) {
+  for (int k = 0; k < c->C; ++k)
+    if ((mask >> k) & 1) c->ch[k].fgen = ++c->gen;
 }
 
 // the tile engine's bounded spins set a timeout word instead of hanging
@@ -1207,6 +1230,7 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
   int rc;
   if ((rc = set_device(c))) return rc;
   const int k = c->cur, mask = 1 << k;
+  fields_written(c, mask);
   if ((rc = sweep_prepare(c, k, beta0, log_scale, lnv, seed, counter_base))) return rc;
   if ((rc = upload_scalars(c))) return rc;
   if (sharded_call(c)) {
@@ -1246,6 +1270,7 @@ int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const doub
   if (n_sweeps == 0) return NNGP_OK;
   int rc;
   if ((rc = set_device(c))) return rc;
+  fields_written(c, (1 << c->C) - 1);
   for (int k = 0; k < c->C; ++k)
     if ((rc = sweep_prepare(c, k, beta0[k], log_scale[k], lnv[k], seed[k], counter_base[k]))) return rc;
   if ((rc = upload_scalars(c))) return rc;
@@ -1623,6 +1648,8 @@ static int tile_group_call(nngp_ctx** ctxs, int G, int n_sweeps, const double* b
 int nngp_sweep_chains_group(nngp_ctx** ctxs, int G, int n_sweeps, const double* beta0, const double* log_scale,
                             const double* lnv, const uint64_t* seed, const uint64_t* counter_base) {
   if (!ctxs || G < 1 || n_sweeps < 0 || !beta0 || !log_scale || !lnv || !seed || !counter_base) return NNGP_ERR_ARG;
+  for (int g = 0; g < G; ++g)
+    if (ctxs[g] && n_sweeps > 0) fields_written(ctxs[g], (1 << ctxs[g]->C) - 1);
   if (ctxs[0] && ctxs[0]->engine == 1) {
     if (G > kTileRanksMax) return fail_msg(ctxs[0], NNGP_ERR_ARG, "sweep_chains_group: too many ranks");
     // one rank: the plain tile sweep (no remote readers, no plan masks)
@@ -1716,6 +1743,7 @@ int nngp_sweep_timed(nngp_ctx* c, int n_sweeps, const double* beta0, const doubl
   if (sharded_call(c)) return fail_msg(c, NNGP_ERR_STATE, "sweep_timed: not available on shard contexts");
   int rc;
   if ((rc = set_device(c))) return rc;
+  fields_written(c, (1 << c->C) - 1);
   for (int k = 0; k < c->C; ++k)
     if ((rc = sweep_prepare(c, k, beta0[k], log_scale[k], lnv[k], seed[k], counter_base[k]))) return rc;
   if ((rc = upload_scalars(c))) return rc;
@@ -1836,6 +1864,7 @@ int nngp_accept_field(nngp_ctx* c) {
   int rc;
   if ((rc = set_device(c))) return rc;
   ChainState& S = c->ch[c->cur];
+  S.fgen = ++c->gen;
   HIPCHK(c, hipMemcpyAsync(S.field_d, S.field_prop_d, c->n * sizeof(double), hipMemcpyDeviceToDevice, c->st));
   return NNGP_OK;  // stream-ordered: no host sync
 }
@@ -1844,6 +1873,14 @@ int nngp_beta0_stats(nngp_ctx* c, double* oqo, double* oqf) {
   if (!c || !oqo || !oqf) return NNGP_ERR_ARG;
   ChainState& S = c->ch[c->cur];
   if (!S.have_factor[0] || !S.have_field) return fail_msg(c, NNGP_ERR_STATE, "beta0_stats: need factor and field");
+  // a log-likelihood pass over the current factor and field already has
+  // sum (B1)^2 and sum (B1)(B(f - shift)): (B1)'(Bf) = that + shift (B1)'(B1)
+  for (const ChainState::RowStats& e : S.rs)
+    if (e.lg == S.lgen[0] && e.fg == S.fgen) {
+      *oqo = e.r[2];
+      *oqf = e.r[3] + e.shift * e.r[2];
+      return NNGP_OK;
+    }
   int rc;
   if ((rc = set_device(c))) return rc;
   int nb = launch_row_stats(c->st, S.linv_d[0], c->nn_d, c->n, c->b, S.field_d, 0.0, nullptr, c->partials_d);

@@ -35,6 +35,9 @@ reproducible.
 """
 from __future__ import annotations
 
+import ctypes
+import threading
+
 import numpy as np
 
 from ._lib import NNGP_ERR_CHOL, NNGPError
@@ -59,6 +62,22 @@ def _interweave_prep(ctx, X, va):
     prec = SX.T @ SX
     cov = np.linalg.inv(prec)
     return {"Xl": Xl, "SX": SX, "covmat": cov, "covmat_chol": np.linalg.cholesky(cov).T}
+
+
+def _prefault(arr: np.ndarray) -> threading.Thread:
+    """Touch the pages of a fresh host array on a helper thread (memset
+    through ctypes, which releases the GIL) while the chain runs: the record
+    copy at the end of the call then lands in resident pages (measured for a
+    40 x 1e6 record block: 18.9 ms into fresh pages, 6.5 ms into touched ones)."""
+    def run():
+        step = 1 << 26
+        base, nb = arr.ctypes.data, arr.nbytes
+        for off in range(0, nb, step):
+            ctypes.memset(base + off, 0, min(step, nb - off))
+
+    th = threading.Thread(target=run, daemon=True)
+    th.start()
+    return th
 
 
 def _propose_factor(ctx, covfun, cp, on_chol_error):
@@ -99,7 +118,7 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
            "log_scale": np.zeros((n_iterations_update, 1)),
            "log_noise_variance": np.zeros((n_iterations_update, 1)),
            "shape": np.zeros((n_iterations_update, n_shape)),
-           "field": np.zeros((int(round(n_iterations_update * field_thinning)), va["n_locs"]))}
+           "field": np.empty((int(round(n_iterations_update * field_thinning)), va["n_locs"]))}
     if has_X:
         rec["beta"] = np.zeros((n_iterations_update, X["X"].shape[1]))
     acc_suf = np.zeros(n_iterations_update)
@@ -113,6 +132,9 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
             ctx.records_reserve(n_rec)
         except NNGPError:
             dev_rec = False
+    if not dev_rec:
+        rec["field"][:] = 0.0
+    touch = _prefault(rec["field"]) if dev_rec else None
 
     # Vecchia factor of the current state (:67-74)
     ctx.factor(0, covfun, covparms(sp_names, params["shape"]))
@@ -232,7 +254,8 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
                 rec["field"][int(it * field_thinning) - 1] = ctx.get_field()
 
     if dev_rec:
-        rec["field"] = ctx.get_records(0, n_rec)
+        touch.join()
+        ctx.get_records(0, n_rec, out=rec["field"])
         ctx.records_reserve(0)
     params["field"] = ctx.get_field()
     return {"state": {"params": params, "transition_kernels": tk}, "records": rec,

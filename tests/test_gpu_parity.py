@@ -633,3 +633,41 @@ def test_tile_engine_r_in_global_memory_equals_lds_bitwise(P, engine, monkeypatc
             out.append(res)
     for k in range(C):
         np.testing.assert_array_equal(out[1][k], out[0][k], err_msg=f"chain {k}")
+
+
+def test_beta0_stats_reuses_loglik_pass_and_invalidates(P, O, engine):
+    """nngp_beta0_stats answers from the last log-likelihood pass over the
+    current factor and field ((B1)'(Bf) = (B1)'(B(f - b0)) + b0 (B1)'(B1)),
+    within 1e-12 of a fresh pass; every write of the field or the factor
+    (set_field, sweep, accept_field, factor, accept_factor) invalidates it."""
+    if engine != "tiles-default":
+        pytest.skip("engine independent")
+    n, m = 5000, 10
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=3)
+    rng = np.random.default_rng(8)
+    cp0, cp1 = [1.0, 0.1, 0.0], [1.0, 0.15, 0.0]
+
+    with P.ChainContext(locs, NN, col, lm, y, device=0) as ctx:
+        ctx.factor(0, "exponential_isotropic", cp0)
+        ctx.set_field(rng.normal(size=n))
+        ctx.set_mu(None, 0.3)
+        fresh = ctx.beta0_stats()                     # no pass cached yet: a direct pass
+        ctx.loglik(0, 0.3, 0.1)
+        cached = ctx.beta0_stats()
+        np.testing.assert_allclose(cached, fresh, rtol=1e-12)
+        ctx.factor(1, "exponential_isotropic", cp1)
+        ctx.loglik(1, 0.3, 0.0)
+        ctx.accept_factor()                           # the proposal's pass becomes the current one
+        after_accept = ctx.beta0_stats()
+        ctx.set_field(ctx.get_field())                # same values, new generation: a fresh pass
+        np.testing.assert_allclose(after_accept, ctx.beta0_stats(), rtol=1e-12)
+        ctx.loglik(0, 0.3, 0.0)
+        ctx.sweep(1, 0.3, 0.0, -0.5, 5, 0)            # the field changes
+        swept = ctx.beta0_stats()
+        ctx.set_field(ctx.get_field())
+        np.testing.assert_allclose(swept, ctx.beta0_stats(), rtol=1e-12)
+        assert abs(swept[1] - after_accept[1]) > 1e-9 * abs(after_accept[1])
+        # the oracle's 1'B'B1 and 1'B'Bf on the final state
+        L, f = ctx.get_linv(0), ctx.get_field()
+        B1, Bf = O.linv_mult(L, np.ones(n), NN), O.linv_mult(L, f, NN)
+        np.testing.assert_allclose(swept, [B1 @ B1, B1 @ Bf], rtol=1e-10)
