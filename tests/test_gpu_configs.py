@@ -7,7 +7,12 @@ path's).  Bars: the 8-rank field == the 1-rank field bitwise after one call;
 the 1-rank field vs the oracle's local-form sweep with the same Philox normals
 on the device factor (1e-9, one sweep); the log-likelihood vs the oracle's on
 that factor (1e-10); sampled factor rows vs the dense conditional (the
-kriging form of vecchia_Linv) within DESIGN §4's conditioning bound."""
+kriging form of vecchia_Linv) within DESIGN §4's conditioning bound.
+
+Engine: the colour shard (NNGP_ENGINE=colors).  The tile shard of this size
+has 2048 tiles (256 per GPU), which only an 8-GPU node holds resident; its
+cross-rank logic is checked at the headline size (test_gpu_tile_shard.py)
+and by bench.py's cross-GPU parity check on the node."""
 import time
 from pathlib import Path
 
@@ -44,7 +49,8 @@ def _dense_row(O, covfun, cp, locs, nn_row):
     return np.concatenate([[1.0], -wts]) / np.sqrt(cv), np.linalg.cond(Cm)
 
 
-def test_configs4_1e7_m20_matern15_eight_rank_shard(P, O, capfd):
+def test_configs4_1e7_m20_matern15_eight_rank_shard(P, O, capfd, monkeypatch):
+    monkeypatch.setenv("NNGP_ENGINE", "colors")
     t0 = time.time()
     n, m, G = 10_000_000, 20, 8
     rng = np.random.default_rng(2024)
