@@ -119,6 +119,7 @@ struct nngp_ctx {
   int* gptr_d = nullptr;
   int* gslot_d = nullptr;
   int* gslot_ptr_d = nullptr;
+  int* bsplit_d = nullptr;        // split tile layouts: first boundary batch of (tile, colour)
   int* nb_ptr_d = nullptr;
   int* nb_d = nullptr;
   int* erow_ptr_d = nullptr;
@@ -232,6 +233,7 @@ TileDev tile_dev(nngp_ctx* c) {
   D.gptr = c->gptr_d;
   D.gslot = c->gslot_d;
   D.gslot_ptr = c->gslot_ptr_d;
+  D.batch_split = c->tl.split ? c->bsplit_d : nullptr;
   D.max_gslots = c->tl.max_gslots;
   D.nb_ptr = c->nb_ptr_d;
   D.nb = c->nb_d;
@@ -373,6 +375,7 @@ void nngp_ctx_destroy(nngp_ctx* c) {
       if (h != c->trank && c->peer_gx[h]) hipIpcCloseMemHandle(c->peer_gx[h]);
   ptrs.push_back(c->rmask_d);
   ptrs.push_back(c->rg_d);
+  ptrs.push_back(c->bsplit_d);
   ptrs.push_back(c->tdev_d);
   for (int k = 0; k < kMaxChains; ++k) {
     ChainState& s = c->ch[k];
@@ -470,8 +473,15 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
         delete c;
         return fail_msg(nullptr, NNGP_ERR_ARG, "NNGP_TILE_NT must be 256, 512 or 1024");
       }
+      // NNGP_TILE_SPLIT=1 (3-4 chains): interior-first layouts (kernels.hip
+      // tile_phase_ib).  Opt-in: measured 3,607 vs 2,564 us per 10-sweep
+      // launch at the headline (two batches per colour, and the next colour's
+      // stream no longer overlaps the hand-off with one register set)
+      const char* tsp = std::getenv("NNGP_TILE_SPLIT");
+      const bool split = tile_double_buffer(n_chains, NT) == 0 && tsp && std::string(tsp) == "1";
       bool ok = cus > 0 && T <= n &&
-                build_tile_layout(nn.data(), n, b, coloring, locs, d, T, NT, tile_rmax(n_chains, NT), c->tl, terr, G);
+                build_tile_layout(nn.data(), n, b, coloring, locs, d, T, NT, tile_rmax(n_chains, NT), c->tl, terr, G,
+                                  split);
       const int need = ok ? tile_lds_bytes(c->tl.max_rows, n_chains, NT, c->tl.K, c->tl.max_batches, c->tl.max_gslots) : 0;
       // NNGP_TILE_R=global: the tiles' r in global memory (kernels.hip RG),
       // one GPU, for layouts beyond the LDS.  Opt-in: at n = 1e7, m = 20 (one
@@ -616,6 +626,10 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     CK(dalloc(&c->gslot_ptr_d, TL.gslot_ptr.size()));
     CK(upload(c->gslot_d, TL.gslot.data(), TL.gslot.size(), c->st));
     CK(upload(c->gslot_ptr_d, TL.gslot_ptr.data(), TL.gslot_ptr.size(), c->st));
+    if (TL.split) {
+      CK(dalloc(&c->bsplit_d, TL.batch_split.size()));
+      CK(upload(c->bsplit_d, TL.batch_split.data(), TL.batch_split.size(), c->st));
+    }
     CK(dalloc(&c->nb_ptr_d, TL.nb_ptr.size()));
     CK(dalloc(&c->nb_d, TL.nb.size()));
     CK(dalloc(&c->erow_ptr_d, TL.erow_ptr.size()));

@@ -509,7 +509,7 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
 
 // ---------------------------------------------------------------- tile layout
 bool build_tile_layout(const int* nn, int n, int b, const int* colors, const double* locs, int d, int T,
-                       int NT, int RMAX, TileLayout& L, std::string& err, int G) {
+                       int NT, int RMAX, TileLayout& L, std::string& err, int G, bool split) {
   L = TileLayout();
   L.n = n; L.b = b; L.NT = NT; L.RMAX = RMAX;
   if (NT < 64 || NT > 1024 || RMAX < 1 || (long long)NT * RMAX > (1 << 20)) { err = "tile layout: bad NT/RMAX"; return false; }
@@ -574,19 +574,42 @@ bool build_tile_layout(const int* nn, int n, int b, const int* colors, const dou
   std::vector<int> tile_of(n);  // loc -> tile
   for (int t = 0; t < T; ++t)
     for (int r = L.tile_row0[t]; r < L.tile_row0[t + 1]; ++r) tile_of[perm[r]] = t;
-  // slot order: tile, colour, Morton
+  // split layouts: a slot is "boundary" when a row of its column has a
+  // member of the previous colour (cyclic) owned by another tile
+  L.split = split;
+  std::vector<char> bnd(split ? n : 0, 0);
+  if (split) {
+    parallel_chunks(n, [&](int, long long i0, long long i1) {
+      for (long long i = i0; i < i1; ++i) {
+        const int cp = (colors[i] - 1 + K - 1) % K + 1, t = tile_of[i];
+        for (long long p = cptr[i]; p < cptr[i + 1] && !bnd[i]; ++p) {
+          const int k = crow[p];
+          for (int u = 0; u < b; ++u) {
+            const int j = nn[(size_t)k * b + u];
+            if (j >= 0 && colors[j] == cp && tile_of[j] != t) { bnd[i] = 1; break; }
+          }
+        }
+      }
+    });
+  }
+  // slot order: tile, colour, (split: interior before boundary), Morton
   L.compact_loc.resize(n);
   std::vector<int> slot_of(n);
   std::vector<int> tc_ptr((size_t)T * K + 1, 0);  // slots of (tile, colour)
   for (int i = 0; i < n; ++i) tc_ptr[(size_t)tile_of[i] * K + colors[i]]++;
   for (size_t p = 0; p < (size_t)T * K; ++p) tc_ptr[p + 1] += tc_ptr[p];
+  std::vector<int> tc_split;  // split: first boundary slot of (tile, colour)
   {
     std::vector<int> f(tc_ptr.begin(), tc_ptr.end() - 1);
-    for (int r = 0; r < n; ++r) {
-      const int i = perm[r];
-      const int x = f[(size_t)tile_of[i] * K + colors[i] - 1]++;
-      L.compact_loc[x] = i;
-      slot_of[i] = x;
+    for (int pass = 0; pass < (split ? 2 : 1); ++pass) {
+      for (int r = 0; r < n; ++r) {
+        const int i = perm[r];
+        if (split && bnd[i] != pass) continue;
+        const int x = f[(size_t)tile_of[i] * K + colors[i] - 1]++;
+        L.compact_loc[x] = i;
+        slot_of[i] = x;
+      }
+      if (split && pass == 0) tc_split = f;
     }
   }
   L.rank_slot0.assign(G + 1, 0);
@@ -622,11 +645,15 @@ bool build_tile_layout(const int* nn, int n, int b, const int* colors, const dou
     for (size_t q = 0; q < rows.size(); ++q) lr_of[rows[q]] = (int)q;
     L.erow.insert(L.erow.end(), rows.begin(), rows.end());
     L.erow_ptr[t + 1] = (int)L.erow.size();
-    // own batches, colour by colour
+    // own batches, colour by colour (split: the interior run, then the boundary run)
     for (int c = 0; c < K; ++c) {
       const size_t pc = (size_t)t * K + c;
       int x = tc_ptr[pc];
-      const int xe = tc_ptr[pc + 1];
+      const int xe_all = tc_ptr[pc + 1];
+      if (split) L.batch_split.push_back((int)L.batch.size());
+      for (int run = 0; run < (split ? 2 : 1); ++run) {
+      const int xe = split && run == 0 ? tc_split[pc] : xe_all;
+      if (split && run == 1) L.batch_split[pc] = (int)L.batch.size();
       while (x < xe) {
         int cells = 0, ns = 0;
         while (x + ns < xe && ns < std::min(NT, kTileSlotsMax)) {
@@ -657,6 +684,7 @@ bool build_tile_layout(const int* nn, int n, int b, const int* colors, const dou
         }
         L.batch.push_back(tb);
         x += ns;
+      }
       }
       L.batch_ptr[pc + 1] = (int)L.batch.size();
     }

@@ -119,6 +119,12 @@ struct TileLayout {
   std::vector<int> erow_ptr, erow;   // local rows of each tile -> device row
   std::vector<TileBatch> batch;      // own batches, grouped by (tile, colour)
   std::vector<int> batch_ptr;        // T*K + 1
+  // split layouts (interior first): the slots of (tile, colour c) whose rows
+  // have no foreign member of colour c-1 (cyclic) come first, in batches of
+  // their own; batch_split[t*K + c] = the first batch of the others
+  // ("boundary" slots: they wait for the hand-off of colour c-1)
+  bool split = false;
+  std::vector<int> batch_split;      // T*K (split layouts)
   std::vector<uint32_t> cell_pk;     // own cells (padded batches)
   std::vector<int> cell_src;         // device Linv index rpos[k]*b + j, or -1 (padding)
   std::vector<int> gcell;            // 2 per ghost cell: local row, index of its foreign slot
@@ -141,7 +147,8 @@ struct TileLayout {
 // also the ranks' slot ranges and the remote-reader mask of every slot.
 constexpr int kMaxTileRanks = 16;
 bool build_tile_layout(const int* nn_rowmajor, int n, int b, const int* colors, const double* locs_colmajor,
-                       int d, int T, int NT, int RMAX, TileLayout& L, std::string& err, int G = 1);
+                       int d, int T, int NT, int RMAX, TileLayout& L, std::string& err, int G = 1,
+                       bool split = false);
 
 // Colour-sharded sweep over G ranks on top of a
 // SweepLayout (every rank builds the same layout from the same inputs):

@@ -147,6 +147,7 @@ struct TileDev {
   const int* gptr;            // T*K+1
   const int* gslot;           // foreign slots of each (tile, colour): slot index
   const int* gslot_ptr;       // T*K+1
+  const int* batch_split;     // T*K: split layouts, first boundary batch of (tile, colour); else null
   const int* nb_ptr;          // T*K+1
   const int* nb;
   const int* erow_ptr;        // T+1

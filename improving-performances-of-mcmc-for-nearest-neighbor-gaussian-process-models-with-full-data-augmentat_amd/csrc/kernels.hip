@@ -1159,7 +1159,7 @@ constexpr int kTSpreadLds = 82 * 1024;  // LDS floor: at most one tile per CU
 int tile_lds_bytes(int max_rows, int C, int NT, int K, int max_batches, int max_gslots) {
   const int rbytes = ((max_rows * C * 8 + 15) / 16) * 16;
   return rbytes + kTSlots * C * 8 + (NT / 64) * C * 8 + 4 * C * 8 + ((max_gslots * C + 1) / 2) * 16 +
-         max_batches * 16 + 3 * (K + 1) * 4 + (NT / 64) * 4 + 64;
+         max_batches * 16 + 4 * (K + 1) * 4 + (NT / 64) * 4 + 64;
 }
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
@@ -1303,6 +1303,7 @@ struct TileState {
   int* bptr_s;    // K+1: batches of colour c = batch_s[bptr_s[c] .. bptr_s[c+1])
   int* gptr_s;    // K+1: ghost cells of colour c (global indices)
   int* gsp_s;     // K+1: foreign slots of colour c (global indices into gslot)
+  int* bsp_s;     // K: split layouts, first boundary batch of colour c (as bptr_s)
   double* gdw_s;  // foreign slots x C: their dw of the current colour
   int* wflag;
   unsigned* spin_s;
@@ -1613,12 +1614,142 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
   TLSTAMP(S, 3);
 }
 
+// One colour phase of a SPLIT layout (one register set, C >= 3): the
+// interior batches of colour c -- slots whose rows have no member of colour
+// c-1 owned by another tile -- go first, while the granules of colour c-1
+// are still in flight; then that hand-off (poll, ghost cells of c-1); then
+// the boundary batches of c.  The chain from a neighbour's draw to this
+// tile's next draw runs through the few boundary slots only; the interior
+// work covers the hand-off latency.  Per row the updates of c and c-1 may
+// land in the other order than in the colour-by-colour schedule (rounding
+// only: an interior slot never reads a row waiting for its c-1 update).
+template <int C, int NT, int RMAX, int GMAX, int PROBE, int SH>
+__device__ __forceinline__ void tile_phase_ib(const TileDev& D, const TileLaunch& a, const TileShard& sh, TileState& S,
+                                              int ph, TileBatchRegs<C, NT, RMAX>& cur, TileGhostRegs<C, GMAX>& gr) {
+  const int K = S.K, t = S.t;
+  const int s = ph / K, c = ph - s * K;
+  const unsigned epoch = (unsigned)ph + 1;
+  S.ph = ph;
+  TLSTAMP(S, 0);
+  const int phn = ph + 1;
+  const int cn = phn % K, sn = phn / K;
+  const bool has_next = phn < S.nph;
+  const bool more = has_next && S.bptr_s[cn] < S.bptr_s[cn + 1];
+  const int bfirst = S.bptr_s[c], bsplit = S.bsp_s[c], bend = S.bptr_s[c + 1];
+  const bool had_int = bsplit > bfirst, had_bnd = bend > bsplit;
+  // the hand-off of the previous colour (none at the first phase of a call)
+  const bool hp = ph > 0;
+  const int cp = hp ? (ph - 1) % K : 0;
+  const int g0 = S.gptr_s[cp], g1 = hp ? S.gptr_s[cp + 1] : g0;
+  const int gs0 = S.gsp_s[cp], nfi = hp ? (S.gsp_s[cp + 1] - gs0) * C : 0;
+  const int gsl_pref = t < nfi ? D.gslot[gs0 + t / C] : 0;
+  const bool pol = t < nfi;
+  u32x4_t gfirst;
+  // ---- 1. interior batches; after the last draw (records dead) the next
+  // batch's records, the hand-off's ghost cells and first poll go out
+  for (int bi = bfirst; bi < bsplit; ++bi) {
+    if (bi != bfirst) {
+      __syncthreads();
+      tile_load_batch<C, NT, RMAX, SH>(D, S.batch_s[bi], cur, t);
+      tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, s, cur, t);
+    }
+    tile_own_draw<C, NT, RMAX, PROBE, SH>(D, a, sh, S, cur, epoch);
+    const int R = cur.R;
+    if (bi + 1 == bsplit) {
+      if (had_bnd) tile_load_items<C, NT, RMAX, SH>(D, S.batch_s[bsplit], cur, t);
+      else if (more) tile_load_items<C, NT, RMAX, SH>(D, S.batch_s[S.bptr_s[cn]], cur, t);
+      if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
+      if (pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * C + t % C) * 16), 0,
+                                                              SH ? kGranAuxSys : kGranAux);
+    }
+    tile_own_scatter<C, NT, RMAX, PROBE>(S, cur, R);
+  }
+  if (!had_int) {
+    if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
+    if (pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * C + t % C) * 16), 0,
+                                                            SH ? kGranAuxSys : kGranAux);
+  } else {
+    if (had_bnd) tile_load_cells<C, NT, RMAX>(D, S.batch_s[bsplit], cur, t);
+    else if (more) tile_load_cells<C, NT, RMAX>(D, S.batch_s[S.bptr_s[cn]], cur, t);
+  }
+  TLSTAMP(S, 6);
+  // ---- 2. hand-off of colour c-1: the granule of each (foreign slot, chain)
+  // until it carries epoch ph -> gdw_s; then its ghost cells
+  if (hp) {
+    const unsigned ep = (unsigned)ph;
+    for (int u0 = 0; u0 < nfi; u0 += NT) {
+      const int u = u0 + t;
+      if (u < nfi) {
+        const int x = u0 == 0 ? gsl_pref : D.gslot[gs0 + u / C];
+        const int ch = u % C;
+        const int off = (int)(((size_t)x * C + ch) * 16);
+        u32x4_t g = u0 == 0 ? gfirst
+                            : __builtin_amdgcn_raw_buffer_load_b128(S.gran, off, 0, SH ? kGranAuxSys : kGranAux);
+        double dw = 0.0;
+        for (unsigned spins = 0;; ++spins) {
+          if (g.z == ep && (g.w ^ g.x ^ g.y) == S.call) {
+            dw = __builtin_bit_cast(double, (unsigned long long)g.x | ((unsigned long long)g.y << 32));
+            if (PROBE == 2) atomicMax(S.spin_s, spins);
+            break;
+          }
+          if (S.timed_out || spins > (1u << 20) ||
+              ((spins & 1023u) == 1023u && __hip_atomic_load(S.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+            if (!S.timed_out) __hip_atomic_store(S.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            S.timed_out = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          g = __builtin_amdgcn_raw_buffer_load_b128(S.gran, off, 0, SH ? kGranAuxSys : kGranAux);
+        }
+        S.gdw_s[u] = dw;
+      }
+    }
+    __syncthreads();
+    if (PROBE == 2 && t == 0 && S.ph < kTimelinePhases) {
+      D.dbg[((size_t)S.T * kTimelinePhases + S.ph) * 8 + 5] = *S.spin_s;
+      *S.spin_s = 0;
+    }
+    for (int gb = g0; gb < g1; gb += NT * GMAX) {
+      if (gb != g0) tile_load_ghosts<C, NT, GMAX>(D, gb, g1, gr, t);
+#pragma unroll
+      for (int k = 0; k < GMAX; ++k)
+        if (gr.lr[k] >= 0)
+#pragma unroll
+          for (int ch = 0; ch < C; ++ch) S.r_s[gr.lr[k] * C + ch] += gr.gv[k][ch] * S.gdw_s[gr.gx[k] * C + ch];
+    }
+    __syncthreads();
+  } else if (had_int && had_bnd) {
+    __syncthreads();  // acc_s: every wave is done with the interior batch
+  }
+  TLSTAMP(S, 2);
+  // ---- 3. boundary batches; after the last draw the next phase's records
+  for (int bi = bsplit; bi < bend; ++bi) {
+    if (bi != bsplit) {
+      __syncthreads();
+      tile_load_batch<C, NT, RMAX, SH>(D, S.batch_s[bi], cur, t);
+    }
+    if (bi != bsplit || had_int) tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, s, cur, t);
+    tile_own_draw<C, NT, RMAX, PROBE, SH>(D, a, sh, S, cur, epoch);
+    const int R = cur.R;
+    if (bi + 1 == bend && more) tile_load_items<C, NT, RMAX, SH>(D, S.batch_s[S.bptr_s[cn]], cur, t);
+    tile_own_scatter<C, NT, RMAX, PROBE>(S, cur, R);
+  }
+  // ---- 4. the next phase's first batch: its cells, then its draw scalars
+  if (more) {
+    if (had_bnd) tile_load_cells<C, NT, RMAX>(D, S.batch_s[S.bptr_s[cn]], cur, t);
+    else if (!had_int) tile_load_batch<C, NT, RMAX, SH>(D, S.batch_s[S.bptr_s[cn]], cur, t);
+    tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, sn, cur, t);
+  }
+  __syncthreads();
+  TLSTAMP(S, 3);
+}
+
 // RG: the tile's r in global memory (D.rg, the tile's local rows at
 // erow_ptr[tile] x C) instead of LDS -- layouts whose tiles do not fit a CU's
 // LDS (n = 1e7 on one GPU).  A row takes at most one update per colour (one
 // member per colour), so the scatter and the ghost adds stay plain
 // read-modify-writes; the phase barriers order them for the workgroup.
-template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE, int SH, int RG>
+template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE, int SH, int RG, int IB>
 __global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D0, TileLaunch a, TileShard sh) {
   using BR = TileBatchRegs<C, NT, RMAX>;
   constexpr int NW = NT / 64;
@@ -1647,7 +1778,8 @@ __global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D0, TileLaunch 
   S.bptr_s = reinterpret_cast<int*>(S.batch_s + nbt);
   S.gptr_s = S.bptr_s + K + 1;
   S.gsp_s = S.gptr_s + K + 1;
-  S.wflag = S.gsp_s + K + 1;                     // NW: the wave holds a slot start
+  S.bsp_s = S.gsp_s + K + 1;                     // K+1 (split layouts)
+  S.wflag = S.bsp_s + K + 1;                     // NW: the wave holds a slot start
   S.spin_s = reinterpret_cast<unsigned*>(S.wflag + NW);  // NNGP_PROBE=2: max poll spins of the phase
   if (PROBE == 2 && t == 0) *S.spin_s = 0;
   TSTAMP(S, -1);
@@ -1662,6 +1794,7 @@ __global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D0, TileLaunch 
     S.bptr_s[i] = D.batch_ptr[T * K + i] - b_lo;
     S.gptr_s[i] = D.gptr[T * K + i];
     S.gsp_s[i] = D.gslot_ptr[T * K + i];
+    if (IB) S.bsp_s[i] = i < K ? D.batch_split[T * K + i] - b_lo : 0;
   }
   if (t < C) {
     S.sc_s[2 * t] = D.scal[t].inv_s2;
@@ -1687,6 +1820,8 @@ __global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D0, TileLaunch 
       tile_phase<C, NT, RMAX, GMAX, DB, PROBE, SH>(D, a, sh, S, ph, A, B, GA, GB);
       if (ph + 1 < S.nph) tile_phase<C, NT, RMAX, GMAX, DB, PROBE, SH>(D, a, sh, S, ph + 1, B, A, GB, GA);
     }
+  } else if (IB) {
+    for (int ph = 0; ph < S.nph; ++ph) tile_phase_ib<C, NT, RMAX, GMAX, PROBE, SH>(D, a, sh, S, ph, A, GA);
   } else {
     for (int ph = 0; ph < S.nph; ++ph) tile_phase<C, NT, RMAX, GMAX, DB, PROBE, SH>(D, a, sh, S, ph, A, A, GA, GA);
   }
@@ -1699,13 +1834,20 @@ __global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D0, TileLaunch 
 
 // sh == nullptr: one GPU, the call-id bump and the whole grid of tiles here;
 // else the caller bumped the call ids and `grid` tiles from sh->tile0 run
-template <int C, int NT, int PROBE, int SH, int RG = 0>
+template <int C, int NT, int PROBE, int SH, int RG = 0, int IB0 = -1>
 static hipError_t launch_tiles_c(hipStream_t st, const TileDev& D, const TileLaunch& a, int lds, const TileShard* sh,
                                  int grid) {
   constexpr int RMAX = tile_rmax(C, NT);
   constexpr int DB = tile_double_buffer(C, NT);
   constexpr int GMAX = tile_gmax(NT);
-  auto k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE, SH, RG>;
+  // split layouts (interior first) at one register set; IB0 >= 0 pins it
+  if constexpr (IB0 < 0 && DB == 0) {
+    if (D.batch_split) return launch_tiles_c<C, NT, PROBE, SH, RG, 1>(st, D, a, lds, sh, grid);
+    return launch_tiles_c<C, NT, PROBE, SH, RG, 0>(st, D, a, lds, sh, grid);
+  }
+  constexpr int IB = IB0 > 0 ? 1 : 0;
+  if (D.batch_split && !IB) return hipErrorInvalidValue;  // split layout: double-buffered path not for it
+  auto k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE, SH, RG, IB>;
   lds = lds < kTSpreadLds ? kTSpreadLds : lds;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return e;

@@ -11,7 +11,11 @@
 // granule buffer per rank, poisoned (NaN) before each colour: a draw reaches
 // a reader of another rank only through the remote puts of the plan (rmask),
 // which must be exactly the set of reader ranks; rank slot ranges checked.
-// Usage: tile_sweep_check <n> <m> <tiles> <chains> <seed> [NT RMAX G]  (prints "ok <stats>")
+// With SPLIT = 1 (the 3+-chain kernel's schedule): per phase, every tile's
+// interior batches of colour c, then the ghost cells of colour c-1 (their
+// hand-off), then the boundary batches of c -- an interior slot must not read
+// a row still missing its colour-(c-1) ghost update.
+// Usage: tile_sweep_check <n> <m> <tiles> <chains> <seed> [NT RMAX G SPLIT]  (prints "ok <stats>")
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -42,6 +46,7 @@ int main(int argc, char** argv) {
   const int NT = argc > 6 ? std::atoi(argv[6]) : 256;
   const int RMAX = argc > 7 ? std::atoi(argv[7]) : 16;
   const int G = argc > 8 ? std::atoi(argv[8]) : 1;
+  const bool SPLIT = argc > 9 && std::atoi(argv[9]) != 0;
   const int d = 2, b = m + 1, sweeps = 3;
   std::mt19937_64 g(seed);
   std::uniform_real_distribution<double> U(0, 1);
@@ -57,7 +62,7 @@ int main(int argc, char** argv) {
   const int K = greedy_coloring(nn.data(), n, b, col);
   TileLayout L;
   std::string err;
-  if (!build_tile_layout(nn.data(), n, b, col.data(), locs.data(), d, T, NT, RMAX, L, err, G)) {
+  if (!build_tile_layout(nn.data(), n, b, col.data(), locs.data(), d, T, NT, RMAX, L, err, G, SPLIT)) {
     std::printf("FAIL build: %s\n", err.c_str());
     return 1;
   }
@@ -202,12 +207,9 @@ int main(int argc, char** argv) {
         }
       }
     }
-    for (int c = 0; c < K; ++c) {
-      for (auto& gb : gbuf) std::fill(gb.begin(), gb.end(), std::nan(""));
-      for (int t = 0; t < L.T; ++t) {
-        const int pc = t * K + c;
+    auto own = [&](int t, int c, int bi_lo, int bi_hi) -> int {
         std::vector<double>& r_s = rt[t];
-        for (int bi = L.batch_ptr[pc]; bi < L.batch_ptr[pc + 1]; ++bi) {
+        for (int bi = bi_lo; bi < bi_hi; ++bi) {
           const TileBatch B = L.batch[bi];
           REQUIRE(B.nslots <= NT && B.R <= RMAX);
           // threads past nthr hold padding only (the kernel skips their loads)
@@ -278,8 +280,9 @@ int main(int argc, char** argv) {
             for (int ch = 0; ch < C; ++ch) r_s[(size_t)lr * C + ch] += cval[ch * ncell + e] * acc_s[(size_t)q * C + ch];
           }
         }
-      }
-      for (int t = 0; t < L.T; ++t) {
+        return 0;
+    };
+    auto ghosts = [&](int t, int c) -> int {
         const int pc = t * K + c;
         std::set<int> nbs(L.nb.begin() + L.nb_ptr[pc], L.nb.begin() + L.nb_ptr[pc + 1]);
         for (int gi = L.gptr[pc]; gi < L.gptr[pc + 1]; ++gi) {
@@ -300,6 +303,29 @@ int main(int argc, char** argv) {
           }
           ++ghosts_applied;
         }
+        return 0;
+    };
+    for (int c = 0; c < K; ++c) {
+      // the granules of colour c are rewritten in this phase: poison them
+      for (int x = 0; x < n; ++x)
+        if (col[L.compact_loc[x]] == c + 1)
+          for (auto& gb : gbuf)
+            for (int ch = 0; ch < C; ++ch) gb[(size_t)x * C + ch] = std::nan("");
+      if (!SPLIT) {
+        for (int t = 0; t < L.T; ++t)
+          if (own(t, c, L.batch_ptr[t * K + c], L.batch_ptr[t * K + c + 1])) return 1;
+        for (int t = 0; t < L.T; ++t)
+          if (ghosts(t, c)) return 1;
+      } else {
+        // interior batches, the hand-off of the previous colour, boundary batches
+        REQUIRE(L.split && L.batch_split.size() == (size_t)L.T * K);
+        for (int t = 0; t < L.T; ++t)
+          if (own(t, c, L.batch_ptr[t * K + c], L.batch_split[t * K + c])) return 1;
+        if (s > 0 || c > 0)
+          for (int t = 0; t < L.T; ++t)
+            if (ghosts(t, (c + K - 1) % K)) return 1;
+        for (int t = 0; t < L.T; ++t)
+          if (own(t, c, L.batch_split[t * K + c], L.batch_ptr[t * K + c + 1])) return 1;
       }
     }
   }

@@ -162,6 +162,23 @@ def test_tile_sweep_emulation(tile_check_exe, n, m, tiles, chains, seed, nt, rma
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
 
 
+@pytest.mark.parametrize("n,m,tiles,chains,seed,nt,rmax,G", [
+    (3000, 10, 16, 3, 1, 256, 16, 1), (1500, 10, 16, 3, 2, 64, 4, 1), (60000, 15, 64, 3, 5, 512, 8, 1),
+    (5000, 15, 24, 3, 6, 256, 16, 8), (40, 3, 8, 4, 7, 64, 1, 2)])
+def test_tile_sweep_emulation_split_schedule(tile_check_exe, n, m, tiles, chains, seed, nt, rmax, G):
+    """Interior-first layouts (NNGP_TILE_SPLIT=1, kernels.hip tile_phase_ib):
+    the emulation runs the kernel's schedule -- per colour c every tile's
+    interior batches, then the hand-off of colour c-1, then the boundary
+    batches -- so an interior slot that read a row still missing its
+    colour-(c-1) ghost update would break the 1e-11 bar against the serial
+    sweep."""
+    import subprocess
+
+    out = subprocess.run([str(tile_check_exe), str(n), str(m), str(tiles), str(chains), str(seed), str(nt), str(rmax),
+                          str(G), "1"], capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
+
+
 @pytest.mark.parametrize("n,m,tiles,G,chains,seed", [
     (3000, 10, 16, 2, 1, 1), (5000, 15, 24, 8, 3, 2), (2000, 8, 12, 3, 2, 3), (400, 5, 16, 16, 1, 4),
     (60000, 15, 64, 8, 1, 5), (8, 2, 8, 8, 1, 6)])

@@ -671,3 +671,38 @@ def test_beta0_stats_reuses_loglik_pass_and_invalidates(P, O, engine):
         L, f = ctx.get_linv(0), ctx.get_field()
         B1, Bf = O.linv_mult(L, np.ones(n), NN), O.linv_mult(L, f, NN)
         np.testing.assert_allclose(swept, [B1 @ B1, B1 @ Bf], rtol=1e-10)
+
+
+@pytest.mark.parametrize("n,m,C", [(60000, 15, 3), (20000, 10, 4)])
+def test_tile_engine_interior_first_split_matches_oracle(P, O, engine, monkeypatch, n, m, C):
+    """Interior-first tile layouts (NNGP_TILE_SPLIT=1: per colour the slots
+    that need no hand-off of the previous colour first, kernels.hip
+    tile_phase_ib): every chain after a call of 3 sweeps against the
+    oracle's local-form sweep with the same normals (rtol 1e-8: rows take the
+    updates of colours c and c-1 in either order)."""
+    if engine != "tiles-default":
+        pytest.skip("sets the layout itself")
+    monkeypatch.setenv("NNGP_TILE_SPLIT", "1")
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=n + 1)
+    rng = np.random.default_rng(2)
+    fields = [rng.normal(size=n) for _ in range(C)]
+    b0s, lss, lnvs, seeds = [0.1 * k for k in range(C)], [0.1] * C, [-0.4] * C, [51 + k for k in range(C)]
+    with P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=C) as ctx:
+        assert ctx.info["sweep_engine"] == 1
+        Ls = []
+        for k in range(C):
+            ctx.select(k)
+            ctx.factor(0, "matern15_isotropic", [1.0, 0.05 + 0.01 * k, 0.0])
+            ctx.set_field(fields[k])
+            ctx.set_mu(None, b0s[k])
+            Ls.append(ctx.get_linv(0))
+        ctx.sweep_chains(3, b0s, lss, lnvs, seeds, [0] * C)
+        got = []
+        for k in range(C):
+            ctx.select(k)
+            got.append(ctx.get_field())
+    for k in range(C):
+        z = O.sweep_normals(seeds[k], 0, 3, n)
+        ref = O.sweep("local", fields[k], Ls[k], NN, col, O.precision_diag(Ls[k], NN), np.ones(n, np.int32), y,
+                      np.full(n, b0s[k]), lm, b0s[k], lss[k], lnvs[k], z)
+        np.testing.assert_allclose(got[k], ref, rtol=1e-8, atol=1e-9, err_msg=f"chain {k}")
