@@ -254,7 +254,7 @@ def shard_parity_check(P, args, world, rank, local_rank, dist):
                 ShardContext(locs, NN, col, lm, y, n_ranks=world, rank=rank, device=local_rank, n_chains=C)
                 if shard else P.ChainContext(locs, NN, col, lm, y, device=local_rank, n_chains=C)))
             if shard:
-                init_shard_comm(ctx, dist)
+                init_shard_comm(ctx, dist, rccl=False)
             for k in range(C):
                 ctx.select(k)
                 ctx.factor(0, "exponential_isotropic", [1.0, 0.1, 0.0])
@@ -304,7 +304,7 @@ def shard_main(P, args, world, rank, local_rank, dist, scaling):
     ctx = agree(lambda: ShardContext(wl["locs"], wl["NN"], wl["col"], wl["lm"], wl["y"], n_ranks=world, rank=rank,
                                      device=local_rank, n_chains=C))
     try:
-        init_shard_comm(ctx, dist)
+        init_shard_comm(ctx, dist, rccl=False)
         rng = np.random.default_rng(7)
 
         def prep():
@@ -339,8 +339,9 @@ def shard_main(P, args, world, rank, local_rank, dist, scaling):
     bytes_sweep = C * (8 * nnz + 40 * n) + 4 * nnz
     achieved = bytes_sweep * args.steps / elapsed / 1e9 / world  # per GPU, whole sharded call (wall clock)
     how = ("tile shard: the tiles of all GPUs in one persistent launch per GPU and call, cross-GPU hand-offs "
-           "as 16-B granules stored into the reader GPU's buffer over xGMI (HIP IPC), RCCL broadcast of each "
-           "rank's slots per call" if tiles else "colour shard: one launch per colour, RCCL all-gather per colour")
+           "as 16-B granules stored into the reader GPU's buffer over xGMI (HIP IPC), each rank's halo slots of w "
+           "stored into the peers' replicas after a call (device flags, no RCCL)" if tiles
+           else "colour shard: one launch per colour, RCCL all-gather per colour")
     out = {"metric": "full-field Gibbs sweeps/sec at n=1e6, m=15; achieved HBM GB/s vs roofline",
            "value": args.steps * C * (n / 1e6) / elapsed, "unit": "sweeps/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
@@ -370,7 +371,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--n", "--n-locs", dest="n", type=int, default=1_000_000,
+                    help="locations per GPU-share (--n-locs: the same, safe under torch.distributed.run)")
     ap.add_argument("--m", type=int, default=15)
     ap.add_argument("--covfun", default="matern15_isotropic")
     ap.add_argument("--range", type=float, default=0.05)

@@ -40,7 +40,7 @@ ABI_SYMBOLS = (
     "nngp_shard_ipc_handle", "nngp_shard_ipc_open",
 )
 SHARD_ID_BYTES = 128  # NNGP_SHARD_ID_BYTES
-IPC_HANDLE_BYTES = 64  # NNGP_IPC_HANDLE_BYTES
+IPC_HANDLE_BYTES = 192  # NNGP_IPC_HANDLE_BYTES
 
 
 class NNGPError(RuntimeError):

@@ -151,7 +151,19 @@ struct nngp_ctx {
   uint32_t* rmask_d = nullptr;     // per slot: remote reader ranks
   TileDev* tdev_d = nullptr;       // kTileRanksMax entries: this rank's TileDev, or a group's
   double* peer_gx[kTileRanksMax] = {};  // the other ranks' granule buffers (IPC mappings)
+  double* peer_w[kTileRanksMax] = {};   // ... their w replicas (exchange without RCCL)
+  unsigned* peer_xf[kTileRanksMax] = {};  // ... their exchange flag words
+  unsigned* xflag_d = nullptr;          // kTileRanksMax flag words the peers write (exchange numbers)
   bool peers_open = false;
+  // exchange without RCCL: after a call only the halo (this rank's slots read
+  // by other ranks' rows) goes out; the chains in stale_mask then have a
+  // replica whose other foreign slots are behind, brought up to date by a
+  // full exchange before anything reads the field (SPMD: every rank does it
+  // at the same entry point)
+  int* halo_d = nullptr;
+  int halo_ptr[kTileRanksMax + 1] = {};
+  unsigned xseq = 0;
+  int stale_mask = 0;
   std::map<long long, hipGraphExec_t> graphs;  // key: n_sweeps << 8 | chain mask
   std::vector<hipGraph_t> graph_objs;
 };
@@ -286,6 +298,10 @@ int fetch4(nngp_ctx* c, int nblocks, double out[4]) {
 
 }  // namespace
 
+// tile shard without RCCL (defined with the sharded sweep below)
+static int tile_ipc_exchange(nngp_ctx* c, bool full);
+static int replica_sync(nngp_ctx* c);
+
 // ====================================================================== ABI
 extern "C" {
 
@@ -371,8 +387,13 @@ void nngp_ctx_destroy(nngp_ctx* c) {
                              c->sg_recv_d, c->sg_src_d, c->sg_val_d, c->xbuf_d, c->sp_pairs_d};
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->peers_open)
-    for (int h = 0; h < c->tG; ++h)
-      if (h != c->trank && c->peer_gx[h]) hipIpcCloseMemHandle(c->peer_gx[h]);
+    for (int h = 0; h < c->tG; ++h) {
+      if (h == c->trank) continue;
+      for (void* q : {(void*)c->peer_gx[h], (void*)c->peer_w[h], (void*)c->peer_xf[h]})
+        if (q) hipIpcCloseMemHandle(q);
+    }
+  ptrs.push_back(c->xflag_d);
+  ptrs.push_back(c->halo_d);
   ptrs.push_back(c->rmask_d);
   ptrs.push_back(c->rg_d);
   ptrs.push_back(c->bsplit_d);
@@ -663,8 +684,24 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     if (c->tG > 1) {
       CK(dalloc(&c->rmask_d, TL.rmask.size()));
       CK(upload(c->rmask_d, TL.rmask.data(), TL.rmask.size(), c->st));
+      // the halo of this rank per peer: its slots with a reader on that peer
+      std::vector<int> halo;
+      for (int h = 0; h < kTileRanksMax; ++h) {
+        c->halo_ptr[h] = (int)halo.size();
+        if (h < c->tG && h != c->trank)
+          for (int x = TL.rank_slot0[c->trank]; x < TL.rank_slot0[c->trank + 1]; ++x)
+            if ((TL.rmask[x] >> h) & 1u) halo.push_back(x);
+      }
+      c->halo_ptr[kTileRanksMax] = (int)halo.size();
+      CK(dalloc(&c->halo_d, halo.size()));
+      CK(upload(c->halo_d, halo.data(), halo.size(), c->st));
+      CK(hipStreamSynchronize(c->st));
     }
-    if (c->tG > 0) CK(dalloc(&c->tdev_d, kTileRanksMax));
+    if (c->tG > 0) {
+      CK(dalloc(&c->tdev_d, kTileRanksMax));
+      CK(dalloc(&c->xflag_d, kTileRanksMax));
+      CK(hipMemsetAsync(c->xflag_d, 0, sizeof(unsigned) * kTileRanksMax, c->st));
+    }
     if (const char* pr = std::getenv("NNGP_PROBE"))
       if ((std::atoi(pr) == 9 || std::atoi(pr) == 2) && (C == 1 || C == 3)) {
         c->tprobe = std::atoi(pr) == 9 ? 1 : 2;
@@ -1005,6 +1042,7 @@ int nngp_set_field(nngp_ctx* c, const double* field) {
   if (!c || !field) return NNGP_ERR_ARG;
   int rc;
   if ((rc = set_device(c))) return rc;
+  c->stale_mask &= ~(1 << c->cur);  // the whole replica of this chain is rewritten
   ChainState& S = c->ch[c->cur];
   S.fgen = ++c->gen;
   if ((rc = upload_field(c, field, S.field_d))) return rc;
@@ -1014,6 +1052,7 @@ int nngp_set_field(nngp_ctx* c, const double* field) {
 
 int nngp_get_field(nngp_ctx* c, double* field) {
   if (!c || !field) return NNGP_ERR_ARG;
+  { int rs_ = replica_sync(c); if (rs_) return rs_; }
   ChainState& S = c->ch[c->cur];
   if (!S.have_field) return fail_msg(c, NNGP_ERR_STATE, "get_field: no field");
   int rc;
@@ -1046,6 +1085,7 @@ int nngp_records_reserve(nngp_ctx* c, int n_rows) {
 
 int nngp_record_field(nngp_ctx* c, int row) {
   if (!c) return NNGP_ERR_ARG;
+  { int rs_ = replica_sync(c); if (rs_) return rs_; }
   ChainState& S = c->ch[c->cur];
   if (!S.rec_d || row < 0 || row >= S.rec_rows) return fail_msg(c, NNGP_ERR_ARG, "record_field: row out of the reserved records");
   if (!S.have_field) return fail_msg(c, NNGP_ERR_STATE, "record_field: no field");
@@ -1097,6 +1137,7 @@ int nngp_set_mu(nngp_ctx* c, const double* mu, double beta0) {
 // ---------------------------------------------------------------- loglik
 int nngp_loglik(nngp_ctx* c, int which, double beta0, double log_scale, double* ll) {
   if (!c || !ll || (which != 0 && which != 1)) return NNGP_ERR_ARG;
+  { int rs_ = replica_sync(c); if (rs_) return rs_; }
   ChainState& S = c->ch[c->cur];
   if (!S.have_factor[which] || !S.have_field) return fail_msg(c, NNGP_ERR_STATE, "loglik: need factor and field");
   int rc;
@@ -1402,6 +1443,54 @@ static int shard_plan_check(const nngp_ctx* c) {
 }
 
 // ---------------------------------------------------------------- tile shard
+// Exchange without RCCL: full -- this rank's slots into every
+// peer's replica (peer copies over xGMI); else only the halo (its slots read
+// by other ranks' rows: what their next prologue needs), stored straight into
+// the peers' replicas.  Then the flags: every rank stores the exchange number
+// into every peer's flag word and waits for all of its own.  A peer writes
+// only this rank's foreign slots, and only after the rendezvous that orders
+// it behind this rank's reads of them.
+static int tile_ipc_exchange(nngp_ctx* c, bool full) {
+  const TileLayout& TL = c->tl;
+  c->xseq++;
+  TilePeerFlags pf;
+  for (int h = 0; h < c->tG; ++h)
+    if (h != c->trank) pf.f[h] = c->peer_xf[h];
+  if (full) {
+    const size_t s0 = (size_t)TL.rank_slot0[c->trank] * c->C;
+    const size_t cnt = (size_t)(TL.rank_slot0[c->trank + 1] - TL.rank_slot0[c->trank]) * c->C;
+    for (int h = 0; h < c->tG; ++h)
+      if (h != c->trank)
+        HIPCHK(c, hipMemcpyAsync(c->peer_w[h] + s0, c->w_slot_d + s0, cnt * sizeof(double), hipMemcpyDeviceToDevice,
+                                 c->st));
+  } else {
+    TilePeerW pw;
+    for (int h = 0; h < c->tG; ++h)
+      if (h != c->trank) pw.w[h] = c->peer_w[h];
+    for (int h = 0; h <= kTileRanksMax; ++h) pw.hptr[h] = c->halo_ptr[h];
+    HIPCHK(c, launch_tile_halo_put(c->st, pw, c->halo_d, c->w_slot_d, c->C));
+  }
+  HIPCHK(c, launch_tile_xsignal(c->st, pf, c->xseq, c->tG, c->trank));
+  HIPCHK(c, launch_tile_xwait(c->st, c->xflag_d, c->ctl_d, c->xseq, c->tG, c->trank));
+  HIPCHK(c, hipMemcpyAsync(c->tmo_h, c->ctl_d + 1, sizeof(unsigned), hipMemcpyDeviceToHost, c->st));
+  return NNGP_OK;
+}
+
+// before an entry point reads the field of a tile-shard rank whose last
+// calls exchanged only the halo: a full exchange, then field = w + beta0 of
+// every slot of those chains again
+static int replica_sync(nngp_ctx* c) {
+  if (!c->stale_mask) return NNGP_OK;
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  const int mask = c->stale_mask;
+  if ((rc = tile_ipc_exchange(c, true))) return rc;
+  if ((rc = enqueue_sweep_body(c, 1, mask, nullptr, 4))) return rc;  // kEpilogue
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  c->stale_mask = 0;
+  return tile_timeout_check(c);
+}
+
 // A call of the tile-sharded sweep on rank trank: prologue
 // (full replica: r = B w of every row), one persistent launch of the rank's
 // tiles (draws read by other ranks' tiles go into their granule buffers over
@@ -1412,6 +1501,7 @@ static int shard_plan_check(const nngp_ctx* c) {
 // never mix (and carry the call id besides).
 static int tile_shard_exchange(nngp_ctx* c) {
   const TileLayout& TL = c->tl;
+  if (!c->comm) return tile_ipc_exchange(c, false);
   ncclResult_t e = ncclGroupStart();
   for (int h = 0; h < c->tG && e == ncclSuccess; ++h) {
     const size_t s0 = (size_t)TL.rank_slot0[h] * c->C, cnt = (size_t)(TL.rank_slot0[h + 1] - TL.rank_slot0[h]) * c->C;
@@ -1436,7 +1526,7 @@ static TileShard tile_shard_args(nngp_ctx* const* ranks, int G, int g0, int Tl) 
 }
 
 static int tile_shard_call(nngp_ctx* c, int n_sweeps, int mask) {
-  if (!c->comm)
+  if (!c->comm && !c->peers_open)
     return fail_msg(c, NNGP_ERR_STATE, "tile shard: no communicator (nngp_shard_comm_init) -- or use nngp_sweep_chains_group");
   if (!c->peers_open)
     return fail_msg(c, NNGP_ERR_STATE, "tile shard: the other ranks' granule buffers are not open (nngp_shard_ipc_open)");
@@ -1470,38 +1560,55 @@ static int tile_shard_call(nngp_ctx* c, int n_sweeps, int mask) {
   }
   if ((rc = enqueue_sweep_body(c, n_sweeps, mask, nullptr, kEpilogue))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->st));
+  if (!c->comm) c->stale_mask |= mask;
   return tile_timeout_check(c);
 }
 
+// the three buffers the other ranks map: granules, w replica, exchange flags
+static_assert(NNGP_IPC_HANDLE_BYTES >= 3 * (int)sizeof(hipIpcMemHandle_t), "IPC handle record");
 int nngp_shard_ipc_handle(nngp_ctx* c, unsigned char* handle, int len) {
-  if (!c || !handle || len < (int)sizeof(hipIpcMemHandle_t)) return NNGP_ERR_ARG;
+  if (!c || !handle || len < NNGP_IPC_HANDLE_BYTES) return NNGP_ERR_ARG;
   if (c->tG < 1) return fail_msg(c, NNGP_ERR_STATE, "shard_ipc_handle: not a tile shard context");
   int rc;
   if ((rc = set_device(c))) return rc;
-  hipIpcMemHandle_t h;
-  HIPCHK(c, hipIpcGetMemHandle(&h, c->dwx_d));
-  std::memcpy(handle, &h, sizeof h);
+  void* bufs[3] = {c->dwx_d, c->w_slot_d, c->xflag_d};
+  for (int k = 0; k < 3; ++k) {
+    hipIpcMemHandle_t h;
+    HIPCHK(c, hipIpcGetMemHandle(&h, bufs[k]));
+    std::memcpy(handle + k * sizeof h, &h, sizeof h);
+  }
   return NNGP_OK;
 }
 
 int nngp_shard_ipc_open(nngp_ctx* c, const unsigned char* handles, int len_each) {
-  if (!c || !handles || len_each < (int)sizeof(hipIpcMemHandle_t)) return NNGP_ERR_ARG;
+  if (!c || !handles || len_each < NNGP_IPC_HANDLE_BYTES) return NNGP_ERR_ARG;
   if (c->tG < 1) return fail_msg(c, NNGP_ERR_STATE, "shard_ipc_open: not a tile shard context");
   if (c->peers_open) return fail_msg(c, NNGP_ERR_STATE, "shard_ipc_open: already open");
   int rc;
   if ((rc = set_device(c))) return rc;
+  auto close_all = [&] {
+    for (int q = 0; q < c->tG; ++q) {
+      if (q == c->trank) continue;
+      for (void** pp : {(void**)&c->peer_gx[q], (void**)&c->peer_w[q], (void**)&c->peer_xf[q]})
+        if (*pp) { hipIpcCloseMemHandle(*pp); *pp = nullptr; }
+    }
+  };
   for (int h = 0; h < c->tG; ++h) {
     if (h == c->trank) continue;
-    hipIpcMemHandle_t hh;
-    std::memcpy(&hh, handles + (size_t)h * len_each, sizeof hh);
-    void* p = nullptr;
-    hipError_t e = hipIpcOpenMemHandle(&p, hh, hipIpcMemLazyEnablePeerAccess);
-    if (e != hipSuccess) {
-      for (int q = 0; q < h; ++q)
-        if (q != c->trank && c->peer_gx[q]) { hipIpcCloseMemHandle(c->peer_gx[q]); c->peer_gx[q] = nullptr; }
-      return fail_hip(c, e, "hipIpcOpenMemHandle (granule buffer of another rank)");
+    void* got[3] = {nullptr, nullptr, nullptr};
+    for (int k = 0; k < 3; ++k) {
+      hipIpcMemHandle_t hh;
+      std::memcpy(&hh, handles + (size_t)h * len_each + k * sizeof hh, sizeof hh);
+      hipError_t e = hipIpcOpenMemHandle(&got[k], hh, hipIpcMemLazyEnablePeerAccess);
+      if (e != hipSuccess) {
+        for (int q = 0; q < k; ++q) hipIpcCloseMemHandle(got[q]);
+        close_all();
+        return fail_hip(c, e, "hipIpcOpenMemHandle (a buffer of another rank)");
+      }
     }
-    c->peer_gx[h] = static_cast<double*>(p);
+    c->peer_gx[h] = static_cast<double*>(got[0]);
+    c->peer_w[h] = static_cast<double*>(got[1]);
+    c->peer_xf[h] = static_cast<unsigned*>(got[2]);
   }
   c->peers_open = true;
   return NNGP_OK;
@@ -1814,6 +1921,7 @@ static TriArgs tri_one(const double* linv) {
 
 int nngp_ancillary_propose(nngp_ctx* c, double beta0, double dlog_scale) {
   if (!c) return NNGP_ERR_ARG;
+  { int rs_ = replica_sync(c); if (rs_) return rs_; }
   ChainState& S = c->ch[c->cur];
   if (!S.have_factor[0] || !S.have_factor[1] || !S.have_field)
     return fail_msg(c, NNGP_ERR_STATE, "ancillary_propose: need both factors and the field");
@@ -1829,6 +1937,7 @@ int nngp_ancillary_propose(nngp_ctx* c, double beta0, double dlog_scale) {
 
 int nngp_ancillary_propose_chains(nngp_ctx* c, int chain_mask, const double* beta0, const double* dlog_scale) {
   if (!c || !beta0 || !dlog_scale || chain_mask <= 0 || chain_mask >= (1 << c->C)) return NNGP_ERR_ARG;
+  { int rs_ = replica_sync(c); if (rs_) return rs_; }
   int rc;
   if ((rc = set_device(c))) return rc;
   TriArgs ta;
@@ -1860,6 +1969,7 @@ int nngp_ancillary_propose_chains(nngp_ctx* c, int chain_mask, const double* bet
 
 int nngp_field_response_ratio(nngp_ctx* c, double beta0, double lnv, double* ratio) {
   if (!c || !ratio) return NNGP_ERR_ARG;
+  { int rs_ = replica_sync(c); if (rs_) return rs_; }
   ChainState& S = c->ch[c->cur];
   if (!S.have_field || !S.have_mu) return fail_msg(c, NNGP_ERR_STATE, "response_ratio: need field and mu");
   int rc;
@@ -1875,6 +1985,7 @@ int nngp_field_response_ratio(nngp_ctx* c, double beta0, double lnv, double* rat
 
 int nngp_accept_field(nngp_ctx* c) {
   if (!c) return NNGP_ERR_ARG;
+  { int rs_ = replica_sync(c); if (rs_) return rs_; }
   int rc;
   if ((rc = set_device(c))) return rc;
   ChainState& S = c->ch[c->cur];
@@ -1885,6 +1996,7 @@ int nngp_accept_field(nngp_ctx* c) {
 
 int nngp_beta0_stats(nngp_ctx* c, double* oqo, double* oqf) {
   if (!c || !oqo || !oqf) return NNGP_ERR_ARG;
+  { int rs_ = replica_sync(c); if (rs_) return rs_; }
   ChainState& S = c->ch[c->cur];
   if (!S.have_factor[0] || !S.have_field) return fail_msg(c, NNGP_ERR_STATE, "beta0_stats: need factor and field");
   // a log-likelihood pass over the current factor and field already has
@@ -1908,6 +2020,7 @@ int nngp_beta0_stats(nngp_ctx* c, double* oqo, double* oqf) {
 
 int nngp_sum_squared_residuals(nngp_ctx* c, double beta0, double* ssr) {
   if (!c || !ssr) return NNGP_ERR_ARG;
+  { int rs_ = replica_sync(c); if (rs_) return rs_; }
   ChainState& S = c->ch[c->cur];
   if (!S.have_field || !S.have_mu) return fail_msg(c, NNGP_ERR_STATE, "ssr: need field and mu");
   int rc;

@@ -202,6 +202,16 @@ hipError_t launch_sweep_tiles(hipStream_t st, const TileDev& D, const TileLaunch
                               int max_batches, int max_gslots, const TileShard* sh = nullptr, int grid = 0);
 // ctl[0] += 1 (call id), ctl[1] = 0 (timeout word): before every launch of a rank
 hipError_t launch_tile_call_bump(hipStream_t st, unsigned* ctl);
+// tile shard, w exchange by peer copies instead of RCCL: signal the peers
+// (flag word `rank` of every other rank := call id), wait for theirs
+struct TilePeerFlags { unsigned* f[kTileRanksMax] = {}; };
+// (flag words carry the exchange sequence number, the same on every rank)
+hipError_t launch_tile_xsignal(hipStream_t st, const TilePeerFlags& pf, unsigned seq, int G, int rank);
+hipError_t launch_tile_xwait(hipStream_t st, const unsigned* xflag, unsigned* ctl, unsigned seq, int G, int rank);
+// halo slots of w into the peers' replicas: hptr[h] .. hptr[h+1] = peer h's
+// entries of `halo` (hptr[kTileRanksMax] = all entries)
+struct TilePeerW { double* w[kTileRanksMax] = {}; int hptr[kTileRanksMax + 1] = {}; };
+hipError_t launch_tile_halo_put(hipStream_t st, const TilePeerW& pw, const int* halo, const double* w, int C);
 // chain `chain`: cell/ghost values from Linv (device order) and precision_diag
 hipError_t launch_tile_refresh(hipStream_t st, const TileDev& D, int nbatches, int NT, const int* cell_src,
                                const int* gsrc, const double* linv, int chain);

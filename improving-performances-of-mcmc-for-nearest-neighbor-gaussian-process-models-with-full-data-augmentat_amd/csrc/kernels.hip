@@ -1174,6 +1174,60 @@ hipError_t launch_tile_call_bump(hipStream_t st, unsigned* ctl) {
   return hipGetLastError();
 }
 
+// tile shard without RCCL: once this rank's own slots of w are in every
+// peer's replica (peer copies ahead on the stream), lane h stores the call id
+// into rank h's flag word `rank`; the wait polls this rank's flag words
+// until every peer's carries the call id (bounded: the timeout word)
+__global__ void tile_xsignal_kernel(TilePeerFlags pf, unsigned seq, int G, int rank) {
+  const int h = threadIdx.x;
+  __threadfence_system();
+  if (h < G && h != rank) __hip_atomic_store(pf.f[h] + rank, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void tile_xwait_kernel(const unsigned* __restrict__ xflag, unsigned* ctl, unsigned seq, int G, int rank) {
+  const int h = threadIdx.x;
+  const unsigned call = seq;
+  if (h < G && h != rank) {
+    for (unsigned spins = 0;; ++spins) {
+      if (__hip_atomic_load(xflag + h, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == call) break;
+      if (spins > (1u << 22)) {
+        __hip_atomic_store(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+}
+
+hipError_t launch_tile_xsignal(hipStream_t st, const TilePeerFlags& pf, unsigned seq, int G, int rank) {
+  hipLaunchKernelGGL(tile_xsignal_kernel, dim3(1), dim3(64), 0, st, pf, seq, G, rank);
+  return hipGetLastError();
+}
+
+hipError_t launch_tile_xwait(hipStream_t st, const unsigned* xflag, unsigned* ctl, unsigned seq, int G, int rank) {
+  hipLaunchKernelGGL(tile_xwait_kernel, dim3(1), dim3(64), 0, st, xflag, ctl, seq, G, rank);
+  return hipGetLastError();
+}
+
+// the rank's halo slots (read by other ranks' rows) into those ranks' w
+// replicas: entry e of peer h's list (hptr[h] <= e < hptr[h+1]) is a slot
+__global__ void tile_halo_put_kernel(TilePeerW pw, const int* __restrict__ halo, const double* __restrict__ w,
+                                     int C) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= pw.hptr[kTileRanksMax]) return;
+  int h = 0;
+  while (e >= pw.hptr[h + 1]) ++h;
+  const int x = halo[e];
+  for (int ch = 0; ch < C; ++ch) pw.w[h][(size_t)x * C + ch] = w[(size_t)x * C + ch];
+}
+
+hipError_t launch_tile_halo_put(hipStream_t st, const TilePeerW& pw, const int* halo, const double* w, int C) {
+  const int ne = pw.hptr[kTileRanksMax];
+  if (ne == 0) return hipSuccess;
+  hipLaunchKernelGGL(tile_halo_put_kernel, dim3((ne + 255) / 256), dim3(256), 0, st, pw, halo, w, C);
+  return hipGetLastError();
+}
+
 // granule cache policy: sc1 (device scope: the producer's write-through store,
 // the consumer's L2-bypassing poll, coherent across the XCDs); tile shard:
 // sc0|sc1 (system scope) for the stores into other ranks' buffers and the

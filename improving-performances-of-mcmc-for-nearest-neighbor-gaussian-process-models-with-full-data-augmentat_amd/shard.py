@@ -98,13 +98,16 @@ def _agreed(dist, fn):
     return res
 
 
-def init_shard_comm(ctx: ShardContext, dist) -> None:
+def init_shard_comm(ctx: ShardContext, dist, rccl: bool = True) -> None:
     """Collective over the torch.distributed group: the RCCL communicator and,
-    for a tile shard, the exchange of the granule-buffer IPC handles (every
-    step agreed by all ranks before the next)."""
+    for a tile shard, the exchange of the IPC handles (every step agreed by
+    all ranks before the next).  rccl=False (tile shard only): no
+    communicator, w is exchanged by peer copies and device flags -- the form
+    that also runs with several ranks on one GPU."""
     if ctx.n_ranks > 1:
-        uid = broadcast_unique_id(dist)
-        _agreed(dist, lambda: ctx.comm_init(uid))
+        if rccl or not ctx.tile_shard:
+            uid = broadcast_unique_id(dist)
+            _agreed(dist, lambda: ctx.comm_init(uid))
         if ctx.tile_shard:
             handles = [None] * ctx.n_ranks
             dist.all_gather_object(handles, _agreed(dist, ctx.ipc_handle))

@@ -52,7 +52,7 @@ extern "C" {
 
 #define NNGP_ABI_VERSION 7
 #define NNGP_SHARD_ID_BYTES 128 /* RCCL unique id */
-#define NNGP_IPC_HANDLE_BYTES 64 /* HIP IPC handle of a tile shard's granule buffer */
+#define NNGP_IPC_HANDLE_BYTES 192 /* HIP IPC handles of a tile shard's granule buffer, w replica, flags */
 
 typedef enum {
   NNGP_OK = 0,
@@ -244,7 +244,9 @@ int nngp_sweep_chains_group(nngp_ctx** ctxs, int n_ranks, int n_sweeps, const do
  * are exchanged out of band (all-gather), and every rank opens the others'.
  * NNGP_ENGINE=colors at creation selects the colour shard instead. */
 int nngp_shard_ipc_handle(nngp_ctx* ctx, unsigned char* handle, int len);
-/* handles: n_ranks x len_each bytes, rank order (this rank's entry ignored) */
+/* handles: n_ranks x len_each bytes, rank order (this rank's entry ignored).
+ * Without a communicator (no nngp_shard_comm_init) a call exchanges w by
+ * peer copies into the mapped replicas and device flags instead of RCCL. */
 int nngp_shard_ipc_open(nngp_ctx* ctx, const unsigned char* handles, int len_each);
 
 /* ---------- measurement ---------- */

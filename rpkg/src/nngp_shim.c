@@ -401,7 +401,7 @@ SEXP C_nngp_shard_ipc_open(SEXP p, SEXP handles) {
   unsigned char buf[16 * NNGP_IPC_HANDLE_BYTES];
   for (int g = 0; g < G; ++g) {
     SEXP h = VECTOR_ELT(handles, g);
-    if (TYPEOF(h) != RAWSXP || XLENGTH(h) != NNGP_IPC_HANDLE_BYTES) Rf_error("nngp: IPC handles must be raw(64)");
+    if (TYPEOF(h) != RAWSXP || XLENGTH(h) != NNGP_IPC_HANDLE_BYTES) Rf_error("nngp: IPC handles must be raw(%d)", NNGP_IPC_HANDLE_BYTES);
     memcpy(buf + (size_t)g * NNGP_IPC_HANDLE_BYTES, RAW(h), NNGP_IPC_HANDLE_BYTES);
   }
   check(nngp_shard_ipc_open(c, buf, NNGP_IPC_HANDLE_BYTES), c);

@@ -70,3 +70,23 @@ def test_tile_shard_headline_equals_single_gpu_bitwise(P, headline, monkeypatch,
     finally:
         for c in ctxs:
             c.close()
+
+
+def test_tile_shard_two_processes_one_gpu_ipc():
+    """The multi-process path of the tile shard (HIP IPC mappings across
+    processes, remote granule stores into the other process's buffer, call ids
+    in step, w by peer copies + device flags) with 2 ranks on the one GPU:
+    tests/mp/tile_shard_ipc_check.py under torch.distributed.run, bitwise equal
+    to one context with the same 32 tiles.  (RCCL itself refuses two ranks on
+    one GPU; its broadcasts replace the copies on an 8-GPU node.)"""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent
+    port = 29900 + os.getpid() % 97
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(root / "tests/mp/tile_shard_ipc_check.py")]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=str(root))
+    assert out.returncode == 0 and "ok tile shard over 2 processes" in out.stdout, out.stdout[-2000:] + out.stderr[-4000:]

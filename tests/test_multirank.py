@@ -103,7 +103,7 @@ class _FakeTileShard:
         self.uid = uid
 
     def ipc_handle(self):
-        return bytes([self.rank + 1]) * 64
+        return bytes([self.rank + 1]) * 192
 
     def ipc_open(self, handles):
         if self.fail_open:
@@ -152,7 +152,7 @@ def test_tile_shard_init_two_ranks(fail_rank):
         for r in range(world):
             st, uid, opened = out[r]
             assert st == "ok" and uid == bytes(range(128))
-            assert opened == [bytes([1]) * 64, bytes([2]) * 64]
+            assert opened == [bytes([1]) * 192, bytes([2]) * 192]
     else:
         for r in range(world):
             st, msg, _ = out[r]
