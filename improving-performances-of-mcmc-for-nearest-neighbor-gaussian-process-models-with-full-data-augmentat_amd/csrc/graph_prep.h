@@ -23,6 +23,7 @@ int greedy_coloring(const int* nn_rowmajor, int n, int b, std::vector<int>& colo
 // Morton (Z-order) key of each location on a 21-bit-per-axis grid over the
 // bounding box of the first min(d,3) coordinates.
 void morton_keys(const double* locs_colmajor, int n, int d, std::vector<uint64_t>& keys);
+void hilbert_keys(const double* locs_colmajor, int n, int d, std::vector<uint64_t>& keys);
 
 // Device layout of the chromatic sweep ("merge-path slot streams").
 //  - r / field / Linv rows: Morton rank of the location (rpos);
