@@ -500,7 +500,12 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       // stream no longer overlaps the hand-off with one register set)
       const char* tsp = std::getenv("NNGP_TILE_SPLIT");
       const bool split = tile_double_buffer(n_chains, NT) == 0 && tsp && std::string(tsp) == "1";
-      bool ok = cus > 0 && T <= n &&
+      // a tile's own rows alone beyond the LDS: no layout to build (n = 8e6 on
+      // one GPU would spend ~30 s building one that cannot run)
+      const bool rg_forced = std::getenv("NNGP_TILE_R") && std::string(std::getenv("NNGP_TILE_R")) == "global";
+      const bool hopeless = !rg_forced && (long long)(n / std::max(T, 1)) * n_chains * 8 > (long long)lds_max;
+      if (hopeless) terr = "tile layout: a tile's own rows exceed the LDS";
+      bool ok = cus > 0 && T <= n && !hopeless &&
                 build_tile_layout(nn.data(), n, b, coloring, locs, d, T, NT, tile_rmax(n_chains, NT), c->tl, terr, G,
                                   split);
       const int need = ok ? tile_lds_bytes(c->tl.max_rows, n_chains, NT, c->tl.K, c->tl.max_batches, c->tl.max_gslots) : 0;
