@@ -658,110 +658,180 @@ bool build_tile_layout(const int* nn, int n, int b, const int* colors, const dou
   L.batch_ptr.assign((size_t)T * K + 1, 0);
   L.gptr.assign((size_t)T * K + 1, 0);
   L.gslot_ptr.assign((size_t)T * K + 1, 0);
-  std::vector<int> gidx(n, -1);  // slot -> index in the current (tile, colour)'s foreign slots
   L.nb_ptr.assign((size_t)T * K + 1, 0);
   L.erow_ptr.assign(T + 1, 0);
-  std::vector<int> lr_of(n, -1);  // device row -> local row of the current tile
-  std::vector<int> rows;
-  std::vector<std::vector<int>> gh(K);  // ghost cells of the current tile by colour: (lr, x, src)
-  std::vector<int> nbmark(T, -1);
-  for (int t = 0; t < T; ++t) {
-    // local rows: own rows, then ghost rows in Morton order
-    rows.clear();
-    for (int r = L.tile_row0[t]; r < L.tile_row0[t + 1]; ++r) rows.push_back(r);
-    const size_t n_own = rows.size();
-    for (int r = L.tile_row0[t]; r < L.tile_row0[t + 1]; ++r) {
-      const int i = perm[r];
-      for (long long p = cptr[i]; p < cptr[i + 1]; ++p) {
-        const int k = crow[p];
-        if (tile_of[k] != t) rows.push_back(L.rpos[k]);
-      }
-    }
-    std::sort(rows.begin() + n_own, rows.end());
-    rows.erase(std::unique(rows.begin() + n_own, rows.end()), rows.end());
-    if (rows.size() > kTilePadRow) { err = "tile layout: too many local rows in a tile"; return false; }
-    L.max_rows = std::max(L.max_rows, (int)rows.size());
-    for (size_t q = 0; q < rows.size(); ++q) lr_of[rows[q]] = (int)q;
-    L.erow.insert(L.erow.end(), rows.begin(), rows.end());
-    L.erow_ptr[t + 1] = (int)L.erow.size();
-    // own batches, colour by colour (split: the interior run, then the boundary run)
-    for (int c = 0; c < K; ++c) {
-      const size_t pc = (size_t)t * K + c;
-      int x = tc_ptr[pc];
-      const int xe_all = tc_ptr[pc + 1];
-      if (split) L.batch_split.push_back((int)L.batch.size());
-      for (int run = 0; run < (split ? 2 : 1); ++run) {
-      const int xe = split && run == 0 ? tc_split[pc] : xe_all;
-      if (split && run == 1) L.batch_split[pc] = (int)L.batch.size();
-      while (x < xe) {
-        int cells = 0, ns = 0;
-        while (x + ns < xe && ns < std::min(NT, kTileSlotsMax)) {
-          const int len = (int)(cptr[L.compact_loc[x + ns] + 1] - cptr[L.compact_loc[x + ns]]);
-          if (cells + len > NT * RMAX) break;
-          cells += len;
-          ++ns;
+  if (split) L.batch_split.assign((size_t)T * K, 0);
+  // Per tile independently (threads over tile ranges), then concatenated in
+  // tile order: the layout is the same for any thread count.
+  struct TileOut {
+    std::vector<int> rows;                 // local rows (device rows)
+    std::vector<TileBatch> batch;          // off relative to the tile's first cell
+    std::vector<int> bptr, bsplit;         // K+1 / K, relative to the tile's first batch
+    std::vector<uint32_t> cell_pk;
+    std::vector<int> cell_src;
+    std::vector<int> slot_f0;              // own slots [tc_ptr[t*K], tc_ptr[t*K+K]): f0 bits
+    std::vector<int> gcell, gsrc, gslot, nb;
+    std::vector<int> gptr, gsptr, nbptr;   // K+1, relative
+    std::vector<int> exported;             // foreign slots this tile reads
+    std::vector<std::pair<int, int>> rbits;  // (slot, reader rank) across ranks
+    int max_gslots = 0;
+    std::string err;
+  };
+  const int nth = std::max(1, std::min(std::min(host_threads(), 8), T));
+  std::vector<TileOut> outs(T);
+  auto build_range = [&](int t0, int t1) {
+    std::vector<int> gidx(n, -1);   // slot -> index in the current (tile, colour)'s foreign slots
+    std::vector<int> lr_of(n, -1);  // device row -> local row of the current tile
+    std::vector<int> nbmark(T, -1);
+    std::vector<std::vector<int>> gh(K);  // ghost cells of the current tile by colour: (lr, x, src)
+    for (int t = t0; t < t1; ++t) {
+      TileOut& o = outs[t];
+      std::vector<int>& rows = o.rows;
+      // local rows: own rows, then ghost rows in curve order
+      for (int r = L.tile_row0[t]; r < L.tile_row0[t + 1]; ++r) rows.push_back(r);
+      const size_t n_own = rows.size();
+      for (int r = L.tile_row0[t]; r < L.tile_row0[t + 1]; ++r) {
+        const int i = perm[r];
+        for (long long p = cptr[i]; p < cptr[i + 1]; ++p) {
+          const int k = crow[p];
+          if (tile_of[k] != t) rows.push_back(L.rpos[k]);
         }
-        const int R = std::max(1, (cells + NT - 1) / NT);
-        TileBatch tb{(int)L.cell_pk.size(), R, ns, x, (cells + R - 1) / R};
-        if ((long long)L.cell_pk.size() + (long long)R * NT > INT32_MAX) { err = "tile layout: too many cells"; return false; }
-        L.cell_pk.resize(L.cell_pk.size() + (size_t)R * NT, kTilePadRow);
-        L.cell_src.resize(L.cell_pk.size(), -1);
-        int f = 0;
-        for (int q = 0; q < ns; ++q) {
-          const int i = L.compact_loc[x + q];
-          L.slot_f0[x + q] = (L.slot_f0[x + q] & kSlotExported) | f;
-          const long long p0 = cptr[i], p1 = cptr[i + 1];
-          for (long long p = p0; p < p1; ++p, ++f) {
-            const int k = crow[p];
-            uint32_t pk = (uint32_t)lr_of[L.rpos[k]] | ((uint32_t)q << kTileQShift);
-            if (p == p0) pk |= kCellStart;
-            if (p == p1 - 1) pk |= kCellEnd;
-            const size_t e = (size_t)tb.off + (size_t)(f % R) * NT + f / R;
-            L.cell_pk[e] = pk;
-            L.cell_src[e] = L.rpos[k] * b + cu[p];
+      }
+      std::sort(rows.begin() + n_own, rows.end());
+      rows.erase(std::unique(rows.begin() + n_own, rows.end()), rows.end());
+      if (rows.size() > kTilePadRow) { o.err = "tile layout: too many local rows in a tile"; return; }
+      for (size_t q = 0; q < rows.size(); ++q) lr_of[rows[q]] = (int)q;
+      // own batches, colour by colour (split: the interior run, then the boundary run)
+      const int xs0 = tc_ptr[(size_t)t * K];
+      o.slot_f0.assign(tc_ptr[(size_t)t * K + K] - xs0, 0);
+      o.bptr.assign(K + 1, 0);
+      if (split) o.bsplit.assign(K, 0);
+      for (int c = 0; c < K; ++c) {
+        const size_t pc = (size_t)t * K + c;
+        int x = tc_ptr[pc];
+        const int xe_all = tc_ptr[pc + 1];
+        if (split) o.bsplit[c] = (int)o.batch.size();
+        for (int run = 0; run < (split ? 2 : 1); ++run) {
+          const int xe = split && run == 0 ? tc_split[pc] : xe_all;
+          if (split && run == 1) o.bsplit[c] = (int)o.batch.size();
+          while (x < xe) {
+            int cells = 0, ns = 0;
+            while (x + ns < xe && ns < std::min(NT, kTileSlotsMax)) {
+              const int len = (int)(cptr[L.compact_loc[x + ns] + 1] - cptr[L.compact_loc[x + ns]]);
+              if (cells + len > NT * RMAX) break;
+              cells += len;
+              ++ns;
+            }
+            const int R = std::max(1, (cells + NT - 1) / NT);
+            TileBatch tb{(int)o.cell_pk.size(), R, ns, x, (cells + R - 1) / R};
+            o.cell_pk.resize(o.cell_pk.size() + (size_t)R * NT, kTilePadRow);
+            o.cell_src.resize(o.cell_pk.size(), -1);
+            int f = 0;
+            for (int q = 0; q < ns; ++q) {
+              const int i = L.compact_loc[x + q];
+              o.slot_f0[x + q - xs0] = f;
+              const long long p0 = cptr[i], p1 = cptr[i + 1];
+              for (long long p = p0; p < p1; ++p, ++f) {
+                const int k = crow[p];
+                uint32_t pk = (uint32_t)lr_of[L.rpos[k]] | ((uint32_t)q << kTileQShift);
+                if (p == p0) pk |= kCellStart;
+                if (p == p1 - 1) pk |= kCellEnd;
+                const size_t e = (size_t)tb.off + (size_t)(f % R) * NT + f / R;
+                o.cell_pk[e] = pk;
+                o.cell_src[e] = L.rpos[k] * b + cu[p];
+              }
+            }
+            o.batch.push_back(tb);
+            x += ns;
           }
         }
-        L.batch.push_back(tb);
-        x += ns;
+        o.bptr[c + 1] = (int)o.batch.size();
       }
+      // ghost cells: foreign members j of the tile's rows, by colour of j
+      for (auto& g : gh) g.clear();
+      for (size_t q = 0; q < rows.size(); ++q) {
+        const int k = perm[rows[q]];
+        for (int u = 0; u < b; ++u) {
+          const int j = nn[(size_t)k * b + u];
+          if (j < 0 || tile_of[j] == t) continue;
+          auto& g = gh[colors[j] - 1];
+          g.push_back((int)q);
+          g.push_back(slot_of[j]);
+          g.push_back(L.rpos[k] * b + u);
+          o.exported.push_back(slot_of[j]);
+        }
       }
-      L.batch_ptr[pc + 1] = (int)L.batch.size();
+      o.gptr.assign(K + 1, 0);
+      o.gsptr.assign(K + 1, 0);
+      o.nbptr.assign(K + 1, 0);
+      for (int c = 0; c < K; ++c) {
+        const size_t pc = (size_t)t * K + c;
+        const int gs0 = (int)o.gslot.size();
+        for (size_t g = 0; g < gh[c].size(); g += 3) {
+          const int x = gh[c][g + 1];
+          if (gidx[x] < 0) { gidx[x] = (int)o.gslot.size() - gs0; o.gslot.push_back(x); }
+          o.gcell.push_back(gh[c][g]);
+          o.gcell.push_back(gidx[x]);
+          o.gsrc.push_back(gh[c][g + 2]);
+          const int u = tile_of[L.compact_loc[x]];
+          if (nbmark[u] != (int)pc) { nbmark[u] = (int)pc; o.nb.push_back(u); }
+          if (G > 1 && u / Tl != t / Tl) o.rbits.emplace_back(x, t / Tl);
+        }
+        for (size_t q = gs0; q < o.gslot.size(); ++q) gidx[o.gslot[q]] = -1;
+        o.gsptr[c + 1] = (int)o.gslot.size();
+        o.max_gslots = std::max(o.max_gslots, (int)o.gslot.size() - gs0);
+        o.gptr[c + 1] = (int)o.gsrc.size();
+        o.nbptr[c + 1] = (int)o.nb.size();
+      }
+      for (int r : rows) lr_of[r] = -1;
     }
-    L.max_batches = std::max(L.max_batches, L.batch_ptr[(size_t)t * K + K] - L.batch_ptr[(size_t)t * K]);
-    // ghost cells: foreign members j of the tile's rows, by colour of j
-    for (auto& g : gh) g.clear();
-    for (size_t q = 0; q < rows.size(); ++q) {
-      const int k = perm[rows[q]];
-      for (int u = 0; u < b; ++u) {
-        const int j = nn[(size_t)k * b + u];
-        if (j < 0 || tile_of[j] == t) continue;
-        auto& g = gh[colors[j] - 1];
-        g.push_back((int)q);
-        g.push_back(slot_of[j]);
-        g.push_back(L.rpos[k] * b + u);
-        L.slot_f0[slot_of[j]] |= kSlotExported;
-      }
+  };
+  {
+    std::vector<std::thread> th;
+    for (int h = 0; h < nth; ++h) {
+      const int t0 = (int)((long long)T * h / nth), t1 = (int)((long long)T * (h + 1) / nth);
+      if (nth == 1) build_range(t0, t1);
+      else th.emplace_back([=, &build_range] { build_range(t0, t1); });
+    }
+    for (auto& x : th) x.join();
+  }
+  // concatenate in tile order
+  for (int t = 0; t < T; ++t) {
+    TileOut& o = outs[t];
+    if (!o.err.empty()) { err = o.err; return false; }
+    L.max_rows = std::max(L.max_rows, (int)o.rows.size());
+    L.erow.insert(L.erow.end(), o.rows.begin(), o.rows.end());
+    L.erow_ptr[t + 1] = (int)L.erow.size();
+    const long long cell0 = (long long)L.cell_pk.size();
+    if (cell0 + (long long)o.cell_pk.size() > INT32_MAX) { err = "tile layout: too many cells"; return false; }
+    const int b0 = (int)L.batch.size();
+    for (TileBatch tb : o.batch) {
+      tb.off += (int)cell0;
+      L.batch.push_back(tb);
     }
     for (int c = 0; c < K; ++c) {
-      const size_t pc = (size_t)t * K + c;
-      const int gs0 = (int)L.gslot.size();
-      for (size_t g = 0; g < gh[c].size(); g += 3) {
-        const int x = gh[c][g + 1];
-        if (gidx[x] < 0) { gidx[x] = (int)L.gslot.size() - gs0; L.gslot.push_back(x); }
-        L.gcell.push_back(gh[c][g]);
-        L.gcell.push_back(gidx[x]);
-        L.gsrc.push_back(gh[c][g + 2]);
-        const int u = tile_of[L.compact_loc[x]];
-        if (nbmark[u] != (int)pc) { nbmark[u] = (int)pc; L.nb.push_back(u); }
-        if (G > 1 && u / Tl != t / Tl) L.rmask[x] |= 1u << (t / Tl);
-      }
-      for (size_t q = gs0; q < L.gslot.size(); ++q) gidx[L.gslot[q]] = -1;
-      L.gslot_ptr[pc + 1] = (int)L.gslot.size();
-      L.max_gslots = std::max(L.max_gslots, (int)L.gslot.size() - gs0);
-      L.gptr[pc + 1] = (int)L.gsrc.size();
-      L.nb_ptr[pc + 1] = (int)L.nb.size();
+      L.batch_ptr[(size_t)t * K + c + 1] = b0 + o.bptr[c + 1];
+      if (split) L.batch_split[(size_t)t * K + c] = b0 + o.bsplit[c];
     }
-    for (int r : rows) lr_of[r] = -1;
+    L.max_batches = std::max(L.max_batches, (int)o.batch.size());
+    L.cell_pk.insert(L.cell_pk.end(), o.cell_pk.begin(), o.cell_pk.end());
+    L.cell_src.insert(L.cell_src.end(), o.cell_src.begin(), o.cell_src.end());
+    const int xs0 = tc_ptr[(size_t)t * K];
+    for (size_t q = 0; q < o.slot_f0.size(); ++q) L.slot_f0[xs0 + q] |= o.slot_f0[q];
+    const int gc0 = (int)L.gsrc.size(), gs0 = (int)L.gslot.size(), nb0 = (int)L.nb.size();
+    L.gcell.insert(L.gcell.end(), o.gcell.begin(), o.gcell.end());
+    L.gsrc.insert(L.gsrc.end(), o.gsrc.begin(), o.gsrc.end());
+    L.gslot.insert(L.gslot.end(), o.gslot.begin(), o.gslot.end());
+    L.nb.insert(L.nb.end(), o.nb.begin(), o.nb.end());
+    for (int c = 0; c < K; ++c) {
+      L.gptr[(size_t)t * K + c + 1] = gc0 + o.gptr[c + 1];
+      L.gslot_ptr[(size_t)t * K + c + 1] = gs0 + o.gsptr[c + 1];
+      L.nb_ptr[(size_t)t * K + c + 1] = nb0 + o.nbptr[c + 1];
+    }
+    L.max_gslots = std::max(L.max_gslots, o.max_gslots);
+    for (int x : o.exported) L.slot_f0[x] |= kSlotExported;
+    for (const auto& xb : o.rbits) L.rmask[xb.first] |= 1u << xb.second;
+    o = TileOut();  // free as we go
   }
   return true;
 }
