@@ -336,7 +336,17 @@ int main(int argc, char** argv) {
       maxrel = std::max(maxrel, std::fabs(a - r) / std::max(1.0, std::fabs(r)));
     }
   if (!(maxrel < 1e-11)) { std::printf("FAIL maxrel %.3e\n", maxrel); return 1; }
-  std::printf("ok K=%d T=%d G=%d max_rows=%d batches=%zu cells=%zu ghosts=%zu nb=%zu remote_puts=%lld maxrel=%.2e\n",
-              K, L.T, G, L.max_rows, L.batch.size(), ncell, ng, L.nb.size(), remote_puts, maxrel);
+  // FNV hash of every layout array (the layout must not depend on the host thread count)
+  unsigned long long lh = 1469598103934665603ULL;
+  auto mix = [&](const void* p, size_t bytes) {
+    for (size_t i = 0; i < bytes; ++i) lh = (lh ^ ((const unsigned char*)p)[i]) * 1099511628211ULL;
+  };
+  auto mixv = [&](const auto& v) { mix(v.data(), v.size() * sizeof(v[0])); };
+  mixv(L.rpos); mixv(L.compact_loc); mixv(L.slot_f0); mixv(L.erow_ptr); mixv(L.erow); mixv(L.batch_ptr);
+  mixv(L.cell_pk); mixv(L.cell_src); mixv(L.gcell); mixv(L.gsrc); mixv(L.gptr); mixv(L.gslot); mixv(L.gslot_ptr);
+  mixv(L.nb_ptr); mixv(L.nb); mixv(L.rmask); mixv(L.batch_split);
+  for (const TileBatch& tb : L.batch) mix(&tb, sizeof tb);
+  std::printf("ok K=%d T=%d G=%d max_rows=%d batches=%zu cells=%zu ghosts=%zu nb=%zu remote_puts=%lld maxrel=%.2e "
+              "layout=%016llx\n", K, L.T, G, L.max_rows, L.batch.size(), ncell, ng, L.nb.size(), remote_puts, maxrel, lh);
   return 0;
 }

@@ -162,6 +162,24 @@ def test_tile_sweep_emulation(tile_check_exe, n, m, tiles, chains, seed, nt, rma
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
 
 
+@pytest.mark.parametrize("args", [("30000", "15", "64", "3", "5", "512", "8", "8", "0"),
+                                  ("20000", "10", "40", "1", "2", "256", "16", "1", "0"),
+                                  ("20000", "10", "48", "3", "3", "512", "8", "4", "1")])
+def test_tile_layout_independent_of_host_threads(tile_check_exe, args):
+    """The tile layout is built per tile on host threads and concatenated in
+    tile order: every layout array (hashed) is the same with 1 and 8 threads."""
+    import os
+    import subprocess
+
+    outs = []
+    for th in ("1", "8"):
+        env = dict(os.environ, NNGP_HOST_THREADS=th)
+        out = subprocess.run([str(tile_check_exe), *args], capture_output=True, text=True, env=env)
+        assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
+        outs.append(out.stdout.split("layout=")[1].split()[0])
+    assert outs[0] == outs[1]
+
+
 @pytest.mark.parametrize("n,m,tiles,chains,seed,nt,rmax,G", [
     (3000, 10, 16, 3, 1, 256, 16, 1), (1500, 10, 16, 3, 2, 64, 4, 1), (60000, 15, 64, 3, 5, 512, 8, 1),
     (5000, 15, 24, 3, 6, 256, 16, 8), (40, 3, 8, 4, 7, 64, 1, 2)])
