@@ -38,6 +38,8 @@ ABI_SYMBOLS = (
     "nngp_ctx_create_shard", "nngp_shard_unique_id", "nngp_shard_comm_init", "nngp_sweep_chains_group",
     "nngp_records_reserve", "nngp_record_field", "nngp_get_records",
     "nngp_shard_ipc_handle", "nngp_shard_ipc_open",
+    "nngp_factor_chains", "nngp_loglik_chains", "nngp_field_response_ratio_chains",
+    "nngp_sum_squared_residuals_chains",
 )
 SHARD_ID_BYTES = 128  # NNGP_SHARD_ID_BYTES
 IPC_HANDLE_BYTES = 192  # NNGP_IPC_HANDLE_BYTES
@@ -115,6 +117,10 @@ def _load():
     L.nngp_shard_unique_id.argtypes = [C.c_char_p, C.c_int]
     L.nngp_shard_comm_init.argtypes = [_vp, C.c_char_p, C.c_int]
     L.nngp_sweep_chains_group.argtypes = [C.POINTER(_vp), C.c_int, C.c_int, _dp, _dp, _dp, _up, _up]
+    L.nngp_factor_chains.argtypes = [_vp, C.c_int, C.c_int, C.c_int, _dp, C.c_int, _ip]
+    L.nngp_loglik_chains.argtypes = [_vp, C.c_int, C.c_int, _dp, _dp, _dp]
+    L.nngp_field_response_ratio_chains.argtypes = [_vp, C.c_int, _dp, _dp, _dp]
+    L.nngp_sum_squared_residuals_chains.argtypes = [_vp, C.c_int, _dp, _dp]
     L.nngp_shard_ipc_handle.argtypes = [_vp, C.c_char_p, C.c_int]
     L.nngp_shard_ipc_open.argtypes = [_vp, C.c_char_p, C.c_int]
     L.nngp_records_reserve.argtypes = [_vp, C.c_int]

@@ -184,6 +184,37 @@ class ChainContext:
         d = np.ascontiguousarray(np.broadcast_to(np.asarray(dlog_scale, np.float64), (k,)))
         self._chk(lib.nngp_ancillary_propose_chains(self._h, int(chain_mask), b, d))
 
+    # ---- batched forms: every chain in chain_mask in one call (one host sync);
+    # per-chain arrays indexed by chain, entries of other chains ignored
+    def _vec(self, v):
+        return np.ascontiguousarray(np.broadcast_to(np.asarray(v, np.float64), (self.n_chains,)))
+
+    def factor_chains(self, which: int, chain_mask: int, covfun: str, covparms) -> np.ndarray:
+        """-> per-chain status (0 = ok, NNGP_ERR_CHOL = not positive definite);
+        covparms: n_chains rows (chains outside the mask: any values)."""
+        cps = np.ascontiguousarray(np.asarray(covparms, np.float64).reshape(self.n_chains, -1))
+        st = np.zeros(self.n_chains, np.int32)
+        self._chk(lib.nngp_factor_chains(self._h, int(which), int(chain_mask), COVFUNS[covfun], cps.reshape(-1),
+                                         cps.shape[1], st))
+        return st
+
+    def loglik_chains(self, which: int, chain_mask: int, beta0, log_scale) -> np.ndarray:
+        out = np.zeros(self.n_chains)
+        self._chk(lib.nngp_loglik_chains(self._h, int(which), int(chain_mask), self._vec(beta0), self._vec(log_scale),
+                                         out))
+        return out
+
+    def field_response_ratio_chains(self, chain_mask: int, beta0, log_noise_variance) -> np.ndarray:
+        out = np.zeros(self.n_chains)
+        self._chk(lib.nngp_field_response_ratio_chains(self._h, int(chain_mask), self._vec(beta0),
+                                                       self._vec(log_noise_variance), out))
+        return out
+
+    def sum_squared_residuals_chains(self, chain_mask: int, beta0) -> np.ndarray:
+        out = np.zeros(self.n_chains)
+        self._chk(lib.nngp_sum_squared_residuals_chains(self._h, int(chain_mask), self._vec(beta0), out))
+        return out
+
     def field_response_ratio(self, beta0: float, log_noise_variance: float) -> float:
         out = C.c_double()
         self._chk(lib.nngp_field_response_ratio(self._h, float(beta0), float(log_noise_variance),
@@ -229,7 +260,8 @@ class ChainView:
     def __getattr__(self, name):
         attr = getattr(self.ctx, name)
         if not callable(attr) or name in ("close", "view", "sweep_chains", "sweep_timed",
-                                                     "ancillary_propose_chains"):
+                                                     "ancillary_propose_chains", "factor_chains", "loglik_chains",
+                                                     "field_response_ratio_chains", "sum_squared_residuals_chains"):
             return attr
 
         def bound(*a, **kw):

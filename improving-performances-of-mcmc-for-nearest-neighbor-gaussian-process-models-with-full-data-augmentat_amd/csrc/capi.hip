@@ -103,7 +103,8 @@ struct nngp_ctx {
   size_t z_cap = 0;
   SweepScalars* scal_d = nullptr;  // C
   SweepScalars* scal_h = nullptr;  // pinned, C
-  double* res_h = nullptr;         // pinned, 8 doubles
+  double* res_h = nullptr;         // pinned, 4 x kMaxChains doubles
+  int* fail_h = nullptr;           // pinned, kMaxChains failure rows of the factors
   unsigned long long* dbg_d = nullptr;  // NNGP_PROBE=9: per-chunk timestamps
   // tile-resident sweep engine (engine == 1; graph_prep.h TileLayout)
   int engine = 0;                 // 0: colour launches, 1: tiles
@@ -281,9 +282,9 @@ int refresh_sweep_values(nngp_ctx* c, int k) {
     const int ng = (int)c->sp.grow.size();
     HIPCHK(c, launch_permute_gather(c->st, ng, c->sg_src_d, c->ch[k].linv_d[0], c->sg_val_d + (size_t)k * ng));
   }
+  // the table entry travels as a kernel argument: no host sync needed
   c->linv_cur_h[k] = c->ch[k].linv_d[0];
-  HIPCHK(c, hipMemcpyAsync(c->linv_cur_d, c->linv_cur_h, sizeof(double*) * c->C, hipMemcpyHostToDevice, c->st));
-  HIPCHK(c, hipStreamSynchronize(c->st));
+  HIPCHK(c, launch_set_ptr(c->st, c->linv_cur_d, k, c->ch[k].linv_d[0]));
   return NNGP_OK;
 }
 
@@ -405,6 +406,7 @@ void nngp_ctx_destroy(nngp_ctx* c) {
   for (void* p : ptrs) if (p) hipFree(p);
   if (c->scal_h) hipHostFree(c->scal_h);
   if (c->res_h) hipHostFree(c->res_h);
+  if (c->fail_h) hipHostFree(c->fail_h);
   if (c->linv_cur_h) hipHostFree(c->linv_cur_h);
   if (c->stage_h) hipHostFree(c->stage_h);
   if (c->mu_stage_h) hipHostFree(c->mu_stage_h);
@@ -618,7 +620,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
   CK(dalloc(&c->linv_cur_d, C));
   CK(hipHostMalloc((void**)&c->linv_cur_h, sizeof(double*) * C, hipHostMallocDefault));
   for (int k = 0; k < C; ++k) c->linv_cur_h[k] = c->ch[k].linv_d[0];
-  CK(dalloc(&c->fail_d, 1));
+  CK(dalloc(&c->fail_d, kMaxChains));
   CK(dalloc(&c->sinfo_d, NS));
   CK(dalloc(&c->compact_loc_d, NS));
   CK(dalloc(&c->dr_d, NS * C));
@@ -750,11 +752,12 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
   CK(dalloc(&c->tmp_d, (size_t)n * C));   // scratch vectors, chain-strided for batched solves
   CK(dalloc(&c->tmp2_d, (size_t)n * C));
   CK(dalloc(&c->partials_d, 4 * kRedBlocks));
-  CK(dalloc(&c->res_d, 8));
+  CK(dalloc(&c->res_d, 4 * kMaxChains));
   CK(dalloc(&c->scal_d, C));
   CK(hipHostMalloc((void**)&c->scal_h, sizeof(SweepScalars) * C, hipHostMallocDefault));
   std::memset(c->scal_h, 0, sizeof(SweepScalars) * C);
-  CK(hipHostMalloc((void**)&c->res_h, 8 * sizeof(double), hipHostMallocDefault));
+  CK(hipHostMalloc((void**)&c->res_h, 4 * kMaxChains * sizeof(double), hipHostMallocDefault));
+  CK(hipHostMalloc((void**)&c->fail_h, kMaxChains * sizeof(int), hipHostMallocDefault));
   CK(upload(c->locs_d, locs_rm.data(), locs_rm.size(), c->st));
   CK(upload(c->nn_d, nn_dev.data(), nn_dev.size(), c->st));
   {
@@ -932,41 +935,81 @@ static int covfun_family(int covfun, int d, const double* cp, int ncp, double* v
   return fam;
 }
 
-int nngp_factor(nngp_ctx* c, int which, int covfun, const double* cp, int ncp) {
-  if (!c || (which != 0 && which != 1) || !cp) return fail_msg(c, NNGP_ERR_ARG, "factor: bad args");
+// the factor of chain k into slot `which`; its failure row (or INT_MAX)
+// lands in fail_d[k] (the caller copies the flags once for all chains)
+static int factor_enqueue(nngp_ctx* c, int k, int which, int covfun, const double* cp, int ncp) {
   double var, nug, nu;
   std::string err;
   int fam = covfun_family(covfun, c->d, cp, ncp, &var, &nug, &nu, err);
   if (fam < 0) return fail_msg(c, NNGP_ERR_ARG, err);
-  int rc;
-  if ((rc = set_device(c))) return rc;
-  ChainState& S = c->ch[c->cur];
+  ChainState& S = c->ch[k];
   const bool sphere = covfun == NNGP_EXPONENTIAL_SPHERE || covfun == NNGP_MATERN_SPHERE;
   if (sphere && c->ds < 3) {
     // sphere on d == 2: scaled coordinates are 3-D; grow the buffer once
+    HIPCHK(c, hipStreamSynchronize(c->st));
     hipFree(c->sc_d);
     c->sc_d = nullptr;
     HIPCHK(c, dalloc(&c->sc_d, (size_t)c->n * 4));
     c->ds = 4;  // capacity marker
   }
   const int use_ds = sphere ? 3 : (c->d <= 2 ? 2 : (c->d == 3 ? 3 : 4));
+  // the scaled coordinates are shared scratch: the chains' factors run one
+  // after another in stream order
   HIPCHK(c, launch_scale_coords(c->st, covfun, cp, ncp, c->locs_d, c->n, c->d, c->sc_d, use_ds));
-  const int big = INT_MAX;
-  HIPCHK(c, hipMemcpyAsync(c->fail_d, &big, sizeof(int), hipMemcpyHostToDevice, c->st));
+  HIPCHK(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->fail_d + k), INT_MAX, 1, c->st));
   S.lgen[which] = ++c->gen;
-  HIPCHK(c, launch_factor(c->st, fam, var, nug, nu, c->sc_d, use_ds, c->nn_d, c->n, c->b, S.linv_d[which], c->fail_d));
-  int fail = 0;
-  HIPCHK(c, hipMemcpyAsync(&fail, c->fail_d, sizeof(int), hipMemcpyDeviceToHost, c->st));
-  HIPCHK(c, hipStreamSynchronize(c->st));
-  if (fail != big) {
-    S.have_factor[which] = false;
-    char buf[160];
-    std::snprintf(buf, sizeof buf, "vecchia factor: local covariance of row %d is not positive definite", fail);
-    return fail_msg(c, NNGP_ERR_CHOL, buf);
-  }
-  S.have_factor[which] = true;
-  if (which == 0) return refresh_sweep_values(c, c->cur);
+  HIPCHK(c, launch_factor(c->st, fam, var, nug, nu, c->sc_d, use_ds, c->nn_d, c->n, c->b, S.linv_d[which],
+                          c->fail_d + k));
   return NNGP_OK;
+}
+
+// after factor_enqueue of the chains in mask: one copy of the flags, one sync
+static int factor_collect(nngp_ctx* c, int which, int mask, int* status) {
+  HIPCHK(c, hipMemcpyAsync(c->fail_h, c->fail_d, sizeof(int) * c->C, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  int rc = NNGP_OK;
+  for (int k = 0; k < c->C; ++k) {
+    if (!((mask >> k) & 1)) continue;
+    ChainState& S = c->ch[k];
+    if (c->fail_h[k] != INT_MAX) {
+      S.have_factor[which] = false;
+      char buf[160];
+      std::snprintf(buf, sizeof buf, "vecchia factor: local covariance of row %d is not positive definite",
+                    c->fail_h[k]);
+      fail_msg(c, NNGP_ERR_CHOL, buf);
+      if (status) status[k] = NNGP_ERR_CHOL;
+      rc = NNGP_ERR_CHOL;
+      continue;
+    }
+    S.have_factor[which] = true;
+    if (status) status[k] = NNGP_OK;
+    if (which == 0) {
+      int r2 = refresh_sweep_values(c, k);
+      if (r2) return r2;
+    }
+  }
+  return rc;
+}
+
+int nngp_factor(nngp_ctx* c, int which, int covfun, const double* cp, int ncp) {
+  if (!c || (which != 0 && which != 1) || !cp) return fail_msg(c, NNGP_ERR_ARG, "factor: bad args");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  if ((rc = factor_enqueue(c, c->cur, which, covfun, cp, ncp))) return rc;
+  return factor_collect(c, which, 1 << c->cur, nullptr);
+}
+
+int nngp_factor_chains(nngp_ctx* c, int which, int chain_mask, int covfun, const double* covparms, int ncp,
+                       int* status) {
+  if (!c || (which != 0 && which != 1) || !covparms || !status || chain_mask <= 0 || chain_mask >= (1 << c->C))
+    return fail_msg(c, NNGP_ERR_ARG, "factor_chains: bad args");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  for (int k = 0; k < c->C; ++k)
+    if ((chain_mask >> k) & 1)
+      if ((rc = factor_enqueue(c, k, which, covfun, covparms + (size_t)k * ncp, ncp))) return rc;
+  rc = factor_collect(c, which, chain_mask, status);
+  return rc == NNGP_ERR_CHOL ? NNGP_OK : rc;  // per-chain outcomes in status
 }
 
 int nngp_get_linv(nngp_ctx* c, int which, double* Linv) {
@@ -1140,25 +1183,55 @@ int nngp_set_mu(nngp_ctx* c, const double* mu, double beta0) {
 }
 
 // ---------------------------------------------------------------- loglik
-int nngp_loglik(nngp_ctx* c, int which, double beta0, double log_scale, double* ll) {
-  if (!c || !ll || (which != 0 && which != 1)) return NNGP_ERR_ARG;
-  { int rs_ = replica_sync(c); if (rs_) return rs_; }
-  ChainState& S = c->ch[c->cur];
+// row statistics of chain k's field under factor `which` into res_d[4k..]
+static int rowstats_enqueue(nngp_ctx* c, int k, int which, double beta0) {
+  ChainState& S = c->ch[k];
   if (!S.have_factor[which] || !S.have_field) return fail_msg(c, NNGP_ERR_STATE, "loglik: need factor and field");
-  int rc;
-  if ((rc = set_device(c))) return rc;
-  int nb = launch_row_stats(c->st, S.linv_d[which], c->nn_d, c->n, c->b, S.field_d, beta0, nullptr,
-                            c->partials_d);
+  int nb = launch_row_stats(c->st, S.linv_d[which], c->nn_d, c->n, c->b, S.field_d, beta0, nullptr, c->partials_d);
   HIPCHK(c, hipGetLastError());
-  double r[4];
-  if ((rc = fetch4(c, nb, r))) return rc;
-  *ll = r[0] - c->n * 0.5 * log_scale - 0.5 * r[1] / std::exp(log_scale);
+  HIPCHK(c, launch_reduce4(c->st, c->partials_d, nb, c->res_d + 4 * k));
+  return NNGP_OK;
+}
+
+static void rowstats_store(nngp_ctx* c, int k, int which, double beta0, const double* r) {
+  ChainState& S = c->ch[k];
   ChainState::RowStats& e = S.rs[S.rs_next];
   S.rs_next ^= 1;
   e.lg = S.lgen[which];
   e.fg = S.fgen;
   e.shift = beta0;
-  for (int k = 0; k < 4; ++k) e.r[k] = r[k];
+  for (int q = 0; q < 4; ++q) e.r[q] = r[q];
+}
+
+int nngp_loglik(nngp_ctx* c, int which, double beta0, double log_scale, double* ll) {
+  if (!c || !ll || (which != 0 && which != 1)) return NNGP_ERR_ARG;
+  double b0[kMaxChains], ls[kMaxChains], out[kMaxChains];
+  b0[c->cur] = beta0;
+  ls[c->cur] = log_scale;
+  int rc = nngp_loglik_chains(c, which, 1 << c->cur, b0, ls, out);
+  if (!rc) *ll = out[c->cur];
+  return rc;
+}
+
+int nngp_loglik_chains(nngp_ctx* c, int which, int chain_mask, const double* beta0, const double* log_scale,
+                       double* ll) {
+  if (!c || !ll || !beta0 || !log_scale || (which != 0 && which != 1) || chain_mask <= 0 ||
+      chain_mask >= (1 << c->C))
+    return NNGP_ERR_ARG;
+  { int rs_ = replica_sync(c); if (rs_) return rs_; }
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  for (int k = 0; k < c->C; ++k)
+    if ((chain_mask >> k) & 1)
+      if ((rc = rowstats_enqueue(c, k, which, beta0[k]))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->res_h, c->res_d, 4 * c->C * sizeof(double), hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  for (int k = 0; k < c->C; ++k) {
+    if (!((chain_mask >> k) & 1)) continue;
+    const double* r = c->res_h + 4 * k;
+    ll[k] = r[0] - c->n * 0.5 * log_scale[k] - 0.5 * r[1] / std::exp(log_scale[k]);
+    rowstats_store(c, k, which, beta0[k], r);
+  }
   return NNGP_OK;
 }
 
@@ -1972,20 +2045,48 @@ int nngp_ancillary_propose_chains(nngp_ctx* c, int chain_mask, const double* bet
   return NNGP_OK;  // stream-ordered
 }
 
-int nngp_field_response_ratio(nngp_ctx* c, double beta0, double lnv, double* ratio) {
-  if (!c || !ratio) return NNGP_ERR_ARG;
+// data-term reductions of chain k (mode 1: the dnorm ratio of the proposal,
+// mode 0: the sum of squared residuals) into res_d[4k..]
+static int obs_enqueue(nngp_ctx* c, int k, int mode, double beta0, double lnv) {
+  ChainState& S = c->ch[k];
+  if (!S.have_field || !S.have_mu) return fail_msg(c, NNGP_ERR_STATE, "data term: need field and mu");
+  int nb = launch_obs_reduce(c->st, mode, c->n_obs, c->y_d, S.mu_is_const ? nullptr : S.mu_d, beta0, c->lm_d,
+                             S.field_d, mode == 1 ? S.field_prop_d : nullptr, mode == 1 ? 0.5 * std::exp(-lnv) : 0.0,
+                             c->partials_d);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, launch_reduce4(c->st, c->partials_d, nb, c->res_d + 4 * k));
+  return NNGP_OK;
+}
+
+static int obs_chains(nngp_ctx* c, int mode, int chain_mask, const double* beta0, const double* lnv, double* out) {
+  if (!c || !out || !beta0 || (mode == 1 && !lnv) || chain_mask <= 0 || chain_mask >= (1 << c->C))
+    return NNGP_ERR_ARG;
   { int rs_ = replica_sync(c); if (rs_) return rs_; }
-  ChainState& S = c->ch[c->cur];
-  if (!S.have_field || !S.have_mu) return fail_msg(c, NNGP_ERR_STATE, "response_ratio: need field and mu");
   int rc;
   if ((rc = set_device(c))) return rc;
-  int nb = launch_obs_reduce(c->st, 1, c->n_obs, c->y_d, S.mu_is_const ? nullptr : S.mu_d, beta0,
-                             c->lm_d, S.field_d, S.field_prop_d, 0.5 * std::exp(-lnv), c->partials_d);
-  HIPCHK(c, hipGetLastError());
-  double r[4];
-  if ((rc = fetch4(c, nb, r))) return rc;
-  *ratio = r[0];
+  for (int k = 0; k < c->C; ++k)
+    if ((chain_mask >> k) & 1)
+      if ((rc = obs_enqueue(c, k, mode, beta0[k], mode == 1 ? lnv[k] : 0.0))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->res_h, c->res_d, 4 * c->C * sizeof(double), hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  for (int k = 0; k < c->C; ++k)
+    if ((chain_mask >> k) & 1) out[k] = c->res_h[4 * k];
   return NNGP_OK;
+}
+
+int nngp_field_response_ratio(nngp_ctx* c, double beta0, double lnv, double* ratio) {
+  if (!c || !ratio) return NNGP_ERR_ARG;
+  double b0[kMaxChains], l[kMaxChains], out[kMaxChains];
+  b0[c->cur] = beta0;
+  l[c->cur] = lnv;
+  int rc = obs_chains(c, 1, 1 << c->cur, b0, l, out);
+  if (!rc) *ratio = out[c->cur];
+  return rc;
+}
+
+int nngp_field_response_ratio_chains(nngp_ctx* c, int chain_mask, const double* beta0, const double* lnv,
+                                     double* ratio) {
+  return obs_chains(c, 1, chain_mask, beta0, lnv, ratio);
 }
 
 int nngp_accept_field(nngp_ctx* c) {
@@ -2025,18 +2126,15 @@ int nngp_beta0_stats(nngp_ctx* c, double* oqo, double* oqf) {
 
 int nngp_sum_squared_residuals(nngp_ctx* c, double beta0, double* ssr) {
   if (!c || !ssr) return NNGP_ERR_ARG;
-  { int rs_ = replica_sync(c); if (rs_) return rs_; }
-  ChainState& S = c->ch[c->cur];
-  if (!S.have_field || !S.have_mu) return fail_msg(c, NNGP_ERR_STATE, "ssr: need field and mu");
-  int rc;
-  if ((rc = set_device(c))) return rc;
-  int nb = launch_obs_reduce(c->st, 0, c->n_obs, c->y_d, S.mu_is_const ? nullptr : S.mu_d, beta0,
-                             c->lm_d, S.field_d, nullptr, 0.0, c->partials_d);
-  HIPCHK(c, hipGetLastError());
-  double r[4];
-  if ((rc = fetch4(c, nb, r))) return rc;
-  *ssr = r[0];
-  return NNGP_OK;
+  double b0[kMaxChains], out[kMaxChains];
+  b0[c->cur] = beta0;
+  int rc = obs_chains(c, 0, 1 << c->cur, b0, nullptr, out);
+  if (!rc) *ssr = out[c->cur];
+  return rc;
+}
+
+int nngp_sum_squared_residuals_chains(nngp_ctx* c, int chain_mask, const double* beta0, double* ssr) {
+  return obs_chains(c, 0, chain_mask, beta0, nullptr, ssr);
 }
 
 int nngp_spmv(nngp_ctx* c, int which, const double* X, int ncols, double* Y) {

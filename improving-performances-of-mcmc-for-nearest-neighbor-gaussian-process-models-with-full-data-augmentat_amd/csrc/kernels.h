@@ -107,6 +107,8 @@ hipError_t launch_spmv_chains(hipStream_t st, const double* const* linv_dev, con
                               const FieldPtrs& f, const SweepScalars* sc, double* out, int C, int mask);
 // reduce `nblocks` x 4 partials into res[4] (deterministic order)
 hipError_t launch_reduce4(hipStream_t st, const double* partials, int nblocks, double* res);
+// dst[k] = p in stream order
+hipError_t launch_set_ptr(hipStream_t st, const double** dst, int k, const double* p);
 
 // chain `chain`: ent_val[chain] from Linv (device order) and
 // dr[s*C+chain].x = precision_diag, for chunks [0, nchunks)

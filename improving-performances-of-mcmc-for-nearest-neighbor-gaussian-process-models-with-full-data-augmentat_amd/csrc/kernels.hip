@@ -1164,6 +1164,17 @@ int tile_lds_bytes(int max_rows, int C, int NT, int K, int max_batches, int max_
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
+// dst[k] = p, in stream order (the current-factor table of captured graphs:
+// the value travels as a kernel argument, no host buffer to keep alive)
+__global__ void set_ptr_kernel(const double** dst, int k, const double* p) {
+  if (threadIdx.x == 0) dst[k] = p;
+}
+
+hipError_t launch_set_ptr(hipStream_t st, const double** dst, int k, const double* p) {
+  hipLaunchKernelGGL(set_ptr_kernel, dim3(1), dim3(64), 0, st, dst, k, p);
+  return hipGetLastError();
+}
+
 __global__ void tile_call_bump_kernel(unsigned* ctl) {
   ctl[0] += 1u;  // call id (never 0 inside a launch)
   ctl[1] = 0u;   // timeout word

@@ -80,27 +80,32 @@ def _prefault(arr: np.ndarray) -> threading.Thread:
     return th
 
 
-def _propose_factor(ctx, covfun, cp, on_chol_error):
-    """vecchia_Linv of a proposal (update_Gaussian.R:123,179).  In the
-    reference a local covariance that is not positive definite makes GpGp
+def _proposal_ok(status, on_chol_error):
+    """Outcome of a proposal's vecchia_Linv (update_Gaussian.R:123,179).  In
+    the reference a local covariance that is not positive definite makes GpGp
     raise an R error, which ends the update call (on_chol_error="error", the
     default); on_chol_error="reject" treats the proposal as rejected instead.
-    Any other failure (HIP, memory, a timeout) always propagates."""
-    try:
-        ctx.factor(1, covfun, cp)
+    Any other failure (HIP, memory, a timeout) propagates from the call."""
+    if status == 0:
         return True
-    except NNGPError as e:
-        if e.status == NNGP_ERR_CHOL and on_chol_error == "reject":
-            return False
-        raise
+    if status == NNGP_ERR_CHOL and on_chol_error != "reject":
+        raise NNGPError(NNGP_ERR_CHOL, "vecchia factor: a local covariance of the proposal is not positive definite")
+    return False
 
 
 def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_iterations_update,
                    field_thinning, ancillary, n_chromatic, iter_start, seed, on_chol_error="error", var_y=None):
     """Chain i's n_iterations_update Gibbs iterations; yields its device
-    requests -- ("anc", beta_0, dlog_scale, ok) for the ancillary proposal and
-    ("sweep", n_sweeps, beta_0, log_scale, log_noise_variance, key, counter)
-    for the chromatic sweeps -- and returns {"state", "records", "acceptance"}."""
+    requests and receives their results, so that the chains of one context
+    are served by one batched call per step (one host sync for all of them):
+      ("fac", covfun, covparms | None)        -> status of the proposal factor
+      ("anc", beta_0, dlog_scale, ok)          -> None (ancillary proposal field)
+      ("ratio", beta_0, lnv) | ("ratio", None) -> dnorm ratio
+      ("llpair", beta_0, new_ls, ls) | (..., None) -> (loglik(1), loglik(0))
+      ("sweep", n_sweeps, beta_0, log_scale, lnv, key, counter) -> None
+      ("ssr", beta_0)                          -> sum of squared residuals
+    Every chain yields every step of an iteration (None = nothing to do), so
+    the chains stay in lockstep.  Returns {"state", "records", "acceptance"}."""
     rng = np.random.default_rng(int(iter_start) + i + 1)
     key = _philox_key(iter_start, i + 1, seed)
     covfun = space_time_model["covfun"]["stationary_covfun"]
@@ -155,12 +160,13 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
             innov = rng.normal(0.0, np.exp(0.5 * tk["covariance_params_ancillary"]["logvar"]), n_shape + 1)
             new_ls = params["log_scale"] + innov[0]
             new_shape = params["shape"] + innov[1:]
-            ok = _propose_factor(ctx, covfun, covparms(sp_names, new_shape), on_chol_error)
+            st = yield ("fac", covfun, covparms(sp_names, new_shape))
+            ok = _proposal_ok(st, on_chol_error)
             # every chain stops here each iteration (ok=False: nothing to
             # propose) so the chains of one context stay in lockstep
             yield ("anc", params["beta_0"], new_ls - params["log_scale"], ok)
+            ratio = yield (("ratio", params["beta_0"], params["log_noise_variance"]) if ok else ("ratio", None))
             if ok:
-                ratio = ctx.field_response_ratio(params["beta_0"], params["log_noise_variance"])
                 if ratio > np.log(rng.uniform()):
                     params["shape"] = new_shape
                     params["log_scale"] = new_ls
@@ -179,19 +185,20 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
         # ---- sufficient covariance update (:165-213)
         innov = rng.normal(0.0, np.exp(0.5 * tk["covariance_params_sufficient"]["logvar"]), n_shape + 1)
         new_ls = params["log_scale"] + innov[0]
-        if np.exp(new_ls) < var_y:
-            new_shape = params["shape"] + innov[1:]
-            ok = _propose_factor(ctx, covfun, covparms(sp_names, new_shape), on_chol_error)
-            if ok:
-                gp_ratio = (ctx.loglik(1, params["beta_0"], new_ls)
-                            - ctx.loglik(0, params["beta_0"], params["log_scale"]))
-                if gp_ratio > np.log(rng.uniform()):
-                    params["shape"] = new_shape
-                    params["log_scale"] = new_ls
-                    ctx.accept_factor()
-                    acc_suf[it - 1] = 1
-                    if has_locs:
-                        iw = _interweave_prep(ctx, X, va)
+        propose = np.exp(new_ls) < var_y
+        new_shape = params["shape"] + innov[1:] if propose else None
+        st = yield ("fac", covfun, covparms(sp_names, new_shape) if propose else None)
+        ok = propose and _proposal_ok(st, on_chol_error)
+        lls = yield (("llpair", params["beta_0"], new_ls, params["log_scale"]) if ok else ("llpair", None))
+        if ok:
+            gp_ratio = lls[0] - lls[1]
+            if gp_ratio > np.log(rng.uniform()):
+                params["shape"] = new_shape
+                params["log_scale"] = new_ls
+                ctx.accept_factor()
+                acc_suf[it - 1] = 1
+                if has_locs:
+                    iw = _interweave_prep(ctx, X, va)
         if adapt and it % 25 == 0:
             a = acc_suf[it - 25:it].mean()
             if a < 0.05:
@@ -232,7 +239,7 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
                key, (int(iter_start) + it - 1) * n_chromatic)
 
         # ---- noise variance (:281-293)
-        ssr = ctx.sum_squared_residuals(params["beta_0"])
+        ssr = yield ("ssr", params["beta_0"])
         for _ in range(10):
             innov = rng.normal(0.0, 0.01)
             if np.exp(params["log_noise_variance"] + innov) < var_y:
@@ -247,7 +254,8 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
         rec["log_noise_variance"][it - 1] = params["log_noise_variance"]
         rec["log_scale"][it - 1] = params["log_scale"]
         rec["shape"][it - 1] = params["shape"]
-        if round(it * field_thinning) == it * field_thinning:
+        # (R's records$field[0, ] <- ... is a no-op: field_thinning = 0 records nothing)
+        if round(it * field_thinning) == it * field_thinning and it * field_thinning >= 1:
             if dev_rec:
                 ctx.record_field(int(it * field_thinning) - 1)
             else:
@@ -264,11 +272,32 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
 
 
 def _serve_one(ctx, req):
-    if req[0] == "anc":
+    """One chain's request on its own -> its result."""
+    kind = req[0]
+    if kind == "fac":
+        if req[2] is None:
+            return None
+        try:
+            ctx.factor(1, req[1], req[2])
+            return 0
+        except NNGPError as e:
+            if e.status == NNGP_ERR_CHOL:
+                return NNGP_ERR_CHOL
+            raise
+    if kind == "anc":
         if req[3]:
             ctx.ancillary_propose(req[1], req[2])
-    else:
-        ctx.sweep(*req[1:])
+        return None
+    if kind == "ratio":
+        return None if req[1] is None else ctx.field_response_ratio(req[1], req[2])
+    if kind == "llpair":
+        if req[1] is None:
+            return None
+        return ctx.loglik(1, req[1], req[2]), ctx.loglik(0, req[1], req[3])
+    if kind == "ssr":
+        return ctx.sum_squared_residuals(req[1])
+    ctx.sweep(*req[1:])
+    return None
 
 
 def _run_chain(i, state, ctx, X, observed_field, space_time_model, va, n_iterations_update,
@@ -279,15 +308,15 @@ def _run_chain(i, state, ctx, X, observed_field, space_time_model, va, n_iterati
     try:
         req = next(prog)
         while True:
-            _serve_one(ctx, req)
-            req = next(prog)
+            req = prog.send(_serve_one(ctx, req))
     except StopIteration as stop:
         return stop.value
 
 
-def _serve_group(owner, ids, reqs, contexts):
+def _serve_group(owner, ids, reqs, contexts, out):
     """Serve the same-kind requests of the chains `ids` of one ChainContext
-    with one batched call; False if they cannot be batched."""
+    with one batched call (results into out[i]); False if they cannot be
+    batched."""
     if owner is None or owner.n_chains < 2:
         return False
     kinds = {reqs[i][0] for i in ids}
@@ -295,6 +324,45 @@ def _serve_group(owner, ids, reqs, contexts):
         return False
     kind = kinds.pop()
     k = owner.n_chains
+    live = [i for i in ids if reqs[i][-1] is not None] if kind in ("fac", "ratio", "llpair") else list(ids)
+    mask = 0
+    for i in live:
+        mask |= 1 << contexts[i].chain
+    for i in ids:
+        out[i] = None
+    if kind == "fac":
+        if not live:
+            return True
+        covfuns = {reqs[i][1] for i in live}
+        if len(covfuns) != 1:
+            return False
+        ncp = len(reqs[live[0]][2])
+        cps = np.zeros((k, ncp))
+        for i in live:
+            cps[contexts[i].chain] = reqs[i][2]
+        st = owner.factor_chains(1, mask, covfuns.pop(), cps)
+        for i in live:
+            out[i] = int(st[contexts[i].chain])
+        return True
+    if kind in ("ratio", "llpair", "ssr"):
+        if not live:
+            return True
+        cols = [np.zeros(k) for _ in range(3)]
+        for i in live:
+            for q, v in enumerate(reqs[i][1:]):
+                cols[q][contexts[i].chain] = v
+        if kind == "ratio":
+            r = owner.field_response_ratio_chains(mask, cols[0], cols[1])
+            res = {i: float(r[contexts[i].chain]) for i in live}
+        elif kind == "ssr":
+            r = owner.sum_squared_residuals_chains(mask, cols[0])
+            res = {i: float(r[contexts[i].chain]) for i in live}
+        else:
+            l1 = owner.loglik_chains(1, mask, cols[0], cols[1])
+            l0 = owner.loglik_chains(0, mask, cols[0], cols[2])
+            res = {i: (float(l1[contexts[i].chain]), float(l0[contexts[i].chain])) for i in live}
+        out.update(res)
+        return True
     if kind == "anc":
         mask, b0, dls = 0, np.zeros(k), np.zeros(k)
         for i in ids:
@@ -330,15 +398,16 @@ def _drive(programs, contexts):
         for i in reqs:
             owner = getattr(contexts[i], "ctx", None)
             groups.setdefault(id(owner) if owner is not None else ("solo", i), []).append(i)
+        served = {}
         for ids in groups.values():
             owner = getattr(contexts[ids[0]], "ctx", None)
-            if not _serve_group(owner, ids, reqs, contexts):
+            if not _serve_group(owner, ids, reqs, contexts, served):
                 for i in ids:
-                    _serve_one(contexts[i], reqs[i])
+                    served[i] = _serve_one(contexts[i], reqs[i])
         nxt = {}
         for i in reqs:
             try:
-                nxt[i] = programs[i].send(None)
+                nxt[i] = programs[i].send(served.get(i))
             except StopIteration as stop:
                 results[i] = stop.value
         reqs = nxt

@@ -200,6 +200,19 @@ int nngp_accept_field(nngp_ctx* ctx);
 int nngp_beta0_stats(nngp_ctx* ctx, double* ones_Q_ones, double* ones_Q_field);
 /* sum (y - field[loc] - mu + beta0)^2 (update_Gaussian.R:281) */
 int nngp_sum_squared_residuals(nngp_ctx* ctx, double beta0, double* ssr);
+/* Batched forms for the chains in chain_mask (bit k = chain k), one host
+ * synchronisation per call: parameter and result arrays have n_chains
+ * entries (entries of other chains ignored).  factor_chains: covparms is
+ * n_chains x ncovparms (row k = chain k); status[k] = NNGP_OK or
+ * NNGP_ERR_CHOL per chain (the call itself returns NNGP_OK then).  Each
+ * chain's result is bitwise the single-chain entry point's. */
+int nngp_factor_chains(nngp_ctx* ctx, int which, int chain_mask, int covfun, const double* covparms,
+                       int ncovparms, int* status);
+int nngp_loglik_chains(nngp_ctx* ctx, int which, int chain_mask, const double* beta0,
+                       const double* log_scale, double* ll);
+int nngp_field_response_ratio_chains(nngp_ctx* ctx, int chain_mask, const double* beta0,
+                                     const double* log_noise_variance, double* ratio);
+int nngp_sum_squared_residuals_chains(nngp_ctx* ctx, int chain_mask, const double* beta0, double* ssr);
 /* Y = B X for X n x ncols column-major (host buffers) */
 int nngp_spmv(nngp_ctx* ctx, int which, const double* X, int ncols, double* Y);
 /* x = B^{-1} u (host buffers, length n) */

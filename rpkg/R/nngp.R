@@ -93,6 +93,16 @@ nngp_device_normals <- function(device, seed, sweep, n)
 
 nngp_shard_unique_id <- function() .Call(C_nngp_shard_unique_id)
 nngp_shard_comm_init <- function(ctx, id) invisible(.Call(C_nngp_shard_comm_init, ctx, id))
+nngp_factor_chains <- function(ctx, which, chain_mask, covfun, covparms)
+  .Call(C_nngp_factor_chains, ctx, as.integer(which), as.integer(chain_mask), nngp_covfun_id(covfun),
+        as.matrix(covparms) + 0)
+nngp_loglik_chains <- function(ctx, which, chain_mask, beta_0, log_scale)
+  .Call(C_nngp_loglik_chains, ctx, as.integer(which), as.integer(chain_mask), as.double(beta_0), as.double(log_scale))
+nngp_field_response_ratio_chains <- function(ctx, chain_mask, beta_0, log_noise_variance)
+  .Call(C_nngp_field_response_ratio_chains, ctx, as.integer(chain_mask), as.double(beta_0),
+        as.double(log_noise_variance))
+nngp_sum_squared_residuals_chains <- function(ctx, chain_mask, beta_0)
+  .Call(C_nngp_sum_squared_residuals_chains, ctx, as.integer(chain_mask), as.double(beta_0))
 nngp_shard_ipc_handle <- function(ctx) .Call(C_nngp_shard_ipc_handle, ctx)
 nngp_shard_ipc_open <- function(ctx, handles) invisible(.Call(C_nngp_shard_ipc_open, ctx, handles))
 nngp_sweep_chains_group <- function(ctxs, n_sweeps, beta_0, log_scale, log_noise_variance, seed, counter_base)

@@ -408,6 +408,59 @@ SEXP C_nngp_shard_ipc_open(SEXP p, SEXP handles) {
   return R_NilValue;
 }
 
+/* ---------- batched per-chain forms (one host sync for all chains) ---------- */
+SEXP C_nngp_factor_chains(SEXP p, SEXP which, SEXP mask, SEXP covfun, SEXP covparms) {
+  nngp_ctx* c = get_ctx(p);
+  nngp_info inf;
+  check(nngp_ctx_info(c, &inf), c);
+  /* covparms: n_chains x ncovparms matrix (row k = chain k), column-major in R */
+  const int k = inf.n_chains, ncp = Rf_ncols(covparms);
+  if (Rf_nrows(covparms) != k) Rf_error("nngp: covparms needs one row per chain");
+  double rm[4 * 16];
+  if (ncp > 16) Rf_error("nngp: at most 16 covariance parameters");
+  for (int i = 0; i < k; ++i)
+    for (int j = 0; j < ncp; ++j) rm[i * ncp + j] = REAL(covparms)[i + (size_t)j * k];
+  SEXP st = PROTECT(Rf_allocVector(INTSXP, k));
+  for (int i = 0; i < k; ++i) INTEGER(st)[i] = 0;
+  const int rc = nngp_factor_chains(c, as_int(which), as_int(mask), as_int(covfun), rm, ncp, INTEGER(st));
+  UNPROTECT(1);
+  check(rc, c);
+  return st;
+}
+
+static SEXP chains_out(nngp_ctx* c) {
+  nngp_info inf;
+  check(nngp_ctx_info(c, &inf), c);
+  return Rf_allocVector(REALSXP, inf.n_chains);
+}
+
+SEXP C_nngp_loglik_chains(SEXP p, SEXP which, SEXP mask, SEXP beta0, SEXP log_scale) {
+  nngp_ctx* c = get_ctx(p);
+  SEXP out = PROTECT(chains_out(c));
+  const int rc = nngp_loglik_chains(c, as_int(which), as_int(mask), REAL(beta0), REAL(log_scale), REAL(out));
+  UNPROTECT(1);
+  check(rc, c);
+  return out;
+}
+
+SEXP C_nngp_field_response_ratio_chains(SEXP p, SEXP mask, SEXP beta0, SEXP lnv) {
+  nngp_ctx* c = get_ctx(p);
+  SEXP out = PROTECT(chains_out(c));
+  const int rc = nngp_field_response_ratio_chains(c, as_int(mask), REAL(beta0), REAL(lnv), REAL(out));
+  UNPROTECT(1);
+  check(rc, c);
+  return out;
+}
+
+SEXP C_nngp_sum_squared_residuals_chains(SEXP p, SEXP mask, SEXP beta0) {
+  nngp_ctx* c = get_ctx(p);
+  SEXP out = PROTECT(chains_out(c));
+  const int rc = nngp_sum_squared_residuals_chains(c, as_int(mask), REAL(beta0), REAL(out));
+  UNPROTECT(1);
+  check(rc, c);
+  return out;
+}
+
 /* ---------- registration ---------- */
 #define E(name, n) {#name, (DL_FUNC)&name, n}
 static const R_CallMethodDef call_methods[] = {
@@ -451,6 +504,10 @@ static const R_CallMethodDef call_methods[] = {
     E(C_nngp_sweep_chains_group, 7),
     E(C_nngp_shard_ipc_handle, 1),
     E(C_nngp_shard_ipc_open, 2),
+    E(C_nngp_factor_chains, 5),
+    E(C_nngp_loglik_chains, 5),
+    E(C_nngp_field_response_ratio_chains, 4),
+    E(C_nngp_sum_squared_residuals_chains, 3),
     {NULL, NULL, 0}};
 #undef E
 

@@ -315,6 +315,24 @@ class _FailingCtx:
     def get_field(self):
         return np.zeros(4)
 
+    def sweep(self, *a):
+        pass
+
+
+def _drive_one(g, ctx):
+    """Run a chain program against one context (update_gaussian._run_chain's
+    loop): -> the request kinds it issued, in order."""
+    from nngp_amd.update_gaussian import _serve_one
+
+    kinds = []
+    try:
+        req = next(g)
+        while True:
+            kinds.append((req[0], req[-1] is not None if req[0] != "anc" else req[3]))
+            req = g.send(_serve_one(ctx, req))
+    except StopIteration:
+        return kinds
+
 
 def _program(ctx, on_chol_error):
     from nngp_amd.update_gaussian import _chain_program
@@ -337,15 +355,16 @@ def test_mh_proposal_factor_failures(P):
     (here a HIP error) propagates in both modes."""
     from nngp_amd._lib import NNGP_ERR_CHOL, NNGP_ERR_HIP, NNGPError
 
-    with pytest.raises(NNGPError):
-        next(_program(_FailingCtx(NNGP_ERR_CHOL), "error"))
-    g = _program(_FailingCtx(NNGP_ERR_CHOL), "reject")
-    req = next(g)
-    assert req[0] == "anc" and req[3] is False      # ancillary proposal rejected
-    assert g.send(None)[0] == "sweep"               # sufficient proposal rejected too, the iteration goes on
+    with pytest.raises(NNGPError) as e:
+        _drive_one(_program(_FailingCtx(NNGP_ERR_CHOL), "error"), _FailingCtx(NNGP_ERR_CHOL))
+    assert e.value.status == NNGP_ERR_CHOL
+    kinds = _drive_one(_program(_FailingCtx(NNGP_ERR_CHOL), "reject"), _FailingCtx(NNGP_ERR_CHOL))
+    # both proposals rejected (no ratio, no log-likelihoods), the iteration goes on
+    assert kinds == [("fac", True), ("anc", False), ("ratio", False), ("fac", True), ("llpair", False),
+                     ("sweep", True), ("ssr", True)], kinds
     for mode in ("error", "reject"):
         with pytest.raises(NNGPError) as e:
-            next(_program(_FailingCtx(NNGP_ERR_HIP), mode))
+            _drive_one(_program(_FailingCtx(NNGP_ERR_HIP), mode), _FailingCtx(NNGP_ERR_HIP))
         assert e.value.status == NNGP_ERR_HIP
 
 
