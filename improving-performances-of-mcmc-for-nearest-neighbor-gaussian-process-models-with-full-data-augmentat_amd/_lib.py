@@ -60,7 +60,8 @@ class Info(C.Structure):
                 ("n_ghost_cells", C.c_longlong), ("n_ranks", C.c_int), ("rank", C.c_int),
                 ("shard_owned", C.c_longlong), ("shard_needed_rows", C.c_longlong),
                 ("shard_exchange_slots", C.c_longlong), ("tile_ghost_pass", C.c_int),
-                ("tile_ghost_cells_max", C.c_int), ("tile_r_global", C.c_int)]
+                ("tile_ghost_cells_max", C.c_int), ("tile_r_global", C.c_int),
+                ("tile_chain_split", C.c_int)]
 
 
 _dp = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")

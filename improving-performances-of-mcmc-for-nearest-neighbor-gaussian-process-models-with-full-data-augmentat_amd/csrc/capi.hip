@@ -127,6 +127,7 @@ struct nngp_ctx {
   int* erow_d = nullptr;
   double* dwx_d = nullptr;        // n x C granules of 16 B
   bool rglobal = false;           // tiles keep r in global memory (rg_d) instead of LDS
+  bool tcs = false;               // chain-split tile launches (one chain per workgroup, kernels.hip sweep_tiles_cs_kernel)
   double* rg_d = nullptr;         // sum of the tiles' local rows x C
   unsigned* ctl_d = nullptr;      // [0] call id, [1] timeout word
   unsigned* tmo_h = nullptr;      // pinned copy of the timeout word after each launch
@@ -491,6 +492,17 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       T = std::max(G, T / G * G);  // a multiple of the ranks
       std::string terr;
       int NT = kTileNT;
+      // NNGP_TILE_CHAINS=split (2-4 chains, one GPU): one workgroup per
+      // (chain, tile), 256-thread tiles, the chains' workgroups of a tile
+      // interleaved on its CU (kernels.hip sweep_tiles_cs_kernel)
+      const char* tch = std::getenv("NNGP_TILE_CHAINS");
+      const std::string tcs = tch ? tch : "";
+      if (tcs != "" && tcs != "split" && tcs != "joint") {
+        delete c;
+        return fail_msg(nullptr, NNGP_ERR_ARG, "NNGP_TILE_CHAINS must be split or joint");
+      }
+      const bool csplit = tcs == "split" && shard_G == 0 && n_chains >= 2;
+      if (csplit) NT = 256;
       if (const char* te = std::getenv("NNGP_TILE_NT")) NT = std::atoi(te);
       if (NT != 256 && NT != 512 && NT != 1024) {
         delete c;
@@ -501,16 +513,28 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       // launch at the headline (two batches per colour, and the next colour's
       // stream no longer overlaps the hand-off with one register set)
       const char* tsp = std::getenv("NNGP_TILE_SPLIT");
-      const bool split = tile_double_buffer(n_chains, NT) == 0 && tsp && std::string(tsp) == "1";
+      const bool split = !csplit && tile_double_buffer(n_chains, NT) == 0 && tsp && std::string(tsp) == "1";
       // a tile's own rows alone beyond the LDS: no layout to build (n = 8e6 on
       // one GPU would spend ~30 s building one that cannot run)
       const bool rg_forced = std::getenv("NNGP_TILE_R") && std::string(std::getenv("NNGP_TILE_R")) == "global";
       const bool hopeless = !rg_forced && (long long)(n / std::max(T, 1)) * n_chains * 8 > (long long)lds_max;
       if (hopeless) terr = "tile layout: a tile's own rows exceed the LDS";
       bool ok = cus > 0 && T <= n && !hopeless &&
-                build_tile_layout(nn.data(), n, b, coloring, locs, d, T, NT, tile_rmax(n_chains, NT), c->tl, terr, G,
+                build_tile_layout(nn.data(), n, b, coloring, locs, d, T, NT,
+                                  csplit ? tile_rmax_cs(NT) : tile_rmax(n_chains, NT), c->tl, terr, G,
                                   split);
-      const int need = ok ? tile_lds_bytes(c->tl.max_rows, n_chains, NT, c->tl.K, c->tl.max_batches, c->tl.max_gslots) : 0;
+      if (ok && csplit) {
+        // n_chains workgroups of one chain per CU
+        const int need1 = tile_lds_bytes(c->tl.max_rows, 1, NT, c->tl.K, c->tl.max_batches, c->tl.max_gslots);
+        if (NT != 256 || (long long)need1 * n_chains > lds_max) {
+          ok = false;
+          terr = "chain-split tiles need 256 threads and " + std::to_string(need1) + " B of LDS per chain x " +
+                 std::to_string(n_chains) + " chains per CU (device: " + std::to_string(lds_max) + ")";
+        } else {
+          c->tcs = true;
+        }
+      }
+      const int need = ok && !csplit ? tile_lds_bytes(c->tl.max_rows, n_chains, NT, c->tl.K, c->tl.max_batches, c->tl.max_gslots) : 0;
       // NNGP_TILE_R=global: the tiles' r in global memory (kernels.hip RG),
       // one GPU, for layouts beyond the LDS.  Opt-in: at n = 1e7, m = 20 (one
       // chain) it measured 362 chain-sweeps/s (26.4 ms per 10-sweep launch,
@@ -899,6 +923,7 @@ int nngp_ctx_info(const nngp_ctx* c, nngp_info* info) {
   info->tile_ghost_pass = c->engine == 1 ? c->tl.NT * tile_gmax(c->tl.NT) : 0;
   info->tile_ghost_cells_max = 0;
   info->tile_r_global = c->rglobal ? 1 : 0;
+  info->tile_chain_split = c->tcs ? 1 : 0;
   if (c->engine == 1)
     for (size_t i = 0; i + 1 < c->tl.gptr.size(); ++i)
       info->tile_ghost_cells_max = std::max(info->tile_ghost_cells_max, c->tl.gptr[i + 1] - c->tl.gptr[i]);
@@ -1304,8 +1329,13 @@ static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, int mask, const double*
     a.n_sweeps = n_sweeps;
     a.chain_mask = mask;
     a.z_in = z_dev;
-    HIPCHK(c, launch_sweep_tiles(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NT, c->tl.max_batches,
-                                  c->tl.max_gslots));
+    if (c->tcs) {
+      HIPCHK(c, launch_sweep_tiles_cs(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NT, c->tl.max_batches,
+                                      c->tl.max_gslots));
+    } else {
+      HIPCHK(c, launch_sweep_tiles(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NT, c->tl.max_batches,
+                                    c->tl.max_gslots));
+    }
     HIPCHK(c, hipMemcpyAsync(c->tmo_h, c->ctl_d + 1, sizeof(unsigned), hipMemcpyDeviceToHost, c->st));
   }
   if ((parts & kColours) && c->engine == 0) {

@@ -185,6 +185,9 @@ int tile_lds_bytes(int max_rows, int C, int NT, int K, int max_batches, int max_
 // buffered: 7.7k vs 10.7k chain-sweeps/s -- the own work needs the waves)
 constexpr int tile_double_buffer(int C, int NT) { return C <= 2 ? 1 : 0; }
 constexpr int tile_rmax(int C, int NT) { return 4096 / NT; }
+// chain-split launches (one chain per workgroup, 3 waves per SIMD): 2048-cell
+// batches keep the kernel within its 168 registers
+constexpr int tile_rmax_cs(int NT) { return 2048 / NT; }
 // ghost-cell registers per thread: NT * GMAX ghost cells of a (tile, colour) per pass
 constexpr int tile_gmax(int NT) { return NT == 256 ? 4 : (NT == 512 ? 3 : 1); }
 // Tile-sharded sweep: the T tiles of the layout are split
@@ -202,6 +205,10 @@ struct TileShard {
 };
 hipError_t launch_sweep_tiles(hipStream_t st, const TileDev& D, const TileLaunch& a, int max_rows, int NT,
                               int max_batches, int max_gslots, const TileShard* sh = nullptr, int grid = 0);
+// chain-split launch: D.C one-chain workgroups per tile (256-thread layouts,
+// one GPU), the chains' phases interleaved on each CU
+hipError_t launch_sweep_tiles_cs(hipStream_t st, const TileDev& D, const TileLaunch& a, int max_rows, int NT,
+                                 int max_batches, int max_gslots);
 // ctl[0] += 1 (call id), ctl[1] = 0 (timeout word): before every launch of a rank
 hipError_t launch_tile_call_bump(hipStream_t st, unsigned* ctl);
 // tile shard, w exchange by peer copies instead of RCCL: signal the peers

@@ -1155,6 +1155,7 @@ constexpr uint32_t kTStart = 1u << 30, kTEnd = 1u << 31;
 constexpr int kTExported = 1 << 30;
 constexpr int kTSlots = 256;       // slots per own batch (graph_prep.h kTileSlotsMax)
 constexpr int kTSpreadLds = 82 * 1024;  // LDS floor: at most one tile per CU
+constexpr int kTCuLds = 160 * 1024;     // LDS per CU
 
 int tile_lds_bytes(int max_rows, int C, int NT, int K, int max_batches, int max_gslots) {
   const int rbytes = ((max_rows * C * 8 + 15) / 16) * 16;
@@ -1262,8 +1263,22 @@ struct TileBatchRegs {
   double w[IMAX], zs[IMAX];   // w; prepped: z / sqrt(P)
 };
 
+// index of item u (= slot-in-batch q x C + chain) of the batch at slot x0 in
+// the per-slot x chain arrays (dr, w_slot, granules).  CS = their chain
+// stride: C, or (chain-split launches: one chain per workgroup, C = 1) the
+// context's chain count, the chain's offset folded into the pointers
+template <int C, int CS>
+__device__ __forceinline__ size_t tile_xu(int x0, int u) {
+  if constexpr (CS == C) {
+    return (size_t)x0 * C + u;
+  } else {
+    const int q = u / C;
+    return (size_t)(x0 + q) * CS + (u - q * C);
+  }
+}
+
 // the batch's per-slot records (the draw preparation waits for them)
-template <int C, int NT, int RMAX, int SH>
+template <int C, int NT, int RMAX, int SH, int CS = C>
 __device__ __forceinline__ void tile_load_items(const TileDev& D, const int4 B, TileBatchRegs<C, NT, RMAX>& b, int t) {
   b.ns = B.z; b.x0 = B.w;
 #pragma unroll
@@ -1271,7 +1286,7 @@ __device__ __forceinline__ void tile_load_items(const TileDev& D, const int4 B, 
     const int u = t + k * NT;
     if (u < b.ns * C) {
       const int q = u / C;
-      const size_t xu = (size_t)b.x0 * C + u;  // = (x0 + q) * C + chain
+      const size_t xu = tile_xu<C, CS>(b.x0, u);  // = (x0 + q) * CS + chain
       const int2 si = D.sinfo[b.x0 + q];
       b.nobs[k] = si.x;
       b.flag[k] = si.y;
@@ -1303,16 +1318,16 @@ __device__ __forceinline__ void tile_load_cells(const TileDev& D, const int4 B, 
   }
 }
 
-template <int C, int NT, int RMAX, int SH>
+template <int C, int NT, int RMAX, int SH, int CS = C>
 __device__ __forceinline__ void tile_load_batch(const TileDev& D, const int4 B, TileBatchRegs<C, NT, RMAX>& b, int t) {
-  tile_load_items<C, NT, RMAX, SH>(D, B, b, t);
+  tile_load_items<C, NT, RMAX, SH, CS>(D, B, b, t);
   tile_load_cells<C, NT, RMAX>(D, B, b, t);
 }
 
 // everything of the Gibbs draw but acc: P = D/s2 + n/t2, w' = (cR - acc/s2)/P
 // + z/sqrt(P) with cR = R/t2 + D w/s2 (w of an own slot is constant until its
 // colour, so this runs a colour ahead, during the previous hand-off)
-template <int C, int NT, int RMAX>
+template <int C, int NT, int RMAX, int CS = C>
 __device__ __forceinline__ void tile_prep_items(const TileDev& D, const TileLaunch& a, const double* sc_s,
                                                 const unsigned long long* seed_s, int s,
                                                 TileBatchRegs<C, NT, RMAX>& b, int t) {
@@ -1323,7 +1338,7 @@ __device__ __forceinline__ void tile_prep_items(const TileDev& D, const TileLaun
       const int q = u / C, ch = u - q * C;
       const double inv_s2 = sc_s[2 * ch], inv_t2 = sc_s[2 * ch + 1];
       double z = 0.0;
-      if (a.z_in) z = a.z_in[((size_t)s * D.n + b.x0 + q) * C + ch];
+      if (a.z_in) z = a.z_in[((size_t)s * D.n + b.x0 + q) * CS + ch];
       else z = normal_loc(seed_s[2 * ch], seed_s[2 * ch + 1] + s, (uint32_t)b.loc[k]);
       const double P = b.a0[k] * inv_s2 + (double)b.nobs[k] * inv_t2;
       const double cR = inv_t2 * b.a1[k] + inv_s2 * (b.a0[k] * b.w[k]);
@@ -1419,7 +1434,7 @@ __device__ __forceinline__ void seg_scan_step(double (&v)[C], int& f) {
 // one own batch of colour c (epoch): products -> slot totals -> draws ->
 // scatter.  LDS and registers only, plus the draws' stores: no global load
 // (a load here would wait behind the next batch's prefetch, vmcnt is in order)
-template <int C, int NT, int RMAX, int PROBE, int SH>
+template <int C, int NT, int RMAX, int PROBE, int SH, int CS = C>
 __device__ __forceinline__ void tile_own_draw(const TileDev& D, const TileLaunch& a, const TileShard& sh, TileState& S,
                                               TileBatchRegs<C, NT, RMAX>& b, unsigned epoch) {
   constexpr int IMAX = TileBatchRegs<C, NT, RMAX>::IMAX;
@@ -1504,7 +1519,7 @@ __device__ __forceinline__ void tile_own_draw(const TileDev& D, const TileLaunch
     if (u < nit) {
       const int ch = u % C;
       double dw = 0.0;
-      const size_t xu = (size_t)b.x0 * C + u;
+      const size_t xu = tile_xu<C, CS>(b.x0, u);
       if ((a.chain_mask >> ch) & 1) {
         const double wn = (b.a0[k] - S.sc_s[2 * ch] * acc_s[u]) * b.a1[k] + b.zs[k];
         dw = wn - b.w[k];
@@ -1563,7 +1578,7 @@ __device__ __forceinline__ void tile_own_scatter(TileState& S, const TileBatchRe
 // the normals pregenerated by a separate kernel -- no Philox here,
 // 132 instead of 255 VGPRs at 1 chain --, double buffering at 3 chains, an L2
 // prefetch of the next stream during the own work, other load orders.)
-template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE, int SH>
+template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE, int SH, int CS = C>
 __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a, const TileShard& sh, TileState& S, int ph,
                                            TileBatchRegs<C, NT, RMAX>& cur, TileBatchRegs<C, NT, RMAX>& nxt,
                                            TileGhostRegs<C, GMAX>& gr, TileGhostRegs<C, GMAX>& grn) {
@@ -1586,7 +1601,7 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
   if (DB) {
     // the next colour's first batch (and ghost chunk): their HBM stream
     // overlaps this colour's work (two register sets)
-    if (more) tile_load_batch<C, NT, RMAX, SH>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
+    if (more) tile_load_batch<C, NT, RMAX, SH, CS>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
     if (has_next && gn1 > gn0) tile_load_ghosts<C, NT, GMAX>(D, gn0, gn1, grn, t);
   }
   // ---- 1. own batches.  One register set (!DB): after the draw of the last
@@ -1599,15 +1614,15 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
   for (int bi = bfirst; bi < bend; ++bi) {
     if (bi != bfirst) {  // rare: a colour with more than one batch in this tile
       __syncthreads();   // acc_s is indexed by slot-in-batch: every wave is done with the last batch
-      tile_load_batch<C, NT, RMAX, SH>(D, S.batch_s[bi], cur, t);
-      tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, s, cur, t);
+      tile_load_batch<C, NT, RMAX, SH, CS>(D, S.batch_s[bi], cur, t);
+      tile_prep_items<C, NT, RMAX, CS>(D, a, S.sc_s, S.seed_s, s, cur, t);
     }
-    tile_own_draw<C, NT, RMAX, PROBE, SH>(D, a, sh, S, cur, epoch);
+    tile_own_draw<C, NT, RMAX, PROBE, SH, CS>(D, a, sh, S, cur, epoch);
     const int R = cur.R;
     if (!DB && bi + 1 == bend) {
-      if (more) tile_load_items<C, NT, RMAX, SH>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
+      if (more) tile_load_items<C, NT, RMAX, SH, CS>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
       if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
-      if (pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * C + t % C) * 16), 0, SH ? kGranAuxSys : kGranAux);
+      if (pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * CS + t % C) * 16), 0, SH ? kGranAuxSys : kGranAux);
     }
     tile_own_scatter<C, NT, RMAX, PROBE>(S, cur, R);
   }
@@ -1616,14 +1631,14 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
   // draw scalars, then (two register sets) the first poll
   if (!DB) {
     if (bend == bfirst) {  // no own batch of this colour in the tile
-      if (more) tile_load_items<C, NT, RMAX, SH>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
+      if (more) tile_load_items<C, NT, RMAX, SH, CS>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
       if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
-      if (pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * C + t % C) * 16), 0, SH ? kGranAuxSys : kGranAux);
+      if (pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * CS + t % C) * 16), 0, SH ? kGranAuxSys : kGranAux);
     }
     if (more) tile_load_cells<C, NT, RMAX>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
   }
-  if (more) tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, sn, nxt, t);
-  if (DB && pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * C + t % C) * 16), 0, SH ? kGranAuxSys : kGranAux);
+  if (more) tile_prep_items<C, NT, RMAX, CS>(D, a, S.sc_s, S.seed_s, sn, nxt, t);
+  if (DB && pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * CS + t % C) * 16), 0, SH ? kGranAuxSys : kGranAux);
   TSTAMP(S, 5);
   TLSTAMP(S, 4);
   // ---- 3. hand-off: the granule of each (foreign slot, chain) of this colour
@@ -1635,7 +1650,7 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
     if (u < nfi) {
       const int x = u0 == 0 ? gsl_pref : D.gslot[gs0 + u / C];
       const int ch = u % C;
-      const int off = (int)(((size_t)x * C + ch) * 16);
+      const int off = (int)(((size_t)x * CS + ch) * 16);
       u32x4_t g = u0 == 0 ? gfirst : __builtin_amdgcn_raw_buffer_load_b128(S.gran, off, 0, SH ? kGranAuxSys : kGranAux);
       double dw = 0.0;
       for (unsigned spins = 0;; ++spins) {
@@ -1814,15 +1829,36 @@ __device__ __forceinline__ void tile_phase_ib(const TileDev& D, const TileLaunch
 // LDS (n = 1e7 on one GPU).  A row takes at most one update per colour (one
 // member per colour), so the scatter and the ghost adds stay plain
 // read-modify-writes; the phase barriers order them for the workgroup.
-template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE, int SH, int RG, int IB>
-__global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D0, TileLaunch a, TileShard sh) {
+// CS: chain stride of the per-slot arrays.  CS == C: the workgroup runs every
+// chain of the context (one workgroup per tile).  CS > C = 1 (chain-split,
+// sweep_tiles_cs_kernel): workgroup b runs chain b / T of tile b % T -- the
+// chains are independent Markov chains, so the CS workgroups of a tile share
+// its CU and each one's stream and hand-off waits overlap the others' work.
+// Chain-major numbering: the dispatcher places chain 0's tiles first, so a
+// chain never waits on a tile of its own that is not resident.
+template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE, int SH, int RG, int IB, int CS>
+__device__ __forceinline__ void sweep_tiles_body(const TileDev& D0, TileLaunch a, const TileShard& sh) {
   using BR = TileBatchRegs<C, NT, RMAX>;
   constexpr int NW = NT / 64;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   // tile shard: global tile index, its rank, that rank's buffers
-  const int Tg = SH ? sh.tile0 + (int)blockIdx.x : (int)blockIdx.x;
+  int Tg = SH ? sh.tile0 + (int)blockIdx.x : (int)blockIdx.x;
   const int rk = SH ? Tg / sh.Tl : 0;
-  const TileDev D = SH ? sh.devs[rk - sh.rank0] : D0;
+  TileDev D = SH ? sh.devs[rk - sh.rank0] : D0;
+  if constexpr (CS != C) {
+    static_assert(C == 1 && !SH && !RG && !IB && !PROBE, "chain-split: one chain per workgroup, single GPU");
+    const int ch0 = Tg / D.T;
+    Tg -= ch0 * D.T;
+    D.cell_val += (size_t)ch0 * D.n_cells;
+    D.gval += (size_t)ch0 * D.n_gcells;
+    D.dr += ch0;
+    D.w_slot += ch0;
+    D.dwx += 2 * ch0;  // 16-B granules
+    D.r += ch0;
+    D.scal += ch0;
+    a.chain_mask >>= ch0;
+    if (a.z_in) a.z_in += ch0;
+  }
   TileState S;
   S.G = SH ? sh.G : 1;
   S.T = Tg; S.t = threadIdx.x; S.lane = S.t & 63; S.wv = S.t >> 6; S.K = D.K;
@@ -1849,7 +1885,7 @@ __global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D0, TileLaunch 
   if (PROBE == 2 && t == 0) *S.spin_s = 0;
   TSTAMP(S, -1);
   for (int lr = t; lr < nrows; lr += NT) {
-    const size_t g = (size_t)D.erow[row0 + lr] * C;
+    const size_t g = (size_t)D.erow[row0 + lr] * CS;
 #pragma unroll
     for (int ch = 0; ch < C; ++ch) S.r_s[lr * C + ch] = D.r[g + ch];
   }
@@ -1874,26 +1910,39 @@ __global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D0, TileLaunch 
   BR A, B;  // batch register sets: the current colour's and (DB) the next one's
   TileGhostRegs<C, GMAX> GA, GB;
   if (S.nph > 0 && S.bptr_s[0] < S.bptr_s[1]) {
-    tile_load_batch<C, NT, RMAX, SH>(D, S.batch_s[S.bptr_s[0]], A, t);
-    tile_prep_items<C, NT, RMAX>(D, a, S.sc_s, S.seed_s, 0, A, t);
+    tile_load_batch<C, NT, RMAX, SH, CS>(D, S.batch_s[S.bptr_s[0]], A, t);
+    tile_prep_items<C, NT, RMAX, CS>(D, a, S.sc_s, S.seed_s, 0, A, t);
   }
   if (DB && S.nph > 0 && S.gptr_s[0] < S.gptr_s[1]) tile_load_ghosts<C, NT, GMAX>(D, S.gptr_s[0], S.gptr_s[1], GA, t);
   __syncthreads();
   TSTAMP(S, 7);
   if (DB) {
     for (int ph = 0; ph < S.nph; ph += 2) {
-      tile_phase<C, NT, RMAX, GMAX, DB, PROBE, SH>(D, a, sh, S, ph, A, B, GA, GB);
-      if (ph + 1 < S.nph) tile_phase<C, NT, RMAX, GMAX, DB, PROBE, SH>(D, a, sh, S, ph + 1, B, A, GB, GA);
+      tile_phase<C, NT, RMAX, GMAX, DB, PROBE, SH, CS>(D, a, sh, S, ph, A, B, GA, GB);
+      if (ph + 1 < S.nph) tile_phase<C, NT, RMAX, GMAX, DB, PROBE, SH, CS>(D, a, sh, S, ph + 1, B, A, GB, GA);
     }
   } else if (IB) {
     for (int ph = 0; ph < S.nph; ++ph) tile_phase_ib<C, NT, RMAX, GMAX, PROBE, SH>(D, a, sh, S, ph, A, GA);
   } else {
-    for (int ph = 0; ph < S.nph; ++ph) tile_phase<C, NT, RMAX, GMAX, DB, PROBE, SH>(D, a, sh, S, ph, A, A, GA, GA);
+    for (int ph = 0; ph < S.nph; ++ph) tile_phase<C, NT, RMAX, GMAX, DB, PROBE, SH, CS>(D, a, sh, S, ph, A, A, GA, GA);
   }
   if (PROBE == 1 && t == 0) {
     unsigned long long* o = D.dbg + (size_t)T * 8;
     for (int k = 0; k < 8; ++k) o[k] = S.tp[k];
   }
+}
+
+template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE, int SH, int RG, int IB>
+__global__ __launch_bounds__(NT) void sweep_tiles_kernel(TileDev D0, TileLaunch a, TileShard sh) {
+  sweep_tiles_body<C, NT, RMAX, GMAX, DB, PROBE, SH, RG, IB, C>(D0, a, sh);
+}
+
+// chain-split: CS one-chain workgroups per tile, CS per CU (CS waves of
+// NT / 64 per SIMD: the register budget of that occupancy)
+template <int CS, int NT, int RMAX, int GMAX>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(CS * NT / 256, CS * NT / 256)))
+void sweep_tiles_cs_kernel(TileDev D0, TileLaunch a) {
+  sweep_tiles_body<1, NT, RMAX, GMAX, 0, 0, 0, 0, 0, CS>(D0, a, TileShard());
 }
 #undef TSTAMP
 
@@ -1969,6 +2018,34 @@ static hipError_t launch_tiles_nt(hipStream_t st, const TileDev& D, const TileLa
     case 2: return launch_tiles_c<2, NT, 0, 0>(st, D, a, lds, nullptr, 0);
     case 3: return launch_tiles_c<3, NT, 0, 0>(st, D, a, lds, nullptr, 0);
     case 4: return launch_tiles_c<4, NT, 0, 0>(st, D, a, lds, nullptr, 0);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// chain-split launch (256-thread tiles, one chain per workgroup, D.C per CU)
+template <int CS>
+static hipError_t launch_tiles_cs(hipStream_t st, const TileDev& D, const TileLaunch& a, int lds) {
+  constexpr int NT = 256;
+  auto k = sweep_tiles_cs_kernel<CS, NT, tile_rmax_cs(NT), tile_gmax(NT)>;
+  // LDS floor: at most CS workgroups per CU
+  const int floor = kTCuLds / (CS + 1) + 64;
+  lds = lds < floor ? floor : lds;
+  if (lds * CS > kTCuLds) return hipErrorInvalidValue;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(tile_call_bump_kernel, dim3(1), dim3(1), 0, st, D.ctl);
+  hipLaunchKernelGGL(k, dim3(D.T * CS), dim3(NT), lds, st, D, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_sweep_tiles_cs(hipStream_t st, const TileDev& D, const TileLaunch& a, int max_rows, int NT,
+                                 int max_batches, int max_gslots) {
+  if (NT != 256 || D.rg || D.batch_split || D.dbg) return hipErrorInvalidValue;
+  const int lds = tile_lds_bytes(max_rows, 1, NT, D.K, max_batches, max_gslots);
+  switch (D.C) {
+    case 2: return launch_tiles_cs<2>(st, D, a, lds);
+    case 3: return launch_tiles_cs<3>(st, D, a, lds);
+    case 4: return launch_tiles_cs<4>(st, D, a, lds);
     default: return hipErrorInvalidValue;
   }
 }

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define NNGP_ABI_VERSION 7
+#define NNGP_ABI_VERSION 8
 #define NNGP_SHARD_ID_BYTES 128 /* RCCL unique id */
 #define NNGP_IPC_HANDLE_BYTES 192 /* HIP IPC handles of a tile shard's granule buffer, w replica, flags */
 
@@ -108,6 +108,7 @@ typedef struct {
   int tile_ghost_pass;       /* tile engine: ghost cells a (tile, colour) applies per register pass */
   int tile_ghost_cells_max;  /* tile engine: most ghost cells of one (tile, colour) */
   int tile_r_global;         /* tile engine: 1 = the tiles' r in global memory (layout beyond the LDS) */
+  int tile_chain_split;      /* tile engine: 1 = one workgroup per (chain, tile), the chains of a tile on one CU */
 } nngp_info;
 
 /* ---------- library ---------- */

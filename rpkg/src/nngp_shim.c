@@ -135,13 +135,14 @@ SEXP C_nngp_ctx_info(SEXP p) {
   const char* nm[] = {"n", "b", "d", "n_obs", "n_colors", "n_levels", "nnz", "n_entries", "max_collen", "device",
                       "n_chains", "lanes_per_chain", "n_chunks", "sweep_engine", "n_tiles", "tile_rows_max",
                       "n_ghost_cells", "n_ranks", "rank", "shard_owned", "shard_needed_rows",
-                      "shard_exchange_slots", "tile_ghost_pass", "tile_ghost_cells_max", "tile_r_global"};
+                      "shard_exchange_slots", "tile_ghost_pass", "tile_ghost_cells_max", "tile_r_global",
+                      "tile_chain_split"};
   const double v[] = {inf.n, inf.b, inf.d, inf.n_obs, inf.n_colors, inf.n_levels, (double)inf.nnz,
                       (double)inf.n_entries, inf.max_collen, inf.device, inf.n_chains, inf.lanes_per_chain,
                       inf.n_chunks, inf.sweep_engine, inf.n_tiles, inf.tile_rows_max, (double)inf.n_ghost_cells,
                       inf.n_ranks, inf.rank, (double)inf.shard_owned, (double)inf.shard_needed_rows,
                       (double)inf.shard_exchange_slots, inf.tile_ghost_pass, inf.tile_ghost_cells_max,
-                      inf.tile_r_global};
+                      inf.tile_r_global, inf.tile_chain_split};
   const int k = (int)(sizeof v / sizeof v[0]);
   SEXP out = PROTECT(Rf_allocVector(REALSXP, k)), names = PROTECT(Rf_allocVector(STRSXP, k));
   for (int i = 0; i < k; ++i) {

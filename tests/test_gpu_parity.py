@@ -706,3 +706,40 @@ def test_tile_engine_interior_first_split_matches_oracle(P, O, engine, monkeypat
         ref = O.sweep("local", fields[k], Ls[k], NN, col, O.precision_diag(Ls[k], NN), np.ones(n, np.int32), y,
                       np.full(n, b0s[k]), lm, b0s[k], lss[k], lnvs[k], z)
         np.testing.assert_allclose(got[k], ref, rtol=1e-8, atol=1e-9, err_msg=f"chain {k}")
+
+
+@pytest.mark.parametrize("n,m,C", [(20000, 10, 2), (60000, 15, 3), (3000, 5, 4), (40000, 20, 3), (1_000_000, 15, 3)])
+def test_tile_engine_chain_split_equals_joint_bitwise(P, engine, monkeypatch, n, m, C):
+    """Chain-split tile launches (NNGP_TILE_CHAINS=split: one workgroup per
+    (chain, tile), the chains' workgroups of a tile sharing its CU) run each
+    chain's arithmetic in the order of the joint 256-thread tiles (one
+    workgroup per tile running every chain): every chain's field bitwise equal
+    after two calls (3 + 2 sweeps)."""
+    if engine != "tiles-default":
+        pytest.skip("sets the engine itself")
+    monkeypatch.setenv("NNGP_TILE_NT", "256")
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=n + C)
+    rng = np.random.default_rng(C)
+    fields = [rng.normal(size=n) for _ in range(C)]
+    out = []
+    for mode in ("joint", "split"):
+        monkeypatch.setenv("NNGP_TILE_CHAINS", mode)
+        with P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=C) as ctx:
+            info = ctx.info
+            assert info["sweep_engine"] == 1 and info["tile_chain_split"] == int(mode == "split"), info
+            for k in range(C):
+                ctx.select(k)
+                ctx.factor(0, "matern15_isotropic", [1.0, 0.05 + 0.01 * k, 0.0])
+                ctx.set_field(fields[k])
+                ctx.set_mu(None, 0.1 * k)
+            ctx.sweep_chains(3, [0.1 * k for k in range(C)], [0.1] * C, [-0.4] * C, [31 + k for k in range(C)],
+                             [0] * C)
+            ctx.sweep_chains(2, [0.1 * k for k in range(C)], [0.0] * C, [-0.5] * C, [41 + k for k in range(C)],
+                             [3] * C)
+            res = []
+            for k in range(C):
+                ctx.select(k)
+                res.append(ctx.get_field())
+            out.append(res)
+    for k in range(C):
+        np.testing.assert_array_equal(out[1][k], out[0][k], err_msg=f"chain {k}")
