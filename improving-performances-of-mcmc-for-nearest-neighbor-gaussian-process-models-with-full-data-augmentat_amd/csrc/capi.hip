@@ -128,6 +128,7 @@ struct nngp_ctx {
   double* dwx_d = nullptr;        // n x C granules of 16 B
   bool rglobal = false;           // tiles keep r in global memory (rg_d) instead of LDS
   bool tcs = false;               // chain-split tile launches (one chain per workgroup, kernels.hip sweep_tiles_cs_kernel)
+  int tstagger = 0;               // chain-split: start offset per chain (NNGP_TILE_STAGGER, 100 MHz ticks)
   double* rg_d = nullptr;         // sum of the tiles' local rows x C
   unsigned* ctl_d = nullptr;      // [0] call id, [1] timeout word
   unsigned* tmo_h = nullptr;      // pinned copy of the timeout word after each launch
@@ -519,9 +520,14 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       const bool rg_forced = std::getenv("NNGP_TILE_R") && std::string(std::getenv("NNGP_TILE_R")) == "global";
       const bool hopeless = !rg_forced && (long long)(n / std::max(T, 1)) * n_chains * 8 > (long long)lds_max;
       if (hopeless) terr = "tile layout: a tile's own rows exceed the LDS";
+      // cells per own batch: NT x RMAX of the kernel; NNGP_TILE_BATCH_CELLS
+      // may lower it (e.g. joint tiles cut like chain-split ones, for bitwise
+      // comparisons)
+      int rmax_l = csplit ? tile_rmax_cs(NT) : tile_rmax(n_chains, NT);
+      if (const char* bc = std::getenv("NNGP_TILE_BATCH_CELLS"))
+        rmax_l = std::max(1, std::min(rmax_l, std::atoi(bc) / NT));
       bool ok = cus > 0 && T <= n && !hopeless &&
-                build_tile_layout(nn.data(), n, b, coloring, locs, d, T, NT,
-                                  csplit ? tile_rmax_cs(NT) : tile_rmax(n_chains, NT), c->tl, terr, G,
+                build_tile_layout(nn.data(), n, b, coloring, locs, d, T, NT, rmax_l, c->tl, terr, G,
                                   split);
       if (ok && csplit) {
         // n_chains workgroups of one chain per CU
@@ -532,6 +538,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
                  std::to_string(n_chains) + " chains per CU (device: " + std::to_string(lds_max) + ")";
         } else {
           c->tcs = true;
+          if (const char* sg = std::getenv("NNGP_TILE_STAGGER")) c->tstagger = std::max(0, std::atoi(sg));
         }
       }
       const int need = ok && !csplit ? tile_lds_bytes(c->tl.max_rows, n_chains, NT, c->tl.K, c->tl.max_batches, c->tl.max_gslots) : 0;
@@ -1330,6 +1337,7 @@ static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, int mask, const double*
     a.chain_mask = mask;
     a.z_in = z_dev;
     if (c->tcs) {
+      a.stagger = c->tstagger;
       HIPCHK(c, launch_sweep_tiles_cs(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NT, c->tl.max_batches,
                                       c->tl.max_gslots));
     } else {

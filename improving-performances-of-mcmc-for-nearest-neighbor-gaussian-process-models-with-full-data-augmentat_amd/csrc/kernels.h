@@ -174,6 +174,7 @@ struct TileLaunch {
   int n_sweeps;
   int chain_mask;
   const double* z_in;         // injected normals, per sweep: slot x C (nullptr: Philox inline)
+  int stagger = 0;            // chain-split: chain k starts k x stagger ticks (100 MHz) late
 };
 
 int tile_lds_bytes(int max_rows, int C, int NT, int K, int max_batches, int max_gslots);

@@ -1845,9 +1845,10 @@ __device__ __forceinline__ void sweep_tiles_body(const TileDev& D0, TileLaunch a
   int Tg = SH ? sh.tile0 + (int)blockIdx.x : (int)blockIdx.x;
   const int rk = SH ? Tg / sh.Tl : 0;
   TileDev D = SH ? sh.devs[rk - sh.rank0] : D0;
+  int ch0 = 0;
   if constexpr (CS != C) {
     static_assert(C == 1 && !SH && !RG && !IB && !PROBE, "chain-split: one chain per workgroup, single GPU");
-    const int ch0 = Tg / D.T;
+    ch0 = Tg / D.T;
     Tg -= ch0 * D.T;
     D.cell_val += (size_t)ch0 * D.n_cells;
     D.gval += (size_t)ch0 * D.n_gcells;
@@ -1916,6 +1917,12 @@ __device__ __forceinline__ void sweep_tiles_body(const TileDev& D0, TileLaunch a
   if (DB && S.nph > 0 && S.gptr_s[0] < S.gptr_s[1]) tile_load_ghosts<C, NT, GMAX>(D, S.gptr_s[0], S.gptr_s[1], GA, t);
   __syncthreads();
   TSTAMP(S, 7);
+  if (CS != C && ch0 > 0 && a.stagger > 0) {
+    // chain-split: the chains' phases out of step (identical work per phase
+    // would keep them in lockstep, contending for the CU at the same time)
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)ch0 * (unsigned)a.stagger) __builtin_amdgcn_s_sleep(4);
+  }
   if (DB) {
     for (int ph = 0; ph < S.nph; ph += 2) {
       tile_phase<C, NT, RMAX, GMAX, DB, PROBE, SH, CS>(D, a, sh, S, ph, A, B, GA, GB);

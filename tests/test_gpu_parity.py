@@ -713,11 +713,13 @@ def test_tile_engine_chain_split_equals_joint_bitwise(P, engine, monkeypatch, n,
     """Chain-split tile launches (NNGP_TILE_CHAINS=split: one workgroup per
     (chain, tile), the chains' workgroups of a tile sharing its CU) run each
     chain's arithmetic in the order of the joint 256-thread tiles (one
-    workgroup per tile running every chain): every chain's field bitwise equal
-    after two calls (3 + 2 sweeps)."""
+    workgroup per tile running every chain) cut into the same 2048-cell
+    batches: every chain's field bitwise equal after two calls (3 + 2
+    sweeps)."""
     if engine != "tiles-default":
         pytest.skip("sets the engine itself")
     monkeypatch.setenv("NNGP_TILE_NT", "256")
+    monkeypatch.setenv("NNGP_TILE_BATCH_CELLS", "2048")
     locs, NN, col, lm, y = make_problem(P, n, m, seed=n + C)
     rng = np.random.default_rng(C)
     fields = [rng.normal(size=n) for _ in range(C)]
