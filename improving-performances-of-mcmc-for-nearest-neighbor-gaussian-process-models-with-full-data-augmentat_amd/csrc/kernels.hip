@@ -1635,9 +1635,14 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
       if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
       if (pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * CS + t % C) * 16), 0, SH ? kGranAuxSys : kGranAux);
     }
+    // the next batch's draw scalars before its cells go out: the cells' loads
+    // are conditional (rows past R), so a wait for the records issued before
+    // them would also wait for every cell
+    if (more) tile_prep_items<C, NT, RMAX, CS>(D, a, S.sc_s, S.seed_s, sn, nxt, t);
     if (more) tile_load_cells<C, NT, RMAX>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
+  } else if (more) {
+    tile_prep_items<C, NT, RMAX, CS>(D, a, S.sc_s, S.seed_s, sn, nxt, t);
   }
-  if (more) tile_prep_items<C, NT, RMAX, CS>(D, a, S.sc_s, S.seed_s, sn, nxt, t);
   if (DB && pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * CS + t % C) * 16), 0, SH ? kGranAuxSys : kGranAux);
   TSTAMP(S, 5);
   TLSTAMP(S, 4);
