@@ -1389,6 +1389,7 @@ struct TileState {
   unsigned* spin_s;
   __amdgpu_buffer_rsrc_t gran;
   unsigned call;
+  int gsl;                          // this phase's first foreign slot index of the thread (loaded a phase ahead)
   unsigned* tmo;
   int G;                            // tile shard: ranks (1: single GPU)
   bool timed_out;
@@ -1597,7 +1598,9 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
   // this colour's foreign slots (one granule per slot and chain): the first
   // NT items' slot indices load now, behind the own work
   const int gs0 = S.gsp_s[c], nfi = (S.gsp_s[c + 1] - gs0) * C;
-  const int gsl_pref = t < nfi ? D.gslot[gs0 + t / C] : 0;
+  // loaded during the previous phase's hand-off: a load issued here would be
+  // waited for behind the draw's (conditional) stores before the first poll
+  const int gsl_pref = S.gsl;
   if (DB) {
     // the next colour's first batch (and ghost chunk): their HBM stream
     // overlaps this colour's work (two register sets)
@@ -1646,6 +1649,10 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
   if (DB && pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * CS + t % C) * 16), 0, SH ? kGranAuxSys : kGranAux);
   TSTAMP(S, 5);
   TLSTAMP(S, 4);
+  {  // the next phase's first foreign slot indices (complete once the polls below have waited)
+    const int gn = S.gsp_s[cn], nfn = has_next ? (S.gsp_s[cn + 1] - gn) * C : 0;
+    S.gsl = t < nfn ? D.gslot[gn + t / C] : 0;
+  }
   // ---- 3. hand-off: the granule of each (foreign slot, chain) of this colour
   // until it carries this epoch -> gdw_s; then every ghost cell adds B[k,j]
   // dw_j to its local row (a slot read by several rows of the tile is fetched
@@ -1910,6 +1917,7 @@ __device__ __forceinline__ void sweep_tiles_body(const TileDev& D0, TileLaunch a
     S.seed_s[2 * t + 1] = D.scal[t].counter_base;
   }
   S.call = SH ? *sh.call : D.ctl[0];
+  S.gsl = 0;
   S.tmo = D.ctl + 1;
   S.gran = __builtin_amdgcn_make_buffer_rsrc(SH ? sh.gx[rk] : D.dwx, 0, 0x7FFFFFFF, 0x00020000);
   __syncthreads();
@@ -1920,6 +1928,7 @@ __device__ __forceinline__ void sweep_tiles_body(const TileDev& D0, TileLaunch a
     tile_prep_items<C, NT, RMAX, CS>(D, a, S.sc_s, S.seed_s, 0, A, t);
   }
   if (DB && S.nph > 0 && S.gptr_s[0] < S.gptr_s[1]) tile_load_ghosts<C, NT, GMAX>(D, S.gptr_s[0], S.gptr_s[1], GA, t);
+  if (S.nph > 0 && t < (S.gsp_s[1] - S.gsp_s[0]) * C) S.gsl = D.gslot[S.gsp_s[0] + t / C];
   __syncthreads();
   TSTAMP(S, 7);
   if (CS != C && ch0 > 0 && a.stagger > 0) {
