@@ -1600,7 +1600,8 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
   const int gs0 = S.gsp_s[c], nfi = (S.gsp_s[c + 1] - gs0) * C;
   // loaded during the previous phase's hand-off: a load issued here would be
   // waited for behind the draw's (conditional) stores before the first poll
-  const int gsl_pref = S.gsl;
+  // (double-buffered: at the phase start, measured faster at 1 chain)
+  const int gsl_pref = DB ? (t < nfi ? D.gslot[gs0 + t / C] : 0) : S.gsl;
   if (DB) {
     // the next colour's first batch (and ghost chunk): their HBM stream
     // overlaps this colour's work (two register sets)
@@ -1649,7 +1650,7 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
   if (DB && pol) gfirst = __builtin_amdgcn_raw_buffer_load_b128(S.gran, (int)(((size_t)gsl_pref * CS + t % C) * 16), 0, SH ? kGranAuxSys : kGranAux);
   TSTAMP(S, 5);
   TLSTAMP(S, 4);
-  {  // the next phase's first foreign slot indices (complete once the polls below have waited)
+  if (!DB) {  // the next phase's first foreign slot indices (complete once the polls below have waited)
     const int gn = S.gsp_s[cn], nfn = has_next ? (S.gsp_s[cn + 1] - gn) * C : 0;
     S.gsl = t < nfn ? D.gslot[gn + t / C] : 0;
   }
