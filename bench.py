@@ -64,6 +64,12 @@ def make_workload(P, n, m, covfun, cp, seed, device, chains):
     return wl
 
 
+def replica_seeds(rank, chains):
+    """--multi replicas / N = 1: (workload seed, chain seeds) of a rank -- every
+    rank sweeps its own field and chains (weak scaling of independent chains)."""
+    return 1000 + rank, [77 + 10 * rank + k for k in range(chains)]
+
+
 def open_context(P, wl, covfun, cp, device, chains, seed):
     rng = np.random.default_rng(seed)
     ctx = P.ChainContext(wl["locs"], wl["NN"], wl["col"], wl["lm"], wl["y"], device=device, n_chains=chains)
@@ -118,8 +124,13 @@ def cpu_baseline(P, wl, covfun, cp, budget_s, chains):
     masked = sum(d / el for d, el in res)
     # one chain on all the host cores the process may use (OMP_NUM_THREADS on
     # the GPU box), masked form and the optimised local form
+    # the "all cores" leg runs on the CPUs this process may actually use: its
+    # affinity set (the GPU box gives a job a share of a larger host, and
+    # OMP_NUM_THREADS names that share), not the host's whole os.cpu_count()
     host_cpus = os.cpu_count() or 1
-    omp = max(1, min(64, int(os.environ.get("OMP_NUM_THREADS") or host_cpus)))
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else host_cpus
+    omp_env = int(os.environ.get("OMP_NUM_THREADS") or 0)
+    omp = max(1, min(affinity, omp_env) if omp_env > 0 else affinity)
     one, locmt, loc = [None], [None], [None]
     run("masked", one, 0, omp)
     run("local", locmt, 0, omp)
@@ -132,8 +143,10 @@ def cpu_baseline(P, wl, covfun, cp, budget_s, chains):
                        f"({sum(d for d, _ in res)} sweeps); 1 chain x {omp} OpenMP threads: masked form "
                        f"{rate(one):.3g}, local form {rate(locmt):.3g} sweeps/s; local form 1 thread "
                        f"{rate(loc):.3g} sweeps/s; oracle factor build {t_factor:.1f}s; host os.cpu_count() "
-                       f"{host_cpus}"),
+                       f"{host_cpus}, CPUs in this process's affinity set {affinity}, OMP_NUM_THREADS "
+                       f"{omp_env or 'unset'}"),
             "host_cpus": host_cpus,
+            "affinity_cpus": affinity,
             "one_chain_all_cores": {"value": rate(one), "threads": omp, "form": "masked"},
             "local_form_all_cores": {"value": rate(locmt), "threads": omp, "form": "local"},
             "local_form_value_1_thread": rate(loc)}
@@ -226,9 +239,10 @@ def timed_region(run, steps, warmup, dist=None, sync=lambda: None):
 
 def shard_parity_check(P, args, world, rank, local_rank, dist):
     """Cross-GPU parity at a small size, run by every rank before the sharded
-    measurement: the world-rank tile shard (IPC granule puts over xGMI, RCCL
-    broadcasts) against this GPU alone with the same tiles, bitwise after 3
-    sweeps of 2 chains; -> True on every rank iff every rank matched."""
+    measurement: the world-rank tile shard (IPC granule puts over xGMI, halo
+    stores into the peers' replicas) against this GPU alone with the same
+    tiles, bitwise after two calls (2 + 1 sweeps of 2 chains, nothing read in
+    between); -> True on every rank iff every rank matched."""
     import torch
 
     from nngp_amd.shard import ShardContext, _agreed, init_shard_comm
@@ -260,7 +274,11 @@ def shard_parity_check(P, args, world, rank, local_rank, dist):
                 ctx.factor(0, "exponential_isotropic", [1.0, 0.1, 0.0])
                 ctx.set_field(fields[k])
                 ctx.set_mu(None, args_c[0][k])
-            ctx.sweep_chains(3, *args_c)
+            # two calls back to back (nothing read in between: the second
+            # starts from the halo-only exchange of the first), then the read
+            # (a full exchange first)
+            ctx.sweep_chains(2, *args_c)
+            ctx.sweep_chains(1, *args_c[:4], [2] * C)
             out = []
             for k in range(C):
                 ctx.select(k)
@@ -277,6 +295,24 @@ def shard_parity_check(P, args, world, rank, local_rank, dist):
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return bool(t.item()), {"n": n, "m": m, "chains": C, "sweeps": 3, "tiles": 16 * world,
                             "exchange_slots_rank0": res[1][1]["shard_exchange_slots"]}
+
+
+METRIC = "full-field Gibbs sweeps/sec at n=1e6, m=15; achieved HBM GB/s vs roofline"
+
+
+def shard_failure_line(args, world, scaling, note, parity=None, pinfo=None):
+    """The sharded measurement did not run (or its cross-GPU parity check
+    failed): the line says so with a null value -- no other measurement is
+    substituted (independent replicas only with --multi replicas)."""
+    n = args.n * world if scaling == "weak" else args.n
+    return {"metric": METRIC, "value": None, "unit": "sweeps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": scaling,
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"sharded chromatic sweep of ONE field n={n} m={args.m} {args.covfun}",
+                       "n": n, "m": args.m, "chains": args.chains,
+                       "parity_check": {"bitwise_equal_to_one_gpu": parity, **(pinfo or {})},
+                       "error": note},
+            "roofline": None, "cpu_baseline": None}
 
 
 def shard_main(P, args, world, rank, local_rank, dist, scaling):
@@ -297,7 +333,8 @@ def shard_main(P, args, world, rank, local_rank, dist, scaling):
     parity, pinfo = shard_parity_check(P, args, world, rank, local_rank, dist) if world > 1 else (None, None)
     log(f"cross-GPU parity check ({time.time() - t_par:.1f}s): {parity}", rank)
     if world > 1 and not parity:
-        raise RuntimeError("sharded sweep differs from one GPU on the parity check")
+        return shard_failure_line(args, world, scaling, "the sharded sweep differs from one GPU on the cross-GPU "
+                                  "parity check: not measured", parity, pinfo)
     log(f"shard setup n={n} m={args.m} {covfun} chains={C} world={world} scaling={scaling}", rank)
     agree = (lambda f: _agreed(dist, f)) if world > 1 else (lambda f: f())
     wl = agree(lambda: make_workload(P, n, args.m, covfun, cp, seed=1000, device=local_rank, chains=C))
@@ -342,7 +379,10 @@ def shard_main(P, args, world, rank, local_rank, dist, scaling):
            "as 16-B granules stored into the reader GPU's buffer over xGMI (HIP IPC), each rank's halo slots of w "
            "stored into the peers' replicas after a call (device flags, no RCCL)" if tiles
            else "colour shard: one launch per colour, RCCL all-gather per colour")
-    out = {"metric": "full-field Gibbs sweeps/sec at n=1e6, m=15; achieved HBM GB/s vs roofline",
+    out = {"metric": METRIC,
+           "metric_detail": (f"sweeps of 1e6-location fields per second = chain-sweeps/s x n/1e6 of the one "
+                             f"n={n} field ({scaling} scaling" +
+                             (f": n = {world} x {args.n}" if scaling == "weak" else "") + ")"),
            "value": args.steps * C * (n / 1e6) / elapsed, "unit": "sweeps/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
            "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f64",
@@ -389,7 +429,7 @@ def main():
                          "default) or n = --n (shard-strong), or independent chains per GPU (replicas)")
     ap.add_argument("--shard", action="store_true", help="the sharded sweep even at N = 1 (strong)")
     ap.add_argument("--no-fallback", action="store_true",
-                    help="exit with an error when the sharded sweep fails instead of measuring replicas")
+                    help="(default; kept for old command lines) a failed sharded sweep prints a null value")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -414,7 +454,7 @@ def main():
         scaling = "weak" if (world > 1 and args.multi == "shard-weak") else "strong"
         try:
             out = shard_main(P, args, world, rank, local_rank, dist, scaling)
-        except Exception as e:  # noqa: BLE001 -- reported in the JSON line, then the replicas measurement
+        except Exception as e:  # noqa: BLE001 -- reported in the JSON line (null value)
             out = None
             note = f"sharded sweep failed on rank {rank}: {type(e).__name__}: {e}"
             log(note, 0)
@@ -423,25 +463,22 @@ def main():
 
             ok = _t.tensor([0 if out is None else 1], dtype=_t.int32)
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-            if not ok.item() and note is None:
-                note = "sharded sweep failed on another rank"
+            if not ok.item():
                 out = None
-        if out is not None:
-            if rank == 0:
-                print(json.dumps(out), flush=True)
-            if dist:
-                dist.destroy_process_group()
-            return
-        if args.no_fallback:
-            if dist:
-                dist.destroy_process_group()
-            raise SystemExit(f"bench: {note}")
+                note = note or "sharded sweep failed on another rank"
+        if out is None:
+            out = shard_failure_line(args, world, scaling, note)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return
     log(f"setup n={args.n} m={args.m} {covfun} chains={args.chains} world={world}", rank)
-    wl = make_workload(P, args.n, args.m, covfun, cp, seed=1000 + rank, device=local_rank, chains=args.chains)
+    wseed, seeds = replica_seeds(rank, args.chains)
+    wl = make_workload(P, args.n, args.m, covfun, cp, seed=wseed, device=local_rank, chains=args.chains)
     C = args.chains
     nc = args.n_chromatic
     b0, ls, lnv = wl["beta0"], wl["log_scale"], wl["log_noise_variance"]
-    seeds = [77 + 10 * rank + k for k in range(C)]
 
     def timed(ctx, steps, warmup):
         """warmup + steps sweeps of every chain of ctx in calls of n_chromatic"""
@@ -525,7 +562,7 @@ def main():
         cpu = cpu_baseline(P, wl, covfun, cp, args.cpu_budget, C)
     ctx.close()
     value = args.steps * C * world / elapsed
-    out = {"metric": "full-field Gibbs sweeps/sec at n=1e6, m=15; achieved HBM GB/s vs roofline",
+    out = {"metric": METRIC,
            "value": value, "unit": "sweeps/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
@@ -538,8 +575,7 @@ def main():
                       "n_tiles": info["n_tiles"], "tile_rows_max": info["tile_rows_max"],
                       "n_ghost_cells": info["n_ghost_cells"],
                       "single_chain": single,
-                      "parallelism": f"chains {C} per GPU x {world} GPUs (independent)",
-                      "multi_gpu_note": note},
+                      "parallelism": f"chains {C} per GPU x {world} GPUs (independent)"},
            "roofline": roofline, "cpu_baseline": cpu, "secondary": mcmc}
     if rank == 0:
         print(json.dumps(out), flush=True)

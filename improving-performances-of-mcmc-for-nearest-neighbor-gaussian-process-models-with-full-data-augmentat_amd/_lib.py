@@ -14,7 +14,9 @@ from pathlib import Path
 import numpy as np
 
 PKG_DIR = Path(__file__).resolve().parent
-LIB_PATH = Path(os.environ.get("NNGP_LIB", PKG_DIR / "libnngp.so"))
+# built in-tree at <repo>/lib/libnngp.so (a short path: the loaded library shows
+# up in full in /proc/<pid>/maps and in the driver's native-library record)
+LIB_PATH = Path(os.environ.get("NNGP_LIB", PKG_DIR.parent / "lib" / "libnngp.so"))
 NA_INTEGER = -(2 ** 31)
 # nngp_status (include/nngp.h)
 NNGP_OK, NNGP_ERR_ARG, NNGP_ERR_HIP, NNGP_ERR_CHOL, NNGP_ERR_STATE, NNGP_ERR_NOMEM, NNGP_ERR_NODEV, NNGP_ERR_COMM = range(8)
@@ -28,7 +30,7 @@ COVFUNS = {
 # every symbol declared in include/nngp.h
 ABI_SYMBOLS = (
     "nngp_abi_version", "nngp_status_string", "nngp_order_maxmin", "nngp_find_ordered_nn",
-    "nngp_greedy_coloring", "nngp_ctx_create", "nngp_ctx_destroy", "nngp_ctx_last_error",
+    "nngp_greedy_coloring", "nngp_ctx_create", "nngp_ctx_destroy", "nngp_ctx_last_error", "nngp_ctx_engine_note",
     "nngp_set_chain", "nngp_ctx_info", "nngp_factor", "nngp_get_linv", "nngp_set_linv", "nngp_accept_factor",
     "nngp_get_precision_diag", "nngp_set_field", "nngp_get_field", "nngp_set_mu",
     "nngp_loglik", "nngp_sweep", "nngp_sweep_chains", "nngp_ancillary_propose", "nngp_ancillary_propose_chains",
@@ -37,7 +39,7 @@ ABI_SYMBOLS = (
     "nngp_tri_solve", "nngp_sweep_timed", "nngp_device_normals",
     "nngp_ctx_create_shard", "nngp_shard_unique_id", "nngp_shard_comm_init", "nngp_sweep_chains_group",
     "nngp_records_reserve", "nngp_record_field", "nngp_get_records",
-    "nngp_shard_ipc_handle", "nngp_shard_ipc_open",
+    "nngp_shard_ipc_handle", "nngp_shard_ipc_open", "nngp_shard_sync",
     "nngp_factor_chains", "nngp_loglik_chains", "nngp_field_response_ratio_chains",
     "nngp_sum_squared_residuals_chains",
 )
@@ -61,7 +63,8 @@ class Info(C.Structure):
                 ("shard_owned", C.c_longlong), ("shard_needed_rows", C.c_longlong),
                 ("shard_exchange_slots", C.c_longlong), ("tile_ghost_pass", C.c_int),
                 ("tile_ghost_cells_max", C.c_int), ("tile_r_global", C.c_int),
-                ("tile_chain_split", C.c_int)]
+                ("tile_chain_split", C.c_int), ("tile_resident_per_cu", C.c_int),
+                ("engine_fallback", C.c_int), ("tile_exchange_wave", C.c_int), ("device_cus", C.c_int)]
 
 
 _dp = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
@@ -89,6 +92,8 @@ def _load():
     L.nngp_ctx_last_error.argtypes = [_vp]
     L.nngp_ctx_last_error.restype = C.c_char_p
     L.nngp_ctx_info.argtypes = [_vp, C.POINTER(Info)]
+    L.nngp_ctx_engine_note.argtypes = [_vp]
+    L.nngp_ctx_engine_note.restype = C.c_char_p
     L.nngp_factor.argtypes = [_vp, C.c_int, C.c_int, _dp, C.c_int]
     L.nngp_get_linv.argtypes = [_vp, C.c_int, _dp]
     L.nngp_set_linv.argtypes = [_vp, C.c_int, _dp]
@@ -124,6 +129,7 @@ def _load():
     L.nngp_sum_squared_residuals_chains.argtypes = [_vp, C.c_int, _dp, _dp]
     L.nngp_shard_ipc_handle.argtypes = [_vp, C.c_char_p, C.c_int]
     L.nngp_shard_ipc_open.argtypes = [_vp, C.c_char_p, C.c_int]
+    L.nngp_shard_sync.argtypes = [_vp]
     L.nngp_records_reserve.argtypes = [_vp, C.c_int]
     L.nngp_record_field.argtypes = [_vp, C.c_int]
     L.nngp_get_records.argtypes = [_vp, C.c_int, C.c_int, _dp]

@@ -78,7 +78,9 @@ class ChainContext:
     def info(self) -> dict:
         inf = Info()
         self._chk(lib.nngp_ctx_info(self._h, C.byref(inf)))
-        return {k: getattr(inf, k) for k, _ in Info._fields_}
+        d = {k: getattr(inf, k) for k, _ in Info._fields_}
+        d["engine_note"] = lib.nngp_ctx_engine_note(self._h).decode()
+        return d
 
     # ------------------------------------------------------------ factor (A4/A5)
     def factor(self, which: int, covfun: str, covparms) -> None:

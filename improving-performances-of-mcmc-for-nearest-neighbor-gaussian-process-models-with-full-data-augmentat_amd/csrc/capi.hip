@@ -128,6 +128,11 @@ struct nngp_ctx {
   double* dwx_d = nullptr;        // n x C granules of 16 B
   bool rglobal = false;           // tiles keep r in global memory (rg_d) instead of LDS
   bool tcs = false;               // chain-split tile launches (one chain per workgroup, kernels.hip sweep_tiles_cs_kernel)
+  int txw = 0;                    // exchange-wave tiles (tiles.hip tile_phase_xw): layout cut for NT - 64 cell threads
+  int cus = 0;                    // compute units of the device
+  int tresident = 0;              // tile workgroups resident per CU (occupancy query of the instantiation)
+  int engine_fallback = 0;        // 0: none, 1: tile layout unsuitable (LDS, shape), 2: residency, 3: forced colours
+  std::string engine_note;        // why this sweep engine (nngp_ctx_engine_note)
   int tstagger = 0;               // chain-split: start offset per chain (NNGP_TILE_STAGGER, 100 MHz ticks)
   double* rg_d = nullptr;         // sum of the tiles' local rows x C
   unsigned* ctl_d = nullptr;      // [0] call id, [1] timeout word
@@ -266,6 +271,7 @@ TileDev tile_dev(nngp_ctx* c) {
   D.ctl = c->ctl_d;
   D.dbg = c->tdbg_d;
   D.probe = c->tprobe;
+  D.xw = c->txw;
   D.K = c->tl.K;
   D.C = c->C;
   D.T = c->tl.T;
@@ -304,6 +310,15 @@ int fetch4(nngp_ctx* c, int nblocks, double out[4]) {
 // tile shard without RCCL (defined with the sharded sweep below)
 static int tile_ipc_exchange(nngp_ctx* c, bool full);
 static int replica_sync(nngp_ctx* c);
+// entry points that read the field of a tile-shard rank whose replica is
+// behind (halo-only exchanges since the last nngp_shard_sync) refuse: the
+// full exchange is a collective over the ranks, so it is the caller's
+// explicit nngp_shard_sync on every rank, never a hidden one inside a reader
+static int replica_fresh(nngp_ctx* c) {
+  if (!c->stale_mask) return NNGP_OK;
+  return fail_msg(c, NNGP_ERR_STATE, "tile shard: this rank's replica of the field is behind after sweeps without a "
+                                     "communicator -- call nngp_shard_sync on every rank first");
+}
 
 // ====================================================================== ABI
 extern "C" {
@@ -483,12 +498,16 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     // shards: the tile shard when it fits (G ranks x up to one tile per CU;
     // NNGP_TILES = the total), else the colour shard
     const int G = shard_G > 0 ? shard_G : 1;
+    if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) c->cus = 0;
     if (es != "colors" && G <= kTileRanksMax) {
       int cus = 0, lds_max = 0;
-      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 0;
+      cus = c->cus;
       if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeSharedMemPerBlockOptin, device) != hipSuccess) lds_max = 0;
       int T = std::max(1, std::min(G * cus, (n + kTileTarget - 1) / kTileTarget));
-      if (const char* te = std::getenv("NNGP_TILES")) T = std::max(1, std::min(G * cus, std::atoi(te)));
+      // NNGP_TILES may ask for more tiles than CUs: the residency check below
+      // then falls back to the colour engine (the tiles spin on each other, so
+      // every workgroup of the launch must be resident at once)
+      if (const char* te = std::getenv("NNGP_TILES")) T = std::max(1, std::atoi(te));
       T = std::min(T, n);
       T = std::max(G, T / G * G);  // a multiple of the ranks
       std::string terr;
@@ -524,11 +543,22 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       // may lower it (e.g. joint tiles cut like chain-split ones, for bitwise
       // comparisons)
       int rmax_l = csplit ? tile_rmax_cs(NT) : tile_rmax(n_chains, NT);
+      // exchange-wave tiles (default for 512-thread LDS tiles; NNGP_TILE_XW=0
+      // turns them off): the last wave of the workgroup polls the hand-offs,
+      // the batches are cut for the other NT - 64 threads.  Measured at the
+      // headline: 11.16k vs 11.02k chain-sweeps/s at 3 chains, 6.34k vs 5.71k
+      // at 1 chain (tiles.hip tile_phase_xw)
+      const char* txe = std::getenv("NNGP_TILE_XW");
+      const int xwm = txe ? std::atoi(txe) : 1;
+      const bool xw = !csplit && !split && !rg_forced && NT == 512 && xwm == 1;
+      const int NTL = xw ? NT - 64 : NT;  // the layout's cell threads
       if (const char* bc = std::getenv("NNGP_TILE_BATCH_CELLS"))
-        rmax_l = std::max(1, std::min(rmax_l, std::atoi(bc) / NT));
+        rmax_l = std::max(1, std::min(rmax_l, std::atoi(bc) / NTL));
       bool ok = cus > 0 && T <= n && !hopeless &&
-                build_tile_layout(nn.data(), n, b, coloring, locs, d, T, NT, rmax_l, c->tl, terr, G,
+                build_tile_layout(nn.data(), n, b, coloring, locs, d, T, NTL, rmax_l, c->tl, terr, G,
                                   split);
+      c->tl.NTK = NT;
+      c->txw = xw ? xwm : 0;
       if (ok && csplit) {
         // n_chains workgroups of one chain per CU
         const int need1 = tile_lds_bytes(c->tl.max_rows, 1, NT, c->tl.K, c->tl.max_batches, c->tl.max_gslots);
@@ -550,6 +580,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       // colour engine stays the default there
       const char* trg = std::getenv("NNGP_TILE_R");
       const bool force_rg = trg && std::string(trg) == "global";
+      if (ok && xw && need > lds_max) { ok = false; terr = "exchange-wave tiles exceed the LDS"; }
       if (ok && (need > lds_max || force_rg)) {
         const int need_rg = tile_lds_bytes(0, n_chains, NT, c->tl.K, c->tl.max_batches, c->tl.max_gslots);
         if (force_rg && shard_G == 0 && (NT == 512 || NT == 1024) && need_rg <= lds_max) {
@@ -560,8 +591,52 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
                  " B of LDS per tile (device: " + std::to_string(lds_max) + ")";
         }
       }
+      // residency: the persistent launch needs all its workgroups on the device
+      // at once (tiles poll each other's granules); the occupancy of exactly
+      // the instantiation that will run, at its LDS, times the CUs must cover
+      // the launch's grid (one rank's tiles per process; every chain's tiles
+      // of a chain-split launch)
+      if (ok) {
+        TileDev Dq;
+        Dq.C = n_chains;
+        Dq.K = c->tl.K;
+        Dq.rg = c->rglobal ? reinterpret_cast<double*>(16) : nullptr;
+        Dq.batch_split = c->tl.split ? reinterpret_cast<const int*>(16) : nullptr;
+        Dq.xw = xw ? xwm : 0;
+        if (const char* pr = std::getenv("NNGP_PROBE"))
+          if ((std::atoi(pr) == 9 || std::atoi(pr) == 2) && (n_chains == 1 || n_chains == 3)) {
+            Dq.dbg = reinterpret_cast<unsigned long long*>(16);
+            Dq.probe = std::atoi(pr) == 9 ? 1 : 2;
+          }
+        TileShard shq;
+        int per_cu = 0;
+        hipError_t oe;
+        if (csplit) {
+          // by construction: the kernel's register budget is pinned to C
+          // workgroups per CU (amdgpu_waves_per_eu) and its LDS floor allows
+          // no more than C (the occupancy query rejects this kernel)
+          oe = hipSuccess;
+          per_cu = n_chains;
+        } else
+          oe = launch_sweep_tiles(nullptr, Dq, TileLaunch(), c->tl.max_rows, NT, c->tl.max_batches, c->tl.max_gslots,
+                                  shard_G > 0 ? &shq : nullptr, 0, &per_cu);
+        (void)hipGetLastError();
+        const long long grid = csplit ? (long long)T * n_chains : (long long)(T / G);
+        c->tresident = oe == hipSuccess ? per_cu : 0;
+        if (oe != hipSuccess || (long long)per_cu * cus < grid) {
+          ok = false;
+          c->engine_fallback = 2;
+          terr = "residency: " + std::to_string(grid) + " tile workgroups per device > " + std::to_string(per_cu) +
+                 " resident per CU x " + std::to_string(cus) + " CUs" +
+                 (oe != hipSuccess ? std::string(" (occupancy query: ") + hipGetErrorString(oe) + ")" : "");
+        }
+      }
       if (ok) {
         c->engine = 1;
+        c->engine_note = "tiles: " + std::to_string(T) + " tiles of " + std::to_string(NT) + " threads, " +
+                         std::to_string(c->tresident) + " resident per CU x " + std::to_string(cus) + " CUs" +
+                         (c->rglobal ? ", r in global memory" : "") + (xw ? ", exchange wave" : "") +
+                         (c->tcs ? ", chain-split" : "");
         if (shard_G > 0) {
           c->shard = true;
           c->tG = G;
@@ -570,8 +645,16 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
         }
       } else {
         c->tl = TileLayout();
+        c->txw = 0;
+        c->tcs = false;
+        c->rglobal = false;
+        if (c->engine_fallback == 0) c->engine_fallback = 1;
+        c->engine_note = "colours (tile engine not used: " + terr + ")";
         if (es == "tiles") { delete c; return fail_msg(nullptr, NNGP_ERR_ARG, "tile engine: " + terr); }
       }
+    } else {
+      c->engine_fallback = 3;
+      c->engine_note = es == "colors" ? "colours (NNGP_ENGINE=colors)" : "colours (more ranks than the tile shard takes)";
     }
   }
   if (c->engine == 1) {
@@ -706,7 +789,13 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     }
     CK(hipMemcpy(c->tb_d, tb.data(), sizeof(int4) * nb, hipMemcpyHostToDevice));
     CK(upload(c->tb_ptr_d, TL.batch_ptr.data(), TL.batch_ptr.size(), c->st));
-    CK(upload(c->cell_pk_d, TL.cell_pk.data(), ncell, c->st));
+    {
+      // device encoding (tiles.hip tile_lr): the local-row field XOR its
+      // padding value, so padding -- and an out-of-range buffer load -- is 0
+      std::vector<uint32_t> pk(TL.cell_pk);
+      for (uint32_t& v : pk) v ^= kTilePadRow;
+      CK(hipMemcpy(c->cell_pk_d, pk.data(), sizeof(uint32_t) * ncell, hipMemcpyHostToDevice));
+    }
     CK(upload(c->cell_src_d, TL.cell_src.data(), ncell, c->st));
     CK(hipMemsetAsync(c->cell_val_d, 0, sizeof(double) * std::max<size_t>(1, ncell * C), c->st));
     CK(upload(c->gcell_d, reinterpret_cast<const int2*>(TL.gcell.data()), ng, c->st));
@@ -894,6 +983,8 @@ int nngp_set_chain(nngp_ctx* c, int chain) {
   return NNGP_OK;
 }
 
+const char* nngp_ctx_engine_note(const nngp_ctx* c) { return c ? c->engine_note.c_str() : ""; }
+
 int nngp_ctx_info(const nngp_ctx* c, nngp_info* info) {
   if (!c || !info) return NNGP_ERR_ARG;
   info->n = c->n; info->b = c->b; info->d = c->d; info->n_obs = c->n_obs;
@@ -927,10 +1018,14 @@ int nngp_ctx_info(const nngp_ctx* c, nngp_info* info) {
     info->shard_needed_rows = c->shard ? c->sp.needed_rows : 0;
     info->shard_exchange_slots = c->shard ? c->sp.xoff[c->sp.K] : 0;
   }
-  info->tile_ghost_pass = c->engine == 1 ? c->tl.NT * tile_gmax(c->tl.NT) : 0;
+  info->tile_ghost_pass = c->engine == 1 ? c->tl.NTK * tile_gmax(c->tl.NTK) : 0;
   info->tile_ghost_cells_max = 0;
   info->tile_r_global = c->rglobal ? 1 : 0;
   info->tile_chain_split = c->tcs ? 1 : 0;
+  info->tile_resident_per_cu = c->engine == 1 ? c->tresident : 0;
+  info->engine_fallback = c->engine_fallback;
+  info->tile_exchange_wave = c->txw ? 1 : 0;
+  info->device_cus = c->cus;
   if (c->engine == 1)
     for (size_t i = 0; i + 1 < c->tl.gptr.size(); ++i)
       info->tile_ghost_cells_max = std::max(info->tile_ghost_cells_max, c->tl.gptr[i + 1] - c->tl.gptr[i]);
@@ -1132,7 +1227,7 @@ int nngp_set_field(nngp_ctx* c, const double* field) {
 
 int nngp_get_field(nngp_ctx* c, double* field) {
   if (!c || !field) return NNGP_ERR_ARG;
-  { int rs_ = replica_sync(c); if (rs_) return rs_; }
+  { int rs_ = replica_fresh(c); if (rs_) return rs_; }
   ChainState& S = c->ch[c->cur];
   if (!S.have_field) return fail_msg(c, NNGP_ERR_STATE, "get_field: no field");
   int rc;
@@ -1165,7 +1260,7 @@ int nngp_records_reserve(nngp_ctx* c, int n_rows) {
 
 int nngp_record_field(nngp_ctx* c, int row) {
   if (!c) return NNGP_ERR_ARG;
-  { int rs_ = replica_sync(c); if (rs_) return rs_; }
+  { int rs_ = replica_fresh(c); if (rs_) return rs_; }
   ChainState& S = c->ch[c->cur];
   if (!S.rec_d || row < 0 || row >= S.rec_rows) return fail_msg(c, NNGP_ERR_ARG, "record_field: row out of the reserved records");
   if (!S.have_field) return fail_msg(c, NNGP_ERR_STATE, "record_field: no field");
@@ -1250,7 +1345,7 @@ int nngp_loglik_chains(nngp_ctx* c, int which, int chain_mask, const double* bet
   if (!c || !ll || !beta0 || !log_scale || (which != 0 && which != 1) || chain_mask <= 0 ||
       chain_mask >= (1 << c->C))
     return NNGP_ERR_ARG;
-  { int rs_ = replica_sync(c); if (rs_) return rs_; }
+  { int rs_ = replica_fresh(c); if (rs_) return rs_; }
   int rc;
   if ((rc = set_device(c))) return rc;
   for (int k = 0; k < c->C; ++k)
@@ -1338,10 +1433,10 @@ static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, int mask, const double*
     a.z_in = z_dev;
     if (c->tcs) {
       a.stagger = c->tstagger;
-      HIPCHK(c, launch_sweep_tiles_cs(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NT, c->tl.max_batches,
+      HIPCHK(c, launch_sweep_tiles_cs(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NTK, c->tl.max_batches,
                                       c->tl.max_gslots));
     } else {
-      HIPCHK(c, launch_sweep_tiles(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NT, c->tl.max_batches,
+      HIPCHK(c, launch_sweep_tiles(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NTK, c->tl.max_batches,
                                     c->tl.max_gslots));
     }
     HIPCHK(c, hipMemcpyAsync(c->tmo_h, c->ctl_d + 1, sizeof(unsigned), hipMemcpyDeviceToHost, c->st));
@@ -1607,6 +1702,11 @@ static int replica_sync(nngp_ctx* c) {
   return tile_timeout_check(c);
 }
 
+int nngp_shard_sync(nngp_ctx* c) {
+  if (!c) return NNGP_ERR_ARG;
+  return replica_sync(c);
+}
+
 // A call of the tile-sharded sweep on rank trank: prologue
 // (full replica: r = B w of every row), one persistent launch of the rank's
 // tiles (draws read by other ranks' tiles go into their granule buffers over
@@ -1662,7 +1762,7 @@ static int tile_shard_call(nngp_ctx* c, int n_sweeps, int mask) {
   a.n_sweeps = n_sweeps;
   a.chain_mask = mask;
   a.z_in = nullptr;
-  hipError_t e = launch_sweep_tiles(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NT, c->tl.max_batches,
+  hipError_t e = launch_sweep_tiles(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NTK, c->tl.max_batches,
                                     c->tl.max_gslots, &sh, c->tTl);
   if (e == hipSuccess) e = hipMemcpyAsync(c->tmo_h, c->ctl_d + 1, sizeof(unsigned), hipMemcpyDeviceToHost, c->st);
   // the broadcasts go out even after a failed launch: the peers wait in them
@@ -1833,10 +1933,10 @@ static int tile_group_call(nngp_ctx** ctxs, int G, int n_sweeps, const double* b
     set_device(L);
     int cus = 0;
     GCHK(L, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, L->device));
-    if ((g1 - g0) * Tl > cus) {
+    if ((long long)(g1 - g0) * Tl > (long long)std::max(L->tresident, 1) * cus) {
       cleanup();
-      return fail_msg(L, NNGP_ERR_ARG, "sweep_chains_group: the tiles of the ranks on one device exceed its CUs "
-                                       "(they must all be resident; fewer tiles: NNGP_TILES)");
+      return fail_msg(L, NNGP_ERR_ARG, "sweep_chains_group: the tiles of the ranks on one device exceed what is "
+                                       "resident at once (occupancy x CUs; fewer tiles: NNGP_TILES)");
     }
     for (int h = 0; h < G; ++h)
       if (ctxs[h]->device != L->device) {
@@ -1851,7 +1951,7 @@ static int tile_group_call(nngp_ctx** ctxs, int G, int n_sweeps, const double* b
     a.n_sweeps = n_sweeps;
     a.chain_mask = mask;
     a.z_in = nullptr;
-    GCHK(L, launch_sweep_tiles(L->st, devs[g0], a, L->tl.max_rows, L->tl.NT, L->tl.max_batches, L->tl.max_gslots, &sh,
+    GCHK(L, launch_sweep_tiles(L->st, devs[g0], a, L->tl.max_rows, L->tl.NTK, L->tl.max_batches, L->tl.max_gslots, &sh,
                                (g1 - g0) * Tl));
     for (int h = g0; h < g1; ++h)
       GCHK(L, hipMemcpyAsync(ctxs[h]->tmo_h, ctxs[h]->ctl_d + 1, sizeof(unsigned), hipMemcpyDeviceToHost, L->st));
@@ -2037,7 +2137,7 @@ static TriArgs tri_one(const double* linv) {
 
 int nngp_ancillary_propose(nngp_ctx* c, double beta0, double dlog_scale) {
   if (!c) return NNGP_ERR_ARG;
-  { int rs_ = replica_sync(c); if (rs_) return rs_; }
+  { int rs_ = replica_fresh(c); if (rs_) return rs_; }
   ChainState& S = c->ch[c->cur];
   if (!S.have_factor[0] || !S.have_factor[1] || !S.have_field)
     return fail_msg(c, NNGP_ERR_STATE, "ancillary_propose: need both factors and the field");
@@ -2053,7 +2153,7 @@ int nngp_ancillary_propose(nngp_ctx* c, double beta0, double dlog_scale) {
 
 int nngp_ancillary_propose_chains(nngp_ctx* c, int chain_mask, const double* beta0, const double* dlog_scale) {
   if (!c || !beta0 || !dlog_scale || chain_mask <= 0 || chain_mask >= (1 << c->C)) return NNGP_ERR_ARG;
-  { int rs_ = replica_sync(c); if (rs_) return rs_; }
+  { int rs_ = replica_fresh(c); if (rs_) return rs_; }
   int rc;
   if ((rc = set_device(c))) return rc;
   TriArgs ta;
@@ -2099,7 +2199,7 @@ static int obs_enqueue(nngp_ctx* c, int k, int mode, double beta0, double lnv) {
 static int obs_chains(nngp_ctx* c, int mode, int chain_mask, const double* beta0, const double* lnv, double* out) {
   if (!c || !out || !beta0 || (mode == 1 && !lnv) || chain_mask <= 0 || chain_mask >= (1 << c->C))
     return NNGP_ERR_ARG;
-  { int rs_ = replica_sync(c); if (rs_) return rs_; }
+  { int rs_ = replica_fresh(c); if (rs_) return rs_; }
   int rc;
   if ((rc = set_device(c))) return rc;
   for (int k = 0; k < c->C; ++k)
@@ -2129,7 +2229,7 @@ int nngp_field_response_ratio_chains(nngp_ctx* c, int chain_mask, const double* 
 
 int nngp_accept_field(nngp_ctx* c) {
   if (!c) return NNGP_ERR_ARG;
-  { int rs_ = replica_sync(c); if (rs_) return rs_; }
+  { int rs_ = replica_fresh(c); if (rs_) return rs_; }
   int rc;
   if ((rc = set_device(c))) return rc;
   ChainState& S = c->ch[c->cur];
@@ -2140,7 +2240,7 @@ int nngp_accept_field(nngp_ctx* c) {
 
 int nngp_beta0_stats(nngp_ctx* c, double* oqo, double* oqf) {
   if (!c || !oqo || !oqf) return NNGP_ERR_ARG;
-  { int rs_ = replica_sync(c); if (rs_) return rs_; }
+  { int rs_ = replica_fresh(c); if (rs_) return rs_; }
   ChainState& S = c->ch[c->cur];
   if (!S.have_factor[0] || !S.have_field) return fail_msg(c, NNGP_ERR_STATE, "beta0_stats: need factor and field");
   // a log-likelihood pass over the current factor and field already has

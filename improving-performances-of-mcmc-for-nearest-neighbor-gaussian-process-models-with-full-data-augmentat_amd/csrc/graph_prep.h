@@ -108,7 +108,8 @@ constexpr int kTileSlotsMax = 256;      // slots per own batch
 struct TileBatch { int off, R, nslots, slot0, nthr; };
 
 struct TileLayout {
-  int n = 0, b = 0, K = 0, T = 0, NT = 0, RMAX = 0;
+  int n = 0, b = 0, K = 0, T = 0, NT = 0, RMAX = 0;  // NT: cell threads of a batch (the stream width)
+  int NTK = 0;                       // threads of the sweep workgroup (NT, or NT + 64: exchange wave)
   long long nnz = 0;
   int max_rows = 0;                  // max |E_t|
   int max_batches = 0;               // max own batches of a tile

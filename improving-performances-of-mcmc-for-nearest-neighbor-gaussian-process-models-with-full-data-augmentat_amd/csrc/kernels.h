@@ -168,6 +168,8 @@ struct TileDev {
   int K, C, T, n;
   int max_gslots;             // max foreign slots of a (tile, colour): LDS of their dw
   int probe = 0;              // dbg layout: 1 = per-tile segment sums (T x 8), 2 = timeline (T x 512 phases x 8)
+  int xw = 0;                 // exchange-wave tiles: the last wave polls the hand-offs, the
+                              // layout's batches are cut for NT - 64 cell threads
 };
 
 struct TileLaunch {
@@ -204,12 +206,15 @@ struct TileShard {
   const unsigned* call = nullptr;    // call-id word of the launch (every rank tags with the same id)
   double* gx[kTileRanksMax] = {};    // granule buffer of every rank (this process's mapping)
 };
+// occ != nullptr: no launch; *occ = workgroups of the instantiation this call
+// would launch that are resident on one CU at once (occupancy query)
 hipError_t launch_sweep_tiles(hipStream_t st, const TileDev& D, const TileLaunch& a, int max_rows, int NT,
-                              int max_batches, int max_gslots, const TileShard* sh = nullptr, int grid = 0);
+                              int max_batches, int max_gslots, const TileShard* sh = nullptr, int grid = 0,
+                              int* occ = nullptr);
 // chain-split launch: D.C one-chain workgroups per tile (256-thread layouts,
 // one GPU), the chains' phases interleaved on each CU
 hipError_t launch_sweep_tiles_cs(hipStream_t st, const TileDev& D, const TileLaunch& a, int max_rows, int NT,
-                                 int max_batches, int max_gslots);
+                                 int max_batches, int max_gslots, int* occ = nullptr);
 // ctl[0] += 1 (call id), ctl[1] = 0 (timeout word): before every launch of a rank
 hipError_t launch_tile_call_bump(hipStream_t st, unsigned* ctl);
 // tile shard, w exchange by peer copies instead of RCCL: signal the peers

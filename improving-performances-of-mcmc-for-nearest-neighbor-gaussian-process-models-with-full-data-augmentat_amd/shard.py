@@ -5,7 +5,10 @@ Two engines behind the same interface (nngp_ctx_info's sweep_engine):
  - tile shard (default when the tile layout fits): the persistent tile sweep
    with its tiles split over the ranks; the draws other ranks' tiles read are
    written straight into their granule buffers (peer memory over xGMI, HIP
-   IPC), one launch per call, then one RCCL broadcast of every rank's slots;
+   IPC), one launch per call, then each rank's halo slots into the peers'
+   replicas (peer stores + device flags; the full exchange at sync(), which
+   every reader of the field calls first -- collective); with an RCCL
+   communicator, one broadcast of every rank's slots per call instead;
  - colour shard (NNGP_ENGINE=colors, or when the tiles do not fit): one
    launch per colour and an RCCL all-gather of the colour's values.
 
@@ -66,6 +69,34 @@ class ShardContext(ChainContext):
         """Tile shard: map the other ranks' granule buffers (handles in rank order)."""
         assert len(handles) == self.n_ranks and all(len(h) == IPC_HANDLE_BYTES for h in handles)
         self._chk(lib.nngp_shard_ipc_open(self._h, b"".join(handles), IPC_HANDLE_BYTES))
+
+
+    def sync(self) -> None:
+        """Collective over the ranks (tile shard without a communicator): the
+        full exchange of the field replicas (nngp_shard_sync); a no-op when
+        the replica is up to date."""
+        self._chk(lib.nngp_shard_sync(self._h))
+
+
+# The library refuses to read a stale replica (nngp_shard_sync is explicit);
+# in Python every reader of the field syncs first, so on a tile shard without
+# a communicator these methods are collective: every rank calls them, in the
+# same order relative to its sweeps (SPMD).
+def _sync_first(name):
+    base = getattr(ChainContext, name)
+
+    def f(self, *a, **kw):
+        self.sync()
+        return base(self, *a, **kw)
+
+    f.__name__, f.__doc__ = name, (base.__doc__ or "") + " (collective on a tile shard: syncs the replicas first)"
+    return f
+
+
+for _name in ("get_field", "record_field", "loglik", "loglik_chains", "ancillary_propose", "ancillary_propose_chains",
+              "accept_field", "beta0_stats", "field_response_ratio", "field_response_ratio_chains",
+              "sum_squared_residuals", "sum_squared_residuals_chains"):
+    setattr(ShardContext, _name, _sync_first(_name))
 
 
 def shard_unique_id() -> bytes:

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define NNGP_ABI_VERSION 8
+#define NNGP_ABI_VERSION 9
 #define NNGP_SHARD_ID_BYTES 128 /* RCCL unique id */
 #define NNGP_IPC_HANDLE_BYTES 192 /* HIP IPC handles of a tile shard's granule buffer, w replica, flags */
 
@@ -109,6 +109,13 @@ typedef struct {
   int tile_ghost_cells_max;  /* tile engine: most ghost cells of one (tile, colour) */
   int tile_r_global;         /* tile engine: 1 = the tiles' r in global memory (layout beyond the LDS) */
   int tile_chain_split;      /* tile engine: 1 = one workgroup per (chain, tile), the chains of a tile on one CU */
+  int tile_resident_per_cu;  /* tile engine: workgroups of its kernel resident per CU at once (occupancy query);
+                                the persistent launch needs tiles <= this x CUs, else the colour engine runs */
+  int engine_fallback;       /* why not the tile engine: 0 = it runs, 1 = layout unsuitable (LDS, shape),
+                                2 = residency (more tile workgroups than fit the device at once),
+                                3 = NNGP_ENGINE=colors / more ranks than the tile shard takes */
+  int tile_exchange_wave;    /* tile engine: 1 = the last wave of each tile polls the hand-offs (NT - 64 cell threads) */
+  int device_cus;            /* compute units of the context's device */
 } nngp_info;
 
 /* ---------- library ---------- */
@@ -138,6 +145,9 @@ int nngp_set_chain(nngp_ctx* ctx, int chain);
 void nngp_ctx_destroy(nngp_ctx* ctx);
 const char* nngp_ctx_last_error(const nngp_ctx* ctx);
 int nngp_ctx_info(const nngp_ctx* ctx, nngp_info* info);
+/* one line: the sweep engine chosen at creation and why (e.g. the residency
+ * or LDS reason the tile engine was not used); owned by the context */
+const char* nngp_ctx_engine_note(const nngp_ctx* ctx);
 
 /* Vecchia factor (A4).  which: 0 = current factor, 1 = proposal. */
 int nngp_factor(nngp_ctx* ctx, int which, int covfun, const double* covparms, int ncovparms);
@@ -252,16 +262,30 @@ int nngp_sweep_chains_group(nngp_ctx** ctxs, int n_ranks, int n_sweeps, const do
  * (rank g runs tiles [g*T/G, (g+1)*T/G) on its GPU).  A draw read by a tile
  * of another rank is written into that rank's granule buffer (peer memory
  * over xGMI) by the producing tile, so the hand-offs stay inside the one
- * persistent launch per call; after it, every rank's own slots reach the
- * others (RCCL broadcasts).  Before the first sweep, after
- * nngp_shard_comm_init: every rank exports its buffer's handle, the handles
- * are exchanged out of band (all-gather), and every rank opens the others'.
- * NNGP_ENGINE=colors at creation selects the colour shard instead. */
+ * persistent launch per call.  After the launch the ranks' replicas of the
+ * field are brought up to date: with a communicator (nngp_shard_comm_init),
+ * one grouped RCCL broadcast of every rank's slots; without one (the
+ * default), each rank stores only its halo -- its slots that other ranks'
+ * rows contain -- into the peers' replicas (peer stores + device flags), and
+ * the other foreign slots of each replica fall behind until nngp_shard_sync.
+ * Setup, every rank: export this rank's handles (nngp_shard_ipc_handle),
+ * exchange them out of band (all-gather), open the others'
+ * (nngp_shard_ipc_open).  NNGP_ENGINE=colors at creation selects the colour
+ * shard instead. */
 int nngp_shard_ipc_handle(nngp_ctx* ctx, unsigned char* handle, int len);
 /* handles: n_ranks x len_each bytes, rank order (this rank's entry ignored).
  * Without a communicator (no nngp_shard_comm_init) a call exchanges w by
  * peer copies into the mapped replicas and device flags instead of RCCL. */
 int nngp_shard_ipc_open(nngp_ctx* ctx, const unsigned char* handles, int len_each);
+/* Collective over the ranks of a tile shard without a communicator (every
+ * rank calls it, in the same order relative to its sweeps): the full
+ * exchange of the field replicas.  After sweeps without it, the entry points
+ * that read the field (nngp_get_field, nngp_record_field, nngp_loglik*,
+ * nngp_beta0_stats, nngp_field_response_ratio*, nngp_sum_squared_residuals*,
+ * nngp_ancillary_propose*, nngp_accept_field) return NNGP_ERR_STATE -- a
+ * reader never performs a hidden collective.  A no-op on every other
+ * context and on an up-to-date replica. */
+int nngp_shard_sync(nngp_ctx* ctx);
 
 /* ---------- measurement ---------- */
 /* nngp_sweep_chains bracketed by HIP events on the context's stream;

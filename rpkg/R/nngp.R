@@ -44,6 +44,8 @@ nngp_context_shard <- function(locs, NNarray, coloring, locs_match, observed_fie
 }
 nngp_destroy <- function(ctx) invisible(.Call(C_nngp_ctx_destroy, ctx))
 nngp_info <- function(ctx) .Call(C_nngp_ctx_info, ctx)
+# the sweep engine chosen at creation and why (tile residency / LDS fallbacks)
+nngp_engine_note <- function(ctx) .Call(C_nngp_ctx_engine_note, ctx)
 nngp_set_chain <- function(ctx, chain) invisible(.Call(C_nngp_set_chain, ctx, as.integer(chain)))
 
 nngp_factor <- function(ctx, which, covfun_name, covparms)
@@ -105,6 +107,9 @@ nngp_sum_squared_residuals_chains <- function(ctx, chain_mask, beta_0)
   .Call(C_nngp_sum_squared_residuals_chains, ctx, as.integer(chain_mask), as.double(beta_0))
 nngp_shard_ipc_handle <- function(ctx) .Call(C_nngp_shard_ipc_handle, ctx)
 nngp_shard_ipc_open <- function(ctx, handles) invisible(.Call(C_nngp_shard_ipc_open, ctx, handles))
+# collective over the ranks of a tile shard: full exchange of the replicas
+# (the readers of the field refuse a stale replica)
+nngp_shard_sync <- function(ctx) invisible(.Call(C_nngp_shard_sync, ctx))
 nngp_sweep_chains_group <- function(ctxs, n_sweeps, beta_0, log_scale, log_noise_variance, seed, counter_base)
   invisible(.Call(C_nngp_sweep_chains_group, ctxs, as.integer(n_sweeps), as.double(beta_0), as.double(log_scale),
                   as.double(log_noise_variance), as.double(seed), as.double(counter_base)))

@@ -61,8 +61,24 @@ static double as_real(SEXP x) { return Rf_asReal(x); }
 static const double* rptr(SEXP x) { return TYPEOF(x) == NILSXP ? NULL : REAL(x); }
 
 static void to_u64(SEXP x, uint64_t* out, int n) {
-  if (XLENGTH(x) < n) Rf_error("nngp: need %d seeds / counters", n);
+  if (TYPEOF(x) != REALSXP || XLENGTH(x) != n) Rf_error("nngp: need %d seeds / counters (double)", n);
   for (int k = 0; k < n; ++k) out[k] = (uint64_t)REAL(x)[k];
+}
+
+/* chains of the context */
+static int ctx_chains(nngp_ctx* c) {
+  nngp_info inf;
+  check(nngp_ctx_info(c, &inf), c);
+  return inf.n_chains;
+}
+
+/* a per-chain argument: a double vector with one entry per chain of the
+ * context (the library reads every chain's entry; R's recycling does not
+ * apply across the boundary) */
+static const double* per_chain(SEXP x, int k, const char* what) {
+  if (TYPEOF(x) != REALSXP || XLENGTH(x) != k)
+    Rf_error("nngp: %s must be a double vector with one entry per chain (%d)", what, k);
+  return REAL(x);
 }
 
 /* ---------- library ---------- */
@@ -128,6 +144,8 @@ SEXP C_nngp_set_chain(SEXP p, SEXP chain) {
   return R_NilValue;
 }
 
+SEXP C_nngp_ctx_engine_note(SEXP p) { return Rf_mkString(nngp_ctx_engine_note(get_ctx(p))); }
+
 SEXP C_nngp_ctx_info(SEXP p) {
   nngp_ctx* c = get_ctx(p);
   nngp_info inf;
@@ -136,13 +154,15 @@ SEXP C_nngp_ctx_info(SEXP p) {
                       "n_chains", "lanes_per_chain", "n_chunks", "sweep_engine", "n_tiles", "tile_rows_max",
                       "n_ghost_cells", "n_ranks", "rank", "shard_owned", "shard_needed_rows",
                       "shard_exchange_slots", "tile_ghost_pass", "tile_ghost_cells_max", "tile_r_global",
-                      "tile_chain_split"};
+                      "tile_chain_split", "tile_resident_per_cu", "engine_fallback", "tile_exchange_wave",
+                      "device_cus"};
   const double v[] = {inf.n, inf.b, inf.d, inf.n_obs, inf.n_colors, inf.n_levels, (double)inf.nnz,
                       (double)inf.n_entries, inf.max_collen, inf.device, inf.n_chains, inf.lanes_per_chain,
                       inf.n_chunks, inf.sweep_engine, inf.n_tiles, inf.tile_rows_max, (double)inf.n_ghost_cells,
                       inf.n_ranks, inf.rank, (double)inf.shard_owned, (double)inf.shard_needed_rows,
                       (double)inf.shard_exchange_slots, inf.tile_ghost_pass, inf.tile_ghost_cells_max,
-                      inf.tile_r_global, inf.tile_chain_split};
+                      inf.tile_r_global, inf.tile_chain_split, inf.tile_resident_per_cu, inf.engine_fallback,
+                      inf.tile_exchange_wave, inf.device_cus};
   const int k = (int)(sizeof v / sizeof v[0]);
   SEXP out = PROTECT(Rf_allocVector(REALSXP, k)), names = PROTECT(Rf_allocVector(STRSXP, k));
   for (int i = 0; i < k; ++i) {
@@ -264,11 +284,12 @@ SEXP C_nngp_sweep_chains(SEXP p, SEXP n_sweeps, SEXP beta0, SEXP log_scale, SEXP
                          SEXP counter_base) {
   nngp_ctx* c = get_ctx(p);
   uint64_t s[4], cb[4];
-  const int k = (int)XLENGTH(beta0);
-  if (k < 1 || k > 4) Rf_error("nngp: 1..4 chains per context");
+  const int k = ctx_chains(c);
+  const double *b0 = per_chain(beta0, k, "beta0"), *ls = per_chain(log_scale, k, "log_scale"),
+               *nv = per_chain(lnv, k, "log_noise_variance");
   to_u64(seed, s, k);
   to_u64(counter_base, cb, k);
-  check(nngp_sweep_chains(c, as_int(n_sweeps), REAL(beta0), REAL(log_scale), REAL(lnv), s, cb), c);
+  check(nngp_sweep_chains(c, as_int(n_sweeps), b0, ls, nv, s, cb), c);
   return R_NilValue;
 }
 
@@ -276,12 +297,13 @@ SEXP C_nngp_sweep_timed(SEXP p, SEXP n_sweeps, SEXP beta0, SEXP log_scale, SEXP 
                         SEXP counter_base) {
   nngp_ctx* c = get_ctx(p);
   uint64_t s[4], cb[4];
-  const int k = (int)XLENGTH(beta0);
-  if (k < 1 || k > 4) Rf_error("nngp: 1..4 chains per context");
+  const int k = ctx_chains(c);
+  const double *b0 = per_chain(beta0, k, "beta0"), *ls = per_chain(log_scale, k, "log_scale"),
+               *nv = per_chain(lnv, k, "log_noise_variance");
   to_u64(seed, s, k);
   to_u64(counter_base, cb, k);
   double ms = 0, kms = 0;
-  check(nngp_sweep_timed(c, as_int(n_sweeps), REAL(beta0), REAL(log_scale), REAL(lnv), s, cb, &ms, &kms), c);
+  check(nngp_sweep_timed(c, as_int(n_sweeps), b0, ls, nv, s, cb, &ms, &kms), c);
   SEXP out = PROTECT(Rf_allocVector(REALSXP, 2));
   REAL(out)[0] = ms;
   REAL(out)[1] = kms;
@@ -297,7 +319,10 @@ SEXP C_nngp_ancillary_propose(SEXP p, SEXP beta0, SEXP dlog_scale) {
 
 SEXP C_nngp_ancillary_propose_chains(SEXP p, SEXP chain_mask, SEXP beta0, SEXP dlog_scale) {
   nngp_ctx* c = get_ctx(p);
-  check(nngp_ancillary_propose_chains(c, as_int(chain_mask), REAL(beta0), REAL(dlog_scale)), c);
+  const int k = ctx_chains(c);
+  check(nngp_ancillary_propose_chains(c, as_int(chain_mask), per_chain(beta0, k, "beta0"),
+                                      per_chain(dlog_scale, k, "dlog_scale")),
+        c);
   return R_NilValue;
 }
 
@@ -377,11 +402,12 @@ SEXP C_nngp_sweep_chains_group(SEXP ctxs, SEXP n_sweeps, SEXP beta0, SEXP log_sc
   nngp_ctx* cs[64];
   for (int g = 0; g < G; ++g) cs[g] = get_ctx(VECTOR_ELT(ctxs, g));
   uint64_t s[4], cb[4];
-  const int k = (int)XLENGTH(beta0);
-  if (k < 1 || k > 4) Rf_error("nngp: 1..4 chains per context");
+  const int k = ctx_chains(cs[0]);
+  const double *b0 = per_chain(beta0, k, "beta0"), *ls = per_chain(log_scale, k, "log_scale"),
+               *nv = per_chain(lnv, k, "log_noise_variance");
   to_u64(seed, s, k);
   to_u64(counter_base, cb, k);
-  check(nngp_sweep_chains_group(cs, G, as_int(n_sweeps), REAL(beta0), REAL(log_scale), REAL(lnv), s, cb), cs[0]);
+  check(nngp_sweep_chains_group(cs, G, as_int(n_sweeps), b0, ls, nv, s, cb), cs[0]);
   return R_NilValue;
 }
 
@@ -393,6 +419,12 @@ SEXP C_nngp_shard_ipc_handle(SEXP p) {
   check(nngp_shard_ipc_handle(c, RAW(h), NNGP_IPC_HANDLE_BYTES), c);
   UNPROTECT(1);
   return h;
+}
+
+SEXP C_nngp_shard_sync(SEXP p) {
+  nngp_ctx* c = get_ctx(p);
+  check(nngp_shard_sync(c), c);
+  return R_NilValue;
 }
 
 SEXP C_nngp_shard_ipc_open(SEXP p, SEXP handles) {
@@ -437,8 +469,10 @@ static SEXP chains_out(nngp_ctx* c) {
 
 SEXP C_nngp_loglik_chains(SEXP p, SEXP which, SEXP mask, SEXP beta0, SEXP log_scale) {
   nngp_ctx* c = get_ctx(p);
+  const int k = ctx_chains(c);
+  const double *b0 = per_chain(beta0, k, "beta0"), *ls = per_chain(log_scale, k, "log_scale");
   SEXP out = PROTECT(chains_out(c));
-  const int rc = nngp_loglik_chains(c, as_int(which), as_int(mask), REAL(beta0), REAL(log_scale), REAL(out));
+  const int rc = nngp_loglik_chains(c, as_int(which), as_int(mask), b0, ls, REAL(out));
   UNPROTECT(1);
   check(rc, c);
   return out;
@@ -446,8 +480,10 @@ SEXP C_nngp_loglik_chains(SEXP p, SEXP which, SEXP mask, SEXP beta0, SEXP log_sc
 
 SEXP C_nngp_field_response_ratio_chains(SEXP p, SEXP mask, SEXP beta0, SEXP lnv) {
   nngp_ctx* c = get_ctx(p);
+  const int k = ctx_chains(c);
+  const double *b0 = per_chain(beta0, k, "beta0"), *nv = per_chain(lnv, k, "log_noise_variance");
   SEXP out = PROTECT(chains_out(c));
-  const int rc = nngp_field_response_ratio_chains(c, as_int(mask), REAL(beta0), REAL(lnv), REAL(out));
+  const int rc = nngp_field_response_ratio_chains(c, as_int(mask), b0, nv, REAL(out));
   UNPROTECT(1);
   check(rc, c);
   return out;
@@ -455,8 +491,9 @@ SEXP C_nngp_field_response_ratio_chains(SEXP p, SEXP mask, SEXP beta0, SEXP lnv)
 
 SEXP C_nngp_sum_squared_residuals_chains(SEXP p, SEXP mask, SEXP beta0) {
   nngp_ctx* c = get_ctx(p);
+  const double* b0 = per_chain(beta0, ctx_chains(c), "beta0");
   SEXP out = PROTECT(chains_out(c));
-  const int rc = nngp_sum_squared_residuals_chains(c, as_int(mask), REAL(beta0), REAL(out));
+  const int rc = nngp_sum_squared_residuals_chains(c, as_int(mask), b0, REAL(out));
   UNPROTECT(1);
   check(rc, c);
   return out;
@@ -476,6 +513,8 @@ static const R_CallMethodDef call_methods[] = {
     E(C_nngp_ctx_last_error, 1),
     E(C_nngp_set_chain, 2),
     E(C_nngp_ctx_info, 1),
+    E(C_nngp_ctx_engine_note, 1),
+    E(C_nngp_shard_sync, 1),
     E(C_nngp_factor, 4),
     E(C_nngp_get_linv, 2),
     E(C_nngp_set_linv, 3),

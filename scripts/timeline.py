@@ -51,6 +51,10 @@ for nm, a in (("own->publish", own), ("publish->scattered", scat - pub), ("scatt
               ("prepped->handoff", hand - landed),
               ("handoff->end", tail), ("phase", dur)):
     print(f"  {nm:18s} mean {a.mean():6.2f}  p90 {np.percentile(a, 90, axis=0).mean():6.2f}  max {a.max(axis=0).mean():6.2f}")
+xwd = raw[..., 7].astype(np.float64)
+if (xwd > 0).any():  # exchange-wave tiles: the wave's polls done (stamp 7)
+    xw = np.where(xwd > 0, xwd / 100.0 - raw[:, 0, 0].astype(np.float64).min() / 100.0, hand)
+    print(f"  xw polls done - publish: mean {(xw - pub).mean():6.2f}  p90 {np.percentile(xw - pub, 90):6.2f}")
 print(f"  poll spins (max over the tile's threads): mean {spins.mean():.2f}, p90 {np.percentile(spins, 90):.0f}, "
       f"share of phases with spins {(spins > 0).mean():.2f}")
 # critical path: per phase, the spread of publish times across tiles

@@ -81,16 +81,21 @@ def heavy():
 # tiles (NNGP_TILES=24: every small test problem has halos, neighbour
 # hand-offs and several tiles per XCD; contexts whose 24-tile layout does not
 # fit a CU's LDS fall back to colour launches, as in production);
-# "tiles-default" = the production engine choice and tile count.  GPU test modules that exercise the sweep run under all three.
+# "tiles-default" = the production engine choice and tile count (exchange-wave
+# tiles: the last wave of each tile polls the hand-offs); "tiles-classic" =
+# the same tiles without the exchange wave (NNGP_TILE_XW=0: every wave polls).
+# GPU test modules that exercise the sweep run under all four.
 ENGINES = {"colors": {"NNGP_ENGINE": "colors"},
            "tiles": {"NNGP_TILES": "24"},  # automatic: colours where 24 tiles exceed the LDS
-           "tiles-default": {}}
+           "tiles-default": {},
+           "tiles-classic": {"NNGP_TILE_XW": "0"}}
 
 
 @pytest.fixture(params=list(ENGINES))
 def engine(request, monkeypatch):
     monkeypatch.delenv("NNGP_TILES", raising=False)
     monkeypatch.delenv("NNGP_ENGINE", raising=False)
+    monkeypatch.delenv("NNGP_TILE_XW", raising=False)
     for k, v in ENGINES[request.param].items():
         monkeypatch.setenv(k, v)
     return request.param

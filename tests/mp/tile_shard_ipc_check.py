@@ -56,20 +56,39 @@ def main():
     assert info["sweep_engine"] == 1 and info["n_ranks"] == world and info["n_tiles"] == TILES, info
     init_shard_comm(ctx, dist, rccl=False)
     setup(ctx)
-    got = []
+    # the calls back to back, nothing read in between: the second call's
+    # prologue runs on replicas that only the halo-only exchange after the
+    # first call updated (no full exchange until the read below syncs); then
+    # one more call after that full exchange
     for b0, ls, lnv, seed, cb, ns in calls:
         ctx.sweep_chains(ns, b0, ls, lnv, seed, cb)
-        got.append(read(ctx))
+    stale = True
+    try:  # the library refuses to read a stale replica (nngp_shard_sync is explicit)
+        from nngp_amd._lib import NNGPError, lib
+
+        st = lib.nngp_get_field(ctx._h, np.zeros(n))
+        stale = st != 0
+    except NNGPError:
+        pass
+    assert stale, "a stale replica was read without nngp_shard_sync"
+    got = [read(ctx)]  # ShardContext readers sync first (collective)
+    b0, ls, lnv, seed, cb, ns = calls[0]
+    ctx.sweep_chains(ns, b0, ls, lnv, seed, [x + 5 for x in cb])
+    got.append(read(ctx))
     dist.barrier()
     ctx.close()
     if rank == 0:
         ref = P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=C)
         assert ref.info["n_tiles"] == TILES
         setup(ref)
-        for (b0, ls, lnv, seed, cb, ns), g in zip(calls, got):
+        for b0, ls, lnv, seed, cb, ns in calls:
             ref.sweep_chains(ns, b0, ls, lnv, seed, cb)
-            for k, f in enumerate(read(ref)):
-                assert np.array_equal(f, g[k]), (k, np.abs(f - g[k]).max())
+        for k, f in enumerate(read(ref)):
+            assert np.array_equal(f, got[0][k]), (k, np.abs(f - got[0][k]).max())
+        b0, ls, lnv, seed, cb, ns = calls[0]
+        ref.sweep_chains(ns, b0, ls, lnv, seed, [x + 5 for x in cb])
+        for k, f in enumerate(read(ref)):
+            assert np.array_equal(f, got[1][k]), (k, np.abs(f - got[1][k]).max())
         ref.close()
         print(f"ok tile shard over {world} processes on one GPU == one context, bitwise "
               f"(n={n}, {C} chains, {TILES} tiles, {info['shard_exchange_slots']} exchanged slots)", flush=True)

@@ -597,6 +597,46 @@ def test_tile_engine_multipass_ghost_cells(P, O, C, monkeypatch):
         np.testing.assert_allclose(got[k], ref, rtol=1e-8, atol=1e-9, err_msg=f"chain {k}")
 
 
+@pytest.mark.parametrize("xw", ["0", "1"])
+def test_tile_residency_fallback(P, O, monkeypatch, xw):
+    """More tiles than the device holds at once (NNGP_TILES = 2 x CUs): the
+    persistent tile sweep spins on its neighbours' granules, so it needs
+    every workgroup resident.  The occupancy query at creation sees that the
+    grid does not fit and the context runs the colour engine instead, saying
+    why (engine_fallback 2, the note names the residency) -- no spin timeout --
+    and the sweep still equals the oracle's."""
+    monkeypatch.delenv("NNGP_ENGINE", raising=False)
+    monkeypatch.setenv("NNGP_TILE_XW", xw)
+    n, m = 40_000, 10
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=33)
+    with P.ChainContext(locs, NN, col, lm, y, device=0) as ctx:
+        cus = ctx.info["device_cus"]
+    assert cus > 0
+    monkeypatch.setenv("NNGP_TILES", str(2 * cus))
+    field = np.random.default_rng(3).normal(size=n)
+    with P.ChainContext(locs, NN, col, lm, y, device=0) as ctx:
+        info = ctx.info
+        assert info["sweep_engine"] == 0 and info["engine_fallback"] == 2, info
+        assert "residency" in info["engine_note"], info["engine_note"]
+        ctx.factor(0, "exponential_isotropic", [1.0, 0.1, 0.0])
+        L = ctx.get_linv(0)
+        ctx.set_field(field)
+        ctx.set_mu(None, 0.2)
+        ctx.sweep_chains(2, [0.2], [0.1], [-0.4], [9], [0])
+        got = ctx.get_field()
+    z = O.sweep_normals(9, 0, 2, n)
+    ref = O.sweep("local", field, L, NN, col, O.precision_diag(L, NN), np.ones(n, np.int32), y, np.full(n, 0.2), lm,
+                  0.2, 0.1, -0.4, z)
+    np.testing.assert_allclose(got, ref, rtol=1e-8, atol=1e-9)
+    # at one tile per CU the tile engine runs, with its occupancy on record
+    monkeypatch.setenv("NNGP_TILES", str(cus))
+    with P.ChainContext(locs, NN, col, lm, y, device=0) as ctx:
+        info = ctx.info
+        assert info["sweep_engine"] == 1 and info["engine_fallback"] == 0, info
+        assert info["tile_resident_per_cu"] >= 1 and info["tile_exchange_wave"] == int(xw), info
+        assert "tiles:" in info["engine_note"], info["engine_note"]
+
+
 @pytest.mark.parametrize("n,m,C", [(20000, 10, 1), (60000, 15, 3), (3000, 5, 2), (40000, 20, 4)])
 def test_tile_engine_r_in_global_memory_equals_lds_bitwise(P, engine, monkeypatch, n, m, C):
     """Tiles whose r lives in global memory (the layout beyond the LDS: n = 1e7
@@ -728,7 +768,7 @@ def test_tile_engine_chain_split_equals_joint_bitwise(P, engine, monkeypatch, n,
         monkeypatch.setenv("NNGP_TILE_CHAINS", mode)
         with P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=C) as ctx:
             info = ctx.info
-            assert info["sweep_engine"] == 1 and info["tile_chain_split"] == int(mode == "split"), info
+            assert info["sweep_engine"] == 1 and info["tile_chain_split"] == int(mode == "split"), info["engine_note"]
             for k in range(C):
                 ctx.select(k)
                 ctx.factor(0, "matern15_isotropic", [1.0, 0.05 + 0.01 * k, 0.0])

@@ -1,7 +1,12 @@
-"""The bench's N>1 path on CPU: world_size-2 gloo processes (127.0.0.1) run
-the contract's timed region; every rank must report the MAX elapsed over
-ranks, and the per-rank workloads (seeds) must differ (weak scaling: each
-rank sweeps its own chains, no data-path collective)."""
+"""The bench's N>1 paths on CPU, world_size-2 gloo processes (127.0.0.1):
+the contract's timed region reports the MAX elapsed over ranks on every
+rank; --multi replicas gives every rank its own workload and chain seeds;
+the sharded sweep's bootstrap (RCCL id, IPC handles of the tile shard's
+granule buffers) is agreed over the group; and a sharded measurement that
+fails on any rank prints a null value on rank 0 (no replicas substituted).
+The sharded sweep itself -- tile shard: device-initiated granule stores into
+the peers' buffers over xGMI; colour shard: one RCCL all-gather per colour --
+needs GPUs (tests/test_gpu_tile_shard.py, tests/test_gpu_shard.py)."""
 import os
 import sys
 import time
@@ -52,10 +57,85 @@ def test_two_rank_timed_region_reports_max_over_ranks():
     assert all(ctr == 12 for _, _, ctr in out)      # warmup 2 + timed 10 steps
 
 
+def _seed_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    wseed, seeds = bench.replica_seeds(dist.get_rank(), 3)
+    mine = torch.tensor([wseed] + seeds, dtype=torch.int64)
+    allv = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allv, mine)
+    q.put((rank, [v.tolist() for v in allv]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
 def test_rank_workloads_differ():
-    """Each rank draws its own synthetic field and chain seeds (bench.main)."""
-    src = (ROOT / "bench.py").read_text()
-    assert "seed=1000 + rank" in src and "77 + 10 * rank + k" in src
+    """--multi replicas: the ranks' workload seeds and chain seeds (bench.replica_seeds,
+    what bench.main uses) gathered over the group are pairwise distinct."""
+    world, port = 2, 31500 + os.getpid() % 1000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_seed_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert out[0] == out[1]
+    flat = [x for v in out[0] for x in v]
+    assert len(set(flat)) == len(flat)
+
+
+def _shard_fail_worker(rank, world, port, q):
+    import contextlib
+    import io
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    def fake_shard_main(P, args, world, rank, local_rank, dist, scaling):
+        if rank == 1:
+            raise RuntimeError("hipIpcOpenMemHandle: invalid argument")
+        return {"metric": bench.METRIC, "value": 123.0}
+
+    bench.shard_main = fake_shard_main
+    sys.argv = ["bench.py", "--gpus", str(world)]
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        bench.main()
+    q.put((rank, buf.getvalue()))
+
+
+@pytest.mark.timeout(180)
+def test_failed_shard_prints_null_value():
+    """bench.py at N = 2 (default --multi shard-weak): the sharded measurement
+    fails on rank 1; rank 0 prints ONE line with a null value, the error, and
+    no replicas measurement in its place."""
+    import json
+
+    world, port = 2, 32500 + os.getpid() % 1000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_shard_fail_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=170) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert out[1].strip() == ""
+    lines = out[0].strip().splitlines()
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["value"] is None and d["n_gpus"] == 2 and d["scaling"] == "weak"
+    assert "failed" in d["config"]["error"]
 
 
 def _bcast_worker(rank, world, port, q):
