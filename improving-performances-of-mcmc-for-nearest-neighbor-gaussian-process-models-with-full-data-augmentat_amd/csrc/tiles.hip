@@ -265,6 +265,13 @@ __device__ __forceinline__ void tile_load_ghosts(const TileDev& D, int gb, int g
   }
 }
 
+// ghost adds of one register pass: r_k += B[k,j] dw_j.  The rows are
+// distinct (one foreign member per colour per row), so every read goes out
+// before any write (see tile_own_scatter)
+struct TileState;
+template <int C, int GMAX>
+__device__ __forceinline__ void tile_ghost_adds(TileState& S, const TileGhostRegs<C, GMAX>& gr);
+
 // per-workgroup state of the persistent sweep
 struct TileState {
   double* r_s;
@@ -289,6 +296,26 @@ struct TileState {
   int T, t, lane, wv, K, nph, ph;
   unsigned long long tp[8], t_prev;
 };
+
+template <int C, int GMAX>
+__device__ __forceinline__ void tile_ghost_adds(TileState& S, const TileGhostRegs<C, GMAX>& gr) {
+  double rv[GMAX][C], dv[GMAX][C];
+#pragma unroll
+  for (int k = 0; k < GMAX; ++k) {
+    const bool ok = gr.lr[k] >= 0;
+    const int row = ok ? gr.lr[k] : 0, x = ok ? gr.gx[k] : 0;
+#pragma unroll
+    for (int ch = 0; ch < C; ++ch) {
+      rv[k][ch] = S.r_s[row * C + ch];
+      dv[k][ch] = S.gdw_s[x * C + ch];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < GMAX; ++k)
+    if (gr.lr[k] >= 0)
+#pragma unroll
+      for (int ch = 0; ch < C; ++ch) S.r_s[gr.lr[k] * C + ch] = rv[k][ch] + gr.gv[k][ch] * dv[k][ch];
+}
 
 #define TSTAMP(S, k)                                                      \
   do {                                                                    \
@@ -340,6 +367,7 @@ __device__ __forceinline__ void tile_own_draw(const TileDev& D, const TileLaunch
   // this thread is complete at its last cell (-> acc_s); the thread's first
   // cells may continue a slot of earlier threads: its end (if here) waits for
   // the carry of those threads.
+  tile_cells_landed(b);
   double run[C], cont[C];
   int cont_q = -1;
   bool seen_start = false;
@@ -447,22 +475,56 @@ __device__ __forceinline__ void tile_own_draw(const TileDev& D, const TileLaunch
 
 // ... and its scatter r_k += B[k,i] dw_i (dw in acc_s).  Needs only the
 // batch's cells: its per-slot records may be overwritten by then.
+// The rows of a batch's cells are distinct (one member per colour per row),
+// so the reads of r and dw of a group of rows all go out before any write:
+// one LDS round trip per group instead of one per cell (the compiler cannot
+// see the distinctness and would order every read after the previous write)
 template <int C, int NT, int RMAX, int PROBE>
 __device__ __forceinline__ void tile_own_scatter(TileState& S, const TileBatchRegs<C, NT, RMAX>& b, int R) {
+  constexpr int GRP = RMAX < 4 ? RMAX : 4;  // rows per group (registers: 2 x GRP x C doubles)
   double* r_s = S.r_s;
   const double* acc_s = S.acc_s;
 #pragma unroll
-  for (int j = 0; j < RMAX; ++j) {
-    if (j < R) {
-      const uint32_t lr = tile_lr(b.pk[j]);
-      if (lr != kTPad) {
-        const int q = (int)((b.pk[j] >> 17) & 0x7FF);
+  for (int j0 = 0; j0 < RMAX; j0 += GRP) {
+    if (j0 >= R) break;
+    double rv[GRP][C], dv[GRP][C];
 #pragma unroll
-        for (int ch = 0; ch < C; ++ch) r_s[lr * C + ch] += b.v[j][ch] * acc_s[q * C + ch];
+    for (int jj = 0; jj < GRP; ++jj) {
+      const int j = j0 + jj;
+      const uint32_t lr = tile_lr(b.pk[j]);
+      const bool ok = j < R && lr != kTPad;
+      const int row = ok ? (int)lr : 0, q = ok ? (int)((b.pk[j] >> 17) & 0x7FF) : 0;
+#pragma unroll
+      for (int ch = 0; ch < C; ++ch) {
+        rv[jj][ch] = r_s[row * C + ch];
+        dv[jj][ch] = acc_s[q * C + ch];
+      }
+    }
+#pragma unroll
+    for (int jj = 0; jj < GRP; ++jj) {
+      const int j = j0 + jj;
+      const uint32_t lr = tile_lr(b.pk[j]);
+      if (j < R && lr != kTPad) {
+#pragma unroll
+        for (int ch = 0; ch < C; ++ch) r_s[lr * C + ch] = rv[jj][ch] + b.v[j][ch] * dv[jj][ch];
       }
     }
   }
   TSTAMP(S, 4);
+}
+
+// every cell register of the batch in place: the one wait for the batch's
+// loads goes here, where they have landed, instead of wherever a later
+// conditional use makes the compiler wait conservatively (vmcnt counts a
+// wave's loads in order: such a wait would cover every load issued since)
+template <int C, int NT, int RMAX>
+__device__ __forceinline__ void tile_cells_landed(const TileBatchRegs<C, NT, RMAX>& b) {
+#pragma unroll
+  for (int j = 0; j < RMAX; ++j) {
+    asm volatile("" ::"v"(b.pk[j]));
+#pragma unroll
+    for (int ch = 0; ch < C; ++ch) asm volatile("" ::"v"(b.v[j][ch]));
+  }
 }
 
 // one colour phase ph = sweep*K + c with `cur` holding its prepared first
@@ -587,11 +649,7 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
   }
   for (int gb = g0; gb < g1; gb += NT * GMAX) {
     if (gb != g0) tile_load_ghosts<C, NT, GMAX>(D, gb, g1, gr, t);
-#pragma unroll
-    for (int k = 0; k < GMAX; ++k)
-      if (gr.lr[k] >= 0)
-#pragma unroll
-        for (int ch = 0; ch < C; ++ch) S.r_s[gr.lr[k] * C + ch] += gr.gv[k][ch] * S.gdw_s[gr.gx[k] * C + ch];
+    tile_ghost_adds<C, GMAX>(S, gr);
   }
   // ---- 4. the next batch's draw scalars (registers only: no barrier needed
   // before them; the barrier below orders the ghost adds before the products)
@@ -697,11 +755,7 @@ __device__ __forceinline__ void tile_phase_ib(const TileDev& D, const TileLaunch
     }
     for (int gb = g0; gb < g1; gb += NT * GMAX) {
       if (gb != g0) tile_load_ghosts<C, NT, GMAX>(D, gb, g1, gr, t);
-#pragma unroll
-      for (int k = 0; k < GMAX; ++k)
-        if (gr.lr[k] >= 0)
-#pragma unroll
-          for (int ch = 0; ch < C; ++ch) S.r_s[gr.lr[k] * C + ch] += gr.gv[k][ch] * S.gdw_s[gr.gx[k] * C + ch];
+      tile_ghost_adds<C, GMAX>(S, gr);
     }
     __syncthreads();
   } else if (had_int && had_bnd) {
@@ -773,7 +827,9 @@ __device__ __forceinline__ void tile_phase_xw(const TileDev& D, TileState& S, in
   }
   // hand-off: every (foreign slot, chain) of colour c until its granule
   // carries this epoch -> gdw_s (polls in flight per lane; a retry waits for
-  // this wave's own polls only)
+  // this wave's own polls only).  (Measured and dropped: a train of 3 poll
+  // rounds in flight per item, 11.65k -> 10.5k chain-sweeps/s: the extra
+  // polls queue in the memory system in front of everyone's stream.)
   for (int u0 = 0; u0 < nfi; u0 += 64 * PB) {
     u32x4_t g[PB];
     int off[PB];
@@ -824,11 +880,7 @@ __device__ __forceinline__ void tile_phase_xw(const TileDev& D, TileState& S, in
   __syncthreads();
   for (int gb = g0; gb < g1; gb += NT * GMAX) {
     if (gb != g0) tile_load_ghosts<C, NT, GMAX>(D, gb, g1, gr, t);
-#pragma unroll
-    for (int k = 0; k < GMAX; ++k)
-      if (gr.lr[k] >= 0)
-#pragma unroll
-        for (int ch = 0; ch < C; ++ch) S.r_s[gr.lr[k] * C + ch] += gr.gv[k][ch] * S.gdw_s[gr.gx[k] * C + ch];
+    tile_ghost_adds<C, GMAX>(S, gr);
   }
   __syncthreads();
 }
@@ -879,7 +931,9 @@ __device__ __forceinline__ void tile_phase_cells(const TileDev& D, const TileLau
   }
   TLSTAMP(S, 6);
   // the next batch's draw scalars, then (one register set) its cells: they
-  // stream while the exchange wave waits for the neighbours
+  // stream while the exchange wave waits for the neighbours.  (Measured and
+  // dropped: the draw's w stores deferred behind the next records, 11.65k ->
+  // 10.5k chain-sweeps/s.)
   if (more) tile_prep_items<C, NTC, RMAX>(D, a, S.sc_s, S.seed_s, sn, nxt, t);
   if (!DB && more) tile_load_cells<C, NTC, RMAX>(D, S.batch_s[S.bptr_s[cn]], nxt, t);
   TLSTAMP(S, 4);
@@ -887,11 +941,7 @@ __device__ __forceinline__ void tile_phase_cells(const TileDev& D, const TileLau
   TLSTAMP(S, 2);
   for (int gb = g0; gb < g1; gb += NT * GMAX) {
     if (gb != g0) tile_load_ghosts<C, NT, GMAX>(D, gb, g1, gr, t);
-#pragma unroll
-    for (int k = 0; k < GMAX; ++k)
-      if (gr.lr[k] >= 0)
-#pragma unroll
-        for (int ch = 0; ch < C; ++ch) S.r_s[gr.lr[k] * C + ch] += gr.gv[k][ch] * S.gdw_s[gr.gx[k] * C + ch];
+    tile_ghost_adds<C, GMAX>(S, gr);
   }
   __syncthreads();
   TLSTAMP(S, 3);

@@ -645,6 +645,9 @@ def test_tile_engine_r_in_global_memory_equals_lds_bitwise(P, engine, monkeypatc
     calls (3 + 2 sweeps)."""
     if engine != "tiles-default":
         pytest.skip("sets the engine itself")
+    # the same 512-thread cell layout on both sides (exchange-wave tiles cut
+    # their batches for 448 cell threads, and r in global memory has none)
+    monkeypatch.setenv("NNGP_TILE_XW", "0")
     locs, NN, col, lm, y = make_problem(P, n, m, seed=n + C)
     rng = np.random.default_rng(C)
     fields = [rng.normal(size=n) for _ in range(C)]
