@@ -206,6 +206,16 @@ hipError_t dalloc(T** p, size_t count) {
   if (count == 0) count = 1;
   return hipMalloc((void**)p, sizeof(T) * count);
 }
+// the buffers other ranks of a tile shard store into over xGMI while this
+// rank's kernels read them (granules, the w replica, the exchange flags):
+// fine-grained device memory, coherent with the peers' stores (a coarse-
+// grained line of them held in this GPU's L2 could be read stale)
+template <typename T>
+hipError_t shared_alloc(T** p, size_t count, bool fine) {
+  if (count == 0) count = 1;
+  if (!fine) return hipMalloc((void**)p, sizeof(T) * count);
+  return hipExtMallocWithFlags((void**)p, sizeof(T) * count, hipDeviceMallocFinegrained);
+}
 template <typename T>
 hipError_t upload(T* dst, const T* src, size_t count, hipStream_t st) {
   if (count == 0) return hipSuccess;
@@ -776,7 +786,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     CK(dalloc(&c->nb_d, TL.nb.size()));
     CK(dalloc(&c->erow_ptr_d, TL.erow_ptr.size()));
     CK(dalloc(&c->erow_d, TL.erow.size()));
-    CK(dalloc(&c->dwx_d, (size_t)n * C * 2));
+    CK(shared_alloc(&c->dwx_d, (size_t)n * C * 2, c->tG > 1));
     if (c->rglobal) CK(dalloc(&c->rg_d, TL.erow.size() * C));
     CK(dalloc(&c->ctl_d, 4));
     CK(hipHostMalloc((void**)&c->tmo_h, sizeof(unsigned), hipHostMallocDefault));
@@ -826,7 +836,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     }
     if (c->tG > 0) {
       CK(dalloc(&c->tdev_d, kTileRanksMax));
-      CK(dalloc(&c->xflag_d, kTileRanksMax));
+      CK(shared_alloc(&c->xflag_d, kTileRanksMax, c->tG > 1));
       CK(hipMemsetAsync(c->xflag_d, 0, sizeof(unsigned) * kTileRanksMax, c->st));
     }
     if (const char* pr = std::getenv("NNGP_PROBE"))
@@ -837,7 +847,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
         CK(hipMemsetAsync(c->tdbg_d, 0, sizeof(unsigned long long) * c->tdbg_n, c->st));
       }
   }
-  CK(dalloc(&c->w_slot_d, NS * C));
+  CK(shared_alloc(&c->w_slot_d, NS * C, c->tG > 1));
   CK(dalloc(&c->r_d, (size_t)n * C));
   CK(dalloc(&c->level_rows_d, n));
   CK(dalloc(&c->level_ptr_d, c->level_ptr.size()));

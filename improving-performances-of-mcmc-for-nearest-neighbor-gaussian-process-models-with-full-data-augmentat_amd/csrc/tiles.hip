@@ -360,8 +360,11 @@ __device__ __forceinline__ void tile_own_draw(const TileDev& D, const TileLaunch
                                               TileBatchRegs<C, NT, RMAX>& b, unsigned epoch) {
   constexpr int IMAX = TileBatchRegs<C, NT, RMAX>::IMAX;
   const int t = S.t, lane = S.lane, wv = S.wv;
-  double* r_s = S.r_s;
-  double* acc_s = S.acc_s;
+  // r (the tile's rows) and acc_s (slot totals, then dw) are disjoint LDS
+  // regions: restrict lets the products' r reads go out ahead of the slot
+  // totals written between them
+  const double* __restrict__ r_s = S.r_s;
+  double* __restrict__ acc_s = S.acc_s;
   const int R = b.R, nit = b.ns * C;
   // products, running sums restarted at slot starts.  A slot that began in
   // this thread is complete at its last cell (-> acc_s); the thread's first
