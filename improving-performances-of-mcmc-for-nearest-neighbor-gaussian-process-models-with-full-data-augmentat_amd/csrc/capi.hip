@@ -91,6 +91,9 @@ struct nngp_ctx {
   int* level_rows_d = nullptr;
   int* level_ptr_d = nullptr;    // DAG level offsets (device copy)
   std::vector<int> tri_seg;      // solve plan: (lv0, lv1, kind) triples, kind 1 = one-workgroup run
+  bool tri_dag = false;          // NNGP_TRI=dag: one sync-free launch for the whole DAG
+  unsigned* tri_tmo_d = nullptr; // its timeout word
+  unsigned* tri_tmo_h = nullptr; // pinned copy, read at the next host sync
   int* obs_ptr_d = nullptr;
   int* obs_idx_d = nullptr;
   int* lm_d = nullptr;  // locs_match, 0-based
@@ -116,6 +119,8 @@ struct nngp_ctx {
   double* cell_val_d = nullptr;   // C x cells
   int2* gcell_d = nullptr;
   int* gsrc_d = nullptr;
+  int4* rorder_d = nullptr;       // tile_refresh work items (kRefreshLists x rorder_len)
+  int rorder_len = 0;
   double* gval_d = nullptr;       // C x ghost cells
   int* gptr_d = nullptr;
   int* gslot_d = nullptr;
@@ -292,8 +297,8 @@ TileDev tile_dev(nngp_ctx* c) {
 // sweep values of B + precision_diag of chain k from its current factor
 int refresh_sweep_values(nngp_ctx* c, int k) {
   if (c->engine == 1)
-    HIPCHK(c, launch_tile_refresh(c->st, tile_dev(c), (int)c->tl.batch.size(), c->tl.NT, c->cell_src_d, c->gsrc_d,
-                                  c->ch[k].linv_d[0], k));
+    HIPCHK(c, launch_tile_refresh(c->st, tile_dev(c), c->rorder_d, c->rorder_len, c->tl.NT, c->cell_src_d,
+                                  c->gsrc_d, c->ch[k].linv_d[0], k));
   else
     HIPCHK(c, launch_sell_refresh(c->st, sweep_dev(c), c->lay.nchunks, c->ent_src_d, c->ch[k].linv_d[0], k));
   if (c->shard && !c->sp.grow.empty()) {
@@ -410,9 +415,9 @@ void nngp_ctx_destroy(nngp_ctx* c) {
                              c->tmp2_d, c->partials_d, c->res_d, c->z_d, c->scal_d, c->dbg_d,
                              c->chunk_first_d, c->loc_rank_d, c->pairs_d, c->level_ptr_d, c->zbuf_d, c->ent_pos_d, c->start_mask_d,
                              c->dpos_d, c->perm_d, c->tb_d, c->tb_ptr_d, c->cell_pk_d, c->cell_src_d,
-                             c->cell_val_d, c->gcell_d, c->gsrc_d, c->gval_d, c->gptr_d, c->gslot_d, c->gslot_ptr_d, c->nb_ptr_d, c->nb_d,
+                             c->cell_val_d, c->gcell_d, c->gsrc_d, c->gval_d, c->gptr_d, c->rorder_d, c->gslot_d, c->gslot_ptr_d, c->nb_ptr_d, c->nb_d,
                              c->erow_ptr_d, c->erow_d, c->dwx_d, c->ctl_d, c->tdbg_d, c->sg_row_d,
-                             c->sg_recv_d, c->sg_src_d, c->sg_val_d, c->xbuf_d, c->sp_pairs_d};
+                             c->sg_recv_d, c->sg_src_d, c->sg_val_d, c->xbuf_d, c->sp_pairs_d, c->tri_tmo_d};
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->peers_open)
     for (int h = 0; h < c->tG; ++h) {
@@ -439,6 +444,7 @@ void nngp_ctx_destroy(nngp_ctx* c) {
   if (c->mu_stage_h) hipHostFree(c->mu_stage_h);
   if (c->mu_stage_ev) hipEventDestroy(c->mu_stage_ev);
   if (c->tmo_h) hipHostFree(c->tmo_h);
+  if (c->tri_tmo_h) hipHostFree(c->tri_tmo_h);
   if (c->st) hipStreamDestroy(c->st);
   delete c;
 }
@@ -812,6 +818,11 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     CK(upload(c->gsrc_d, TL.gsrc.data(), ng, c->st));
     CK(hipMemsetAsync(c->gval_d, 0, sizeof(double) * std::max<size_t>(1, ng * C), c->st));
     CK(upload(c->gptr_d, TL.gptr.data(), TL.gptr.size(), c->st));
+    {
+      const std::vector<int4> ro = tile_refresh_order(TL.batch_ptr, TL.gptr, TL.T, TL.K, c->rorder_len);
+      CK(dalloc(&c->rorder_d, ro.size()));
+      CK(upload(c->rorder_d, ro.data(), ro.size(), c->st));
+    }
     CK(upload(c->nb_ptr_d, TL.nb_ptr.data(), TL.nb_ptr.size(), c->st));
     CK(upload(c->nb_d, TL.nb.data(), TL.nb.size(), c->st));
     CK(upload(c->erow_ptr_d, TL.erow_ptr.data(), TL.erow_ptr.size(), c->st));
@@ -857,9 +868,16 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     // workgroup (a barrier per level; one CU streams ~10 B/cycle, so only
     // small levels are cheaper there than behind a launch), larger levels get
     // a launch each
-    // (NNGP_TRI=level: one launch per level, the reference plan of the tests)
+    // (NNGP_TRI=level: one launch per level, the reference plan of the tests;
+    // NNGP_TRI=levels: this plan; default: the sync-free one-launch solve,
+    // tri_dag_kernel)
     const char* e = std::getenv("NNGP_TRI");
     const bool per_level = e && std::string(e) == "level";
+    c->tri_dag = !per_level && !(e && std::string(e) == "levels");
+    CK(dalloc(&c->tri_tmo_d, 1));
+    CK(hipMemset(c->tri_tmo_d, 0, sizeof(unsigned)));
+    CK(hipHostMalloc((void**)&c->tri_tmo_h, sizeof(unsigned), hipHostMallocDefault));
+    *c->tri_tmo_h = 0;
     const int L = (int)c->level_ptr.size() - 1;
     for (int lv = 0; lv < L;) {
       const int sz = c->level_ptr[lv + 1] - c->level_ptr[lv];
@@ -2123,6 +2141,12 @@ int nngp_sweep_timed(nngp_ctx* c, int n_sweeps, const double* beta0, const doubl
 
 // ---------------------------------------------------------------- MH helpers
 static int tri_solve_dev(nngp_ctx* c, const TriArgs& ta, const double* u, double* x) {
+  if (c->tri_dag) {
+    HIPCHK(c, launch_tri_dag(c->st, ta, c->level_rows_d, c->n, c->nn_d, c->b, u, x, (long long)c->n * ta.stride,
+                             c->tri_tmo_d));
+    HIPCHK(c, hipMemcpyAsync(c->tri_tmo_h, c->tri_tmo_d, sizeof(unsigned), hipMemcpyDeviceToHost, c->st));
+    return NNGP_OK;
+  }
   for (size_t k = 0; k + 2 < c->tri_seg.size(); k += 3) {
     const int lv0 = c->tri_seg[k], lv1 = c->tri_seg[k + 1];
     if (c->tri_seg[k + 2]) {
@@ -2131,6 +2155,17 @@ static int tri_solve_dev(nngp_ctx* c, const TriArgs& ta, const double* u, double
       const int a = c->level_ptr[lv0], e = c->level_ptr[lv1];
       if (e > a) HIPCHK(c, launch_tri_level(c->st, ta, c->level_rows_d + a, e - a, c->nn_d, c->b, u, x));
     }
+  }
+  return NNGP_OK;
+}
+
+// after a host sync: did a sync-free solve since the last check time out?
+// (its unfinished entries are NaN)
+static int tri_timeout_check(nngp_ctx* c) {
+  if (c->tri_tmo_h && *c->tri_tmo_h) {
+    *c->tri_tmo_h = 0;
+    HIPCHK(c, hipMemsetAsync(c->tri_tmo_d, 0, sizeof(unsigned), c->st));
+    return fail_msg(c, NNGP_ERR_HIP, "triangular solve: a dependency wait timed out (waves not co-resident?)");
   }
   return NNGP_OK;
 }
@@ -2217,6 +2252,7 @@ static int obs_chains(nngp_ctx* c, int mode, int chain_mask, const double* beta0
       if ((rc = obs_enqueue(c, k, mode, beta0[k], mode == 1 ? lnv[k] : 0.0))) return rc;
   HIPCHK(c, hipMemcpyAsync(c->res_h, c->res_d, 4 * c->C * sizeof(double), hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
+  if ((rc = tri_timeout_check(c))) return rc;  // the proposal field of a ratio comes from the solve
   for (int k = 0; k < c->C; ++k)
     if ((chain_mask >> k) & 1) out[k] = c->res_h[4 * k];
   return NNGP_OK;
@@ -2312,7 +2348,8 @@ int nngp_tri_solve(nngp_ctx* c, int which, const double* u, double* x) {
   if ((rc = set_device(c))) return rc;
   if ((rc = upload_field(c, u, c->tmp_d))) return rc;
   if ((rc = tri_solve_dev(c, tri_one(S.linv_d[which]), c->tmp_d, c->tmp2_d))) return rc;
-  return download_field(c, c->tmp2_d, x);
+  if ((rc = download_field(c, c->tmp2_d, x))) return rc;
+  return tri_timeout_check(c);
 }
 
 int nngp_device_normals(int device, uint64_t seed, uint64_t sweep, int n, double* z) {

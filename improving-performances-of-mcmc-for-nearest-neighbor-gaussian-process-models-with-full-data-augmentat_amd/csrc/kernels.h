@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <vector>
 
 namespace nngp {
 
@@ -228,8 +229,13 @@ hipError_t launch_tile_xwait(hipStream_t st, const unsigned* xflag, unsigned* ct
 struct TilePeerW { double* w[kTileRanksMax] = {}; int hptr[kTileRanksMax + 1] = {}; };
 hipError_t launch_tile_halo_put(hipStream_t st, const TilePeerW& pw, const int* halo, const double* w, int C);
 // chain `chain`: cell/ghost values from Linv (device order) and precision_diag
-hipError_t launch_tile_refresh(hipStream_t st, const TileDev& D, int nbatches, int NT, const int* cell_src,
-                               const int* gsrc, const double* linv, int chain);
+// work items of the refresh, dealt to kRefreshLists (= XCDs) lists by tile;
+// olen = the longest list
+constexpr int kRefreshLists = 8;
+std::vector<int4> tile_refresh_order(const std::vector<int>& batch_ptr, const std::vector<int>& gptr, int T, int K,
+                                     int& olen);
+hipError_t launch_tile_refresh(hipStream_t st, const TileDev& D, const int4* order, int olen, int NT,
+                               const int* cell_src, const int* gsrc, const double* linv, int chain);
 
 // obs reductions: mode 0 -> partial[0] += (y - f[loc] - mu + beta0)^2
 //                 mode 1 -> partial[0] += ((y-b)^2 - (y-a)^2) / (2 sd^2),
@@ -251,6 +257,11 @@ hipError_t launch_tri_level(hipStream_t st, const TriArgs& a, const int* rows, i
 // levels [lv0, lv1) of the DAG (small ones) in one 1024-thread workgroup
 hipError_t launch_tri_levels_block(hipStream_t st, const TriArgs& a, const int* rows, const int* lptr, int lv0,
                                    int lv1, const int* nn, int b, const double* u, double* x);
+// the whole DAG in one sync-free launch (rows = all levels back to back,
+// nrows of them); x (x_len doubles) is overwritten with a pending sentinel
+// first; *tmo is set if a wait timed out
+hipError_t launch_tri_dag(hipStream_t st, const TriArgs& a, const int* rows, int nrows, const int* nn, int b,
+                          const double* u, double* x, long long x_len, unsigned* tmo);
 // y[i] = shift + scale * x[i*xstride]
 // dst[i] = src[idx[i]] (gather) / dst[idx[i]] = src[i] (scatter), i < n:
 // R order <-> device row order of a field-sized vector

@@ -145,16 +145,16 @@ __constant__ double kExp2Tab[64] = {
 
 // exp(x) for x <= 0 (the factor's correlations): x = (64 m + j) ln2/64 + r,
 // |r| <= ln2/128, exp(x) = 2^m 2^(j/64) e^r with e^r - 1 by a degree-6
-// Taylor polynomial; within 1 ulp of the correctly rounded exp (measured,
-// scripts/micro/dmath.hip).  Very negative x (including the padding
-// distances of ~1e30) gives exactly 0.
+// Taylor polynomial of degree 5 (truncation r^6/720 <= 3.5e-17 for
+// |r| <= ln2/128, below half an ulp); within 1 ulp of the correctly rounded
+// exp (measured, scripts/micro/dmath.hip).  Very negative x (including the
+// padding distances of ~1e30) gives exactly 0.
 __device__ __forceinline__ double exp_nonpos(double x, const double* tab) {
   const double k = __builtin_rint(x * 92.33248261689366);  // 64/ln2
   double r = __builtin_fma(-k, 0.010830424696249145, x);    // ln2/64, high part
   r = __builtin_fma(-k, 3.623510646634843e-19, r);          // low part
   const int ki = (int)k;                                      // saturates for huge |x|
-  double p = 1.3888888888888889e-03;
-  p = __builtin_fma(p, r, 8.3333333333333332e-03);
+  double p = 8.3333333333333332e-03;
   p = __builtin_fma(p, r, 4.1666666666666664e-02);
   p = __builtin_fma(p, r, 1.6666666666666666e-01);
   p = __builtin_fma(p, r, 0.5);
@@ -250,8 +250,12 @@ hipError_t launch_scale_coords(hipStream_t st, int covfun, const double* cp, int
 // Linv[i, j] = x[BM-1-j] with L^T x = e_last.
 // One row of the factor from its neighbour coordinates xa(r, k) (locsub
 // order: the point itself last) and its count of valid neighbours bs.
-template <int BM, int FAM, int DS, class XA>
-__device__ __forceinline__ void factor_row(const XA& xa, int bs, int i, double var, double nugget, int b,
+// The Cholesky runs on the correlation scale (K = C / var: off-diagonal
+// correlations, diagonal 1 + nugget) and the solution is scaled by
+// rsv = 1/sqrt(var) at the end (chol(var K) = sqrt(var) chol(K)): one multiply
+// per output instead of one per covariance entry.
+template <int BM, int FAM, int DS, int V, class XA>
+__device__ __forceinline__ void factor_row(const XA& xa, int bs, int i, double rsv, double nugget, int b,
                                            const double* __restrict__ tab, double* __restrict__ linv,
                                            int* __restrict__ fail) {
   constexpr int T = BM * (BM + 1) / 2;
@@ -274,13 +278,23 @@ __device__ __forceinline__ void factor_row(const XA& xa, int bs, int i, double v
       }
       const double dist = sqrt_pos(s2);
       const double e = exp_nonpos(-dist, tab);
-      L[t * (t + 1) / 2 + q] = FAM == 1 ? var * ((1.0 + dist) * e) : var * e;
+      L[t * (t + 1) / 2 + q] = FAM == 1 ? __builtin_fma(dist, e, e) : e;
     }
 #pragma unroll
     for (int q = 0; q <= t; ++q) {
-      double s = q == t ? (dt ? 1.0 : var * (1.0 + nugget)) : L[t * (t + 1) / 2 + q];
+      double s = q == t ? (dt ? 1.0 : 1.0 + nugget) : L[t * (t + 1) / 2 + q];
+      if (V & 1) {  // two partial sums: half the dependent chain
+        double s1 = 0.0;
 #pragma unroll
-      for (int p = 0; p < q; ++p) s -= L[t * (t + 1) / 2 + p] * L[q * (q + 1) / 2 + p];
+        for (int p = 0; p < q; ++p) {
+          if (p & 1) s1 -= L[t * (t + 1) / 2 + p] * L[q * (q + 1) / 2 + p];
+          else s -= L[t * (t + 1) / 2 + p] * L[q * (q + 1) / 2 + p];
+        }
+        s += s1;
+      } else {
+#pragma unroll
+        for (int p = 0; p < q; ++p) s -= L[t * (t + 1) / 2 + p] * L[q * (q + 1) / 2 + p];
+      }
       if (q < t) {
         L[t * (t + 1) / 2 + q] = s * inv[q];
       } else {
@@ -303,7 +317,7 @@ __device__ __forceinline__ void factor_row(const XA& xa, int bs, int i, double v
   if (bad) atomicMin(fail, i + 1);
 #pragma unroll
   for (int j = 0; j < BM; ++j)
-    if (j < b) linv[(size_t)i * b + j] = (j < bs) ? x[BM - 1 - j] : 0.0;
+    if (j < b) linv[(size_t)i * b + j] = (j < bs) ? x[BM - 1 - j] * rsv : 0.0;
 }
 
 // neighbour indices of row i (clamped to n-1; entries j >= b read as -1)
@@ -341,7 +355,7 @@ __device__ __forceinline__ int gather_coords(double (&X)[BM][DS], const int (&nc
 // next group's coordinate gathers and the group after's neighbour indices
 // are in flight while this group's covariance/Cholesky runs (one wave per
 // SIMD fits the register footprint, so no other wave hides that latency).
-template <int BM, int FAM, int DS>
+template <int BM, int FAM, int DS, int V>
 __global__ __launch_bounds__(64) void factor_kernel(double var, double nugget, double nu, double norm,
                                                    const double* __restrict__ sc,
                                                    const int* __restrict__ nn, int n, int b,
@@ -349,10 +363,23 @@ __global__ __launch_bounds__(64) void factor_kernel(double var, double nugget, d
   __shared__ double tab[64];
   tab[threadIdx.x] = kExp2Tab[threadIdx.x];
   __syncthreads();
+  const double rsv = rsqrt_pos(var);
   const int stride = gridDim.x * 64;
   int i = blockIdx.x * 64 + threadIdx.x;
   int nc[BM], nx[BM];
   double X[BM][DS];
+  if (V & 2) {  // indices one group ahead only (no coordinates in flight)
+    load_nn_row<BM>(nx, nn, i, n, b);
+    for (int base = blockIdx.x * 64; base < n; base += stride, i += stride) {
+#pragma unroll
+      for (int r = 0; r < BM; ++r) nc[r] = nx[r];
+      const int bs = gather_coords<BM, DS>(X, nc, sc, i, n);
+      load_nn_row<BM>(nx, nn, i + stride, n, b);
+      if (i < n)
+        factor_row<BM, FAM, DS, V>([&](int r, int k) { return X[r][k]; }, bs, i, rsv, nugget, b, tab, linv, fail);
+    }
+    return;
+  }
   load_nn_row<BM>(nc, nn, i, n, b);
   int bs = gather_coords<BM, DS>(X, nc, sc, i, n);
   load_nn_row<BM>(nx, nn, i + stride, n, b);
@@ -361,7 +388,7 @@ __global__ __launch_bounds__(64) void factor_kernel(double var, double nugget, d
     const int bsn = gather_coords<BM, DS>(Xn, nx, sc, i + stride, n);
     load_nn_row<BM>(nx, nn, i + 2 * stride, n, b);
     if (i < n)
-      factor_row<BM, FAM, DS>([&](int r, int k) { return X[r][k]; }, bs, i, var, nugget, b, tab, linv, fail);
+      factor_row<BM, FAM, DS, V>([&](int r, int k) { return X[r][k]; }, bs, i, rsv, nugget, b, tab, linv, fail);
 #pragma unroll
     for (int r = 0; r < BM; ++r)
 #pragma unroll
@@ -427,13 +454,6 @@ __global__ __launch_bounds__(64) void factor_kernel_rt(double var, double nugget
   for (int j = 0; j < b; ++j) linv[(size_t)i * b + j] = (j < bs) ? x[bs - 1 - j] : 0.0;
 }
 
-// Planar coordinates (DS = 2): the coordinates of the next group of 64 rows
-// are DMA'd global -> LDS (global_load_lds_dwordx4, one 16-byte point per
-// lane and neighbour) into the second of two stages while this group
-// computes, so the in-flight coordinates occupy no VGPRs (the factor's L
-// needs nearly all of them).  Stage layout [r][lane] x 16 B; 32 KB per
-// one-wave workgroup at BM = 16.  Missing neighbours load the point itself
-// and read back as the far-away padding of gather_coords.
 #define NNGP_FACTOR_ARGS var, nugget, nu, norm, sc, nn, n, b, linv, fail
 // workgroups of a grid-stride kernel: NNGP_FACTOR_GRID (default 2) x the
 // resident one-wave workgroups of the current device, at most the row
@@ -457,7 +477,7 @@ static int resident_grid(const void* kern, int groups) {
 template <int BM, int FAM, int DS>
 static hipError_t launch_factor_one(hipStream_t st, double var, double nugget, double nu, double norm,
                                     const double* sc, const int* nn, int n, int b, double* linv, int* fail) {
-  const auto kern = factor_kernel<BM, FAM, DS>;
+  const auto kern = factor_kernel<BM, FAM, DS, 0>;
   const int g = resident_grid(reinterpret_cast<const void*>(kern), (n + 63) / 64);
   hipLaunchKernelGGL(kern, dim3(g), dim3(64), 0, st, NNGP_FACTOR_ARGS);
   return hipGetLastError();
@@ -553,20 +573,33 @@ __global__ __launch_bounds__(256) void row_stats_kernel(const double* __restrict
   double acc[4] = {0, 0, 0, 0};
   const int g = threadIdx.x & (G - 1);
   const int rows_per_grid = gridDim.x * (blockDim.x / G);
-  for (int k = blockIdx.x * (blockDim.x / G) + threadIdx.x / G; k < n; k += rows_per_grid) {
-    double l = 0.0, xv = 0.0;
+  // two rows per group and trip (k, k + rows_per_grid): their loads are in
+  // flight together; the row sums and their accumulation order are those of
+  // one row per trip (bitwise the same results)
+  for (int k = blockIdx.x * (blockDim.x / G) + threadIdx.x / G; k < n; k += 2 * rows_per_grid) {
+    const int k2 = k + rows_per_grid;
+    const bool two = k2 < n;
+    int idx = -1, idx2 = -1;
     if (g < b) {
-      const int idx = nn[(size_t)k * b + g];
-      if (idx >= 0) {
-        l = linv[(size_t)k * b + g];
-        xv = x[idx] - shift;
-      }
+      idx = __builtin_nontemporal_load(nn + (size_t)k * b + g);
+      if (two) idx2 = __builtin_nontemporal_load(nn + (size_t)k2 * b + g);
     }
-    double u = l * xv, a = l;
+    double l = 0.0, xv = 0.0, l2 = 0.0, xv2 = 0.0;
+    if (idx >= 0) {
+      l = __builtin_nontemporal_load(linv + (size_t)k * b + g);
+      xv = x[idx] - shift;
+    }
+    if (idx2 >= 0) {
+      l2 = __builtin_nontemporal_load(linv + (size_t)k2 * b + g);
+      xv2 = x[idx2] - shift;
+    }
+    double u = l * xv, a = l, u2 = l2 * xv2, a2 = l2;
 #pragma unroll
     for (int off = 1; off < G; off <<= 1) {
       u += __shfl_xor(u, off, 64);
       a += __shfl_xor(a, off, 64);
+      u2 += __shfl_xor(u2, off, 64);
+      a2 += __shfl_xor(a2, off, 64);
     }
     if (g == 0) {
       acc[0] += log(linv[(size_t)k * b]);
@@ -574,6 +607,13 @@ __global__ __launch_bounds__(256) void row_stats_kernel(const double* __restrict
       acc[2] += a * a;
       acc[3] += a * u;
       if (out) out[(size_t)k * out_stride] = u;
+      if (two) {
+        acc[0] += log(linv[(size_t)k2 * b]);
+        acc[1] += u2 * u2;
+        acc[2] += a2 * a2;
+        acc[3] += a2 * u2;
+        if (out) out[(size_t)k2 * out_stride] = u2;
+      }
     }
   }
   block_sum4(acc, partials + 4 * blockIdx.x);
@@ -1167,6 +1207,128 @@ hipError_t launch_tri_levels_block(hipStream_t st, const TriArgs& a, const int* 
   else
     hipLaunchKernelGGL(tri_levels_block_kernel<32>, dim3(1), dim3(1024), 0, st, a, rows, lptr, lv0, lv1, nn, b, u,
                        x);
+  return hipGetLastError();
+}
+
+// Sync-free variant: the whole DAG in ONE persistent launch, no level
+// barriers.  x starts as a NaN sentinel (kTriPending, never produced by
+// arithmetic); a (row, chain) item is ready when none of the x values it
+// reads is the sentinel any more, and its result is stored with device scope
+// (sc1, write-through) so items on other CUs / XCDs see it.  Item order =
+// level order (rows[] holds the levels back to back, chains interleaved);
+// wave w takes items 4w.., 4(w+W).., ... (16 lanes per item, as tri_row16:
+// the same products, the same DPP row reduction, so x is bitwise the level
+// kernels' x).  Progress: the grid is at most the resident waves, so the
+// lowest unfinished item always sits in a running wave whose every earlier
+// item is done, and it only reads lower items.  Inside a wave the 4 items
+// are retried until all are done (an item may read one of the same wave), and
+// every wave's waits are bounded: on a timeout the word *tmo is set, the
+// unfinished entries stay NaN and the waves leave.
+constexpr unsigned long long kTriPending = 0x7FF4A5A5DEAD5A5Aull;
+
+__device__ __forceinline__ double tri_load_dev(const double* p) {
+  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+template <int BMAX>
+__global__ __launch_bounds__(256) void tri_dag_kernel(TriArgs a, const int* __restrict__ rows, long long nitems,
+                                                      const int* __restrict__ nn, int b,
+                                                      const double* __restrict__ u, double* x,
+                                                      unsigned* __restrict__ tmo) {
+  constexpr int J = BMAX / 16;
+  const int l = threadIdx.x & 15, sub = (threadIdx.x >> 4) & 3;
+  const long long W = (long long)gridDim.x * (blockDim.x >> 6);
+  const long long w = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int S = a.stride;
+  bool quit = false;
+  for (long long base = 4 * w; base < nitems && !quit; base += 4 * W) {
+    const long long it = base + sub;
+    const bool active = it < nitems;
+    const int i = active ? rows[it / a.nc] : 0;
+    const int kk = active ? (int)(it % a.nc) : 0;
+    const int k = a.kidx[kk];
+    const double* lr = a.linv[kk] + (size_t)i * b;
+    int idx[J];
+    double lv[J], xv[J];
+    bool have[J];
+#pragma unroll
+    for (int q = 0; q < J; ++q) {
+      const int j = l + 16 * q;
+      idx[q] = (active && j >= 1 && j < b) ? __builtin_nontemporal_load(nn + (size_t)i * b + j) : -1;
+      lv[q] = idx[q] >= 0 ? __builtin_nontemporal_load(lr + j) : 0.0;
+      xv[q] = 0.0;
+      have[q] = idx[q] < 0;
+    }
+    const double ui = (active && l == 15) ? u[(size_t)i * S + k] : 0.0;
+    const double d0 = (active && l == 15) ? lr[0] : 1.0;
+    bool done = !active;
+    for (unsigned spins = 0;; ++spins) {
+      bool ready = true;
+#pragma unroll
+      for (int q = 0; q < J; ++q) {
+        if (!have[q]) {
+          const double v = tri_load_dev(x + (size_t)idx[q] * S + k);
+          if (__builtin_bit_cast(unsigned long long, v) != kTriPending) {
+            xv[q] = v;
+            have[q] = true;
+          } else {
+            ready = false;
+          }
+        }
+      }
+      const unsigned long long bal = __ballot(ready);
+      const bool grp = ((bal >> (16 * sub)) & 0xFFFFull) == 0xFFFFull;
+      double p = 0.0;
+#pragma unroll
+      for (int q = 0; q < J; ++q) p = __builtin_fma(lv[q], xv[q], p);
+      p += dpp_f64<0x111, 0xF, true>(p);  // row_shr:1
+      p += dpp_f64<0x112, 0xF, true>(p);  // row_shr:2
+      p += dpp_f64<0x114, 0xF, true>(p);  // row_shr:4
+      p += dpp_f64<0x118, 0xF, true>(p);  // row_shr:8 -> lane 15 holds the row sum
+      if (!done && grp) {
+        if (l == 15)
+          __hip_atomic_store(reinterpret_cast<unsigned long long*>(x + (size_t)i * S + k),
+                             __builtin_bit_cast(unsigned long long, (ui - p) / d0), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        done = true;
+      }
+      if (__ballot(!done) == 0) break;
+      // (wave-uniform: the timeout word is read by the first lane only)
+      if (spins > (1u << 22) ||
+          ((spins & 255u) == 255u &&
+           __builtin_amdgcn_readfirstlane(__hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))) {
+        __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        quit = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+}
+
+__global__ void fill_u64_kernel(long long n, unsigned long long v, unsigned long long* __restrict__ p) {
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x)
+    p[e] = v;
+}
+
+hipError_t launch_tri_dag(hipStream_t st, const TriArgs& a, const int* rows, int nrows, const int* nn, int b,
+                          const double* u, double* x, long long x_len, unsigned* tmo) {
+  const auto kern = b <= 16 ? tri_dag_kernel<16> : tri_dag_kernel<32>;
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                              hipSuccess || cus <= 0)
+    return hipErrorInvalidDevice;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), 256, 0);
+  if (e != hipSuccess) return e;
+  if (per_cu <= 0) return hipErrorInvalidConfiguration;
+  const long long nitems = (long long)nrows * a.nc;
+  long long g = std::min<long long>((long long)cus * per_cu, (nitems + 15) / 16);
+  if (g < 1) g = 1;
+  const int gf = (int)std::min<long long>((x_len + 255) / 256, 4096);
+  hipLaunchKernelGGL(fill_u64_kernel, dim3(gf > 0 ? gf : 1), dim3(256), 0, st, x_len, kTriPending,
+                     reinterpret_cast<unsigned long long*>(x));
+  hipLaunchKernelGGL(kern, dim3((int)g), dim3(256), 0, st, a, rows, nitems, nn, b, u, x, tmo);
   return hipGetLastError();
 }
 

@@ -1232,34 +1232,67 @@ hipError_t launch_sweep_tiles(hipStream_t st, const TileDev& D, const TileLaunch
 }
 
 // B values of chain `chain` into the tile layout + precision_diag (column
-// sums of squares in stream = row order, as sell_refresh); workgroups
-// [0, nbatches) take one own batch each (NT = the layout's threads per tile,
-// cell f of the batch at off + (f % R)*NT + f / R), the rest copy ghost values
-__global__ __launch_bounds__(256) void tile_refresh_kernel(TileDev D, int nbatches, int NT,
-                                                           const int* __restrict__ cell_src,
+// sums of squares in stream = row order, as sell_refresh).  Work items
+// (order[], built with the layout): an own batch (cell f of the batch at
+// off + (f % R)*NT + f / R; NT = the layout's threads per tile) or a run of
+// <= 2048 ghost cells.  The items of a tile read Linv rows of that tile (a
+// contiguous device-row range), so the items are dealt to the XCDs by tile:
+// block b runs item b / 8 of list b % 8 (the dispatcher's round robin over
+// the 8 XCDs; speed only), and each list holds whole tiles of a contiguous
+// tile range -- a tile's rows are fetched into ONE L2 and every Linv line is
+// read from HBM about once instead of once per cell
+__global__ __launch_bounds__(256) void tile_refresh_kernel(TileDev D, const int4* __restrict__ order, int olen,
+                                                           int NT, const int* __restrict__ cell_src,
                                                            const int* __restrict__ gsrc,
                                                            const double* __restrict__ linv, int chain) {
   __shared__ double sq[4096];
   __shared__ unsigned char endf[4096];
+  // U independent gathers in flight per thread
+  constexpr int U = 8;
   const int t = threadIdx.x;
-  if ((int)blockIdx.x >= nbatches) {
+  const int4 o = order[(size_t)(blockIdx.x % kRefreshLists) * olen + blockIdx.x / kRefreshLists];
+  if (o.x == 2) return;
+  if (o.x == 1) {  // ghost cells [o.y, o.z)
     double* gv = const_cast<double*>(D.gval) + (size_t)chain * D.n_gcells;
-    for (long long g = (long long)(blockIdx.x - nbatches) * 256 + t; g < D.n_gcells;
-         g += (long long)(gridDim.x - nbatches) * 256)
-      gv[g] = linv[gsrc[g]];
+    for (int g0 = o.y + t; g0 < o.z; g0 += U * 256) {
+      int src[U];
+      double v[U];
+#pragma unroll
+      for (int q = 0; q < U; ++q) src[q] = g0 + q * 256 < o.z ? __builtin_nontemporal_load(gsrc + g0 + q * 256) : -1;
+#pragma unroll
+      for (int q = 0; q < U; ++q) v[q] = src[q] >= 0 ? linv[src[q]] : 0.0;
+#pragma unroll
+      for (int q = 0; q < U; ++q)
+        if (g0 + q * 256 < o.z) gv[g0 + q * 256] = v[q];
+    }
     return;
   }
-  const int4 B = D.batch[blockIdx.x];  // refresh kernel: one batch per workgroup
+  const int4 B = D.batch[o.y];
   double* cv = const_cast<double*>(D.cell_val) + (size_t)chain * D.n_cells;
   const int R = B.y & 0xFFFF;
-  for (int e0 = t; e0 < R * NT; e0 += 256) {
-    const long long e = B.x + e0;
-    const int src = cell_src[e];
-    const double v = src >= 0 ? linv[src] : 0.0;
-    cv[e] = v;
-    const int f = (e0 % NT) * R + e0 / NT;  // e0 = j*NT + thread
-    sq[f] = v * v;
-    endf[f] = (D.cell_pk[e] & kTEnd) ? 1 : 0;
+  const int ncell = R * NT;
+  for (int e00 = t; e00 < ncell; e00 += U * 256) {
+    int src[U];
+    unsigned pk[U];
+    double v[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int e0 = e00 + q * 256;
+      src[q] = e0 < ncell ? __builtin_nontemporal_load(cell_src + B.x + e0) : -1;
+      pk[q] = e0 < ncell ? __builtin_nontemporal_load(D.cell_pk + B.x + e0) : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < U; ++q) v[q] = src[q] >= 0 ? linv[src[q]] : 0.0;
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int e0 = e00 + q * 256;
+      if (e0 < ncell) {
+        cv[B.x + e0] = v[q];
+        const int f = (e0 % NT) * R + e0 / NT;  // e0 = j*NT + thread
+        sq[f] = v[q] * v[q];
+        endf[f] = (pk[q] & kTEnd) ? 1 : 0;
+      }
+    }
   }
   __syncthreads();
   if (t < B.z) {
@@ -1274,12 +1307,28 @@ __global__ __launch_bounds__(256) void tile_refresh_kernel(TileDev D, int nbatch
   }
 }
 
-hipError_t launch_tile_refresh(hipStream_t st, const TileDev& D, int nbatches, int NT, const int* cell_src,
-                               const int* gsrc, const double* linv, int chain) {
-  const int gx = D.n_gcells > 0 ? 256 : 0;
-  if (nbatches + gx == 0) return hipSuccess;
-  hipLaunchKernelGGL(tile_refresh_kernel, dim3(nbatches + gx), dim3(256), 0, st, D, nbatches, NT, cell_src, gsrc,
-                     linv, chain);
+std::vector<int4> tile_refresh_order(const std::vector<int>& batch_ptr, const std::vector<int>& gptr, int T, int K,
+                                     int& olen) {
+  std::vector<std::vector<int4>> lists(kRefreshLists);
+  for (int t = 0; t < T; ++t) {
+    std::vector<int4>& l = lists[(size_t)t * kRefreshLists / T];
+    for (int q = batch_ptr[(size_t)t * K]; q < batch_ptr[(size_t)(t + 1) * K]; ++q) l.push_back(make_int4(0, q, 0, 0));
+    const int g1 = gptr[(size_t)(t + 1) * K];
+    for (int g = gptr[(size_t)t * K]; g < g1; g += 2048) l.push_back(make_int4(1, g, std::min(g + 2048, g1), 0));
+  }
+  olen = 0;
+  for (const auto& l : lists) olen = std::max(olen, (int)l.size());
+  std::vector<int4> order((size_t)kRefreshLists * std::max(olen, 1), make_int4(2, 0, 0, 0));
+  for (int x = 0; x < kRefreshLists; ++x)
+    for (size_t j = 0; j < lists[x].size(); ++j) order[(size_t)x * olen + j] = lists[x][j];
+  return order;
+}
+
+hipError_t launch_tile_refresh(hipStream_t st, const TileDev& D, const int4* order, int olen, int NT,
+                               const int* cell_src, const int* gsrc, const double* linv, int chain) {
+  if (olen == 0) return hipSuccess;
+  hipLaunchKernelGGL(tile_refresh_kernel, dim3(kRefreshLists * olen), dim3(256), 0, st, D, order, olen, NT, cell_src,
+                     gsrc, linv, chain);
   return hipGetLastError();
 }
 

@@ -390,15 +390,17 @@ def test_single_chain_sweep_inside_batched_context(P, O):
     np.testing.assert_allclose(got[1], ref, rtol=1e-9, atol=1e-10)
 
 
+@pytest.mark.parametrize("plan", ["dag", "levels"])
 @pytest.mark.parametrize("n,m", [(5000, 5), (120000, 15)])
-def test_blocked_tri_solve_equals_level_schedule(P, O, n, m, monkeypatch):
-    """The blocked solve plan (runs of small DAG levels in one workgroup) gives
-    exactly the bits of one launch per level, repeatedly, and matches the
-    oracle."""
+def test_blocked_tri_solve_equals_level_schedule(P, O, n, m, plan, monkeypatch):
+    """The sync-free one-launch solve (default, `dag`) and the blocked plan
+    (`levels`: runs of small DAG levels in one workgroup) give exactly the
+    bits of one launch per level, repeatedly, and match the oracle."""
     locs, NN, col, lm, y = make_problem(P, n, m, seed=n + 1)
     cp = COVS["matern15_isotropic"]
     rng = np.random.default_rng(3)
     us = [rng.normal(size=n) for _ in range(3)]
+    monkeypatch.setenv("NNGP_TRI", plan)
     with _ctx(P, locs, NN, col, lm, y) as ctx:
         ctx.factor(0, "matern15_isotropic", cp)
         got = [ctx.tri_solve(0, u) for u in us]
