@@ -588,7 +588,8 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
         }
       }
       const int need = ok && !csplit ? tile_lds_bytes(c->tl.max_rows, n_chains, NT, c->tl.K, c->tl.max_batches, c->tl.max_gslots) : 0;
-      // NNGP_TILE_R=global: the tiles' r in global memory (kernels.hip RG),
+      // NNGP_TILE_R=global: the tiles' r in global memory (tiles.hip RG; one
+      // GPU, or a tile shard with 512-thread tiles),
       // one GPU, for layouts beyond the LDS.  Opt-in: at n = 1e7, m = 20 (one
       // chain) it measured 362 chain-sweeps/s (26.4 ms per 10-sweep launch,
       // 1024 threads: 341) against the colour engine's 449 -- five serial
@@ -599,7 +600,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       if (ok && xw && need > lds_max) { ok = false; terr = "exchange-wave tiles exceed the LDS"; }
       if (ok && (need > lds_max || force_rg)) {
         const int need_rg = tile_lds_bytes(0, n_chains, NT, c->tl.K, c->tl.max_batches, c->tl.max_gslots);
-        if (force_rg && shard_G == 0 && (NT == 512 || NT == 1024) && need_rg <= lds_max) {
+        if (force_rg && (NT == 512 || (NT == 1024 && shard_G == 0)) && need_rg <= lds_max) {
           c->rglobal = true;
         } else {
           ok = false;

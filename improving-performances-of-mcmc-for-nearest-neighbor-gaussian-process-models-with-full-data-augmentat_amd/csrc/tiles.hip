@@ -1146,7 +1146,18 @@ static hipError_t launch_tiles_c(hipStream_t st, const TileDev& D, const TileLau
 template <int NT>
 static hipError_t launch_tiles_nt(hipStream_t st, const TileDev& D, const TileLaunch& a, int lds, const TileShard* sh,
                                   int grid, int* occ) {
-  if (D.rg) {  // r in global memory: 512- or 1024-thread tiles, one GPU
+  if (D.rg) {  // r in global memory: 512- or 1024-thread tiles; tile shards 512
+    if constexpr (NT == 512) {
+      if (sh) {
+        switch (D.C) {
+          case 1: return launch_tiles_c<1, NT, 0, 1, 1>(st, D, a, lds, sh, grid, occ);
+          case 2: return launch_tiles_c<2, NT, 0, 1, 1>(st, D, a, lds, sh, grid, occ);
+          case 3: return launch_tiles_c<3, NT, 0, 1, 1>(st, D, a, lds, sh, grid, occ);
+          case 4: return launch_tiles_c<4, NT, 0, 1, 1>(st, D, a, lds, sh, grid, occ);
+          default: return hipErrorInvalidValue;
+        }
+      }
+    }
     if constexpr (NT == 512 || NT == 1024) {
       if (sh) return hipErrorInvalidValue;
       switch (D.C) {
