@@ -259,6 +259,10 @@ def shard_parity_check(P, args, world, rank, local_rank, dist):
     args_c = ([0.1, 0.2], [0.0, 0.1], [-0.5, -0.3], [5, 6], [0, 0])
     old = os.environ.get("NNGP_TILES")
     os.environ["NNGP_TILES"] = str(16 * world)  # the same tiles on one GPU and over the ranks
+    # shard calls always rebuild r = B w in their prologue: the one-GPU side
+    # does too (a warm call starts from the carried-over r, last bits apart)
+    old_warm = os.environ.get("NNGP_SWEEP_WARM")
+    os.environ["NNGP_SWEEP_WARM"] = "0"
     try:
         res = []
         for shard in (False, True):
@@ -290,6 +294,10 @@ def shard_parity_check(P, args, world, rank, local_rank, dist):
             os.environ.pop("NNGP_TILES", None)
         else:
             os.environ["NNGP_TILES"] = old
+        if old_warm is None:
+            os.environ.pop("NNGP_SWEEP_WARM", None)
+        else:
+            os.environ["NNGP_SWEEP_WARM"] = old_warm
     ok = all(np.array_equal(a, b) for a, b in zip(res[0][0], res[1][0])) and res[1][1]["sweep_engine"] == 1
     t = torch.tensor([1 if ok else 0], dtype=torch.int32)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
@@ -574,6 +582,11 @@ def main():
                       "sweep_engine": "tiles" if info["sweep_engine"] == 1 else "colours",
                       "n_tiles": info["n_tiles"], "tile_rows_max": info["tile_rows_max"],
                       "n_ghost_cells": info["n_ghost_cells"],
+                      "call_prologue": ("warm: a call whose field, factor and beta_0 are unchanged since the "
+                                        "last call starts from the slot-order w and r = B w that call left "
+                                        "(NNGP_SWEEP_WARM=0: rebuild every call)"
+                                        if os.environ.get("NNGP_SWEEP_WARM", "1") != "0" and info["sweep_engine"] == 1
+                                        else "cold: w -> slots and r = B w rebuilt every call"),
                       "single_chain": single,
                       "parallelism": f"chains {C} per GPU x {world} GPUs (independent)"},
            "roofline": roofline, "cpu_baseline": cpu, "secondary": mcmc}

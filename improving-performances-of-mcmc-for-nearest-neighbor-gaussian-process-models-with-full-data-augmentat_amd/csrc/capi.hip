@@ -45,6 +45,18 @@ struct ChainState {
   // nngp_beta0_stats reuses a pass over the current factor and field
   uint64_t fgen = 1, lgen[2] = {1, 1};
   struct RowStats { uint64_t lg = 0, fg = 0; double shift = 0.0, r[4] = {0, 0, 0, 0}; } rs[2];
+  // sum_k log Linv[k][0] of the last two factors seen by a log-likelihood
+  // pass (keyed by the factor generation): later passes over the same factor
+  // skip the n logs
+  struct LogDet { uint64_t lg = 0; double v = 0.0; } ld[2];
+  int ld_next = 0;
+  // warm sweep calls (tile engine, one GPU): the last call left w in slot
+  // order and r = B w (the tile kernel writes its r back) for this field,
+  // factor and beta0 -- the next call with all three unchanged skips its
+  // prologue (field -> slots, r = B w)
+  bool warm = false;
+  uint64_t warm_fgen = 0, warm_lgen = 0;
+  double warm_beta0 = 0.0;
   int rs_next = 0;
 };
 
@@ -132,6 +144,7 @@ struct nngp_ctx {
   int* erow_d = nullptr;
   double* dwx_d = nullptr;        // n x C granules of 16 B
   bool rglobal = false;           // tiles keep r in global memory (rg_d) instead of LDS
+  bool warm_on = false;           // warm sweep calls allowed (tile engine, not a shard; NNGP_SWEEP_WARM=0: off)
   bool tcs = false;               // chain-split tile launches (one chain per workgroup, kernels.hip sweep_tiles_cs_kernel)
   int txw = 0;                    // exchange-wave tiles (tiles.hip tile_phase_xw): layout cut for NT - 64 cell threads
   int cus = 0;                    // compute units of the device
@@ -650,6 +663,10 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       }
       if (ok) {
         c->engine = 1;
+        {
+          const char* sw = std::getenv("NNGP_SWEEP_WARM");
+          c->warm_on = shard_G == 0 && !(sw && std::string(sw) == "0");
+        }
         c->engine_note = "tiles: " + std::to_string(T) + " tiles of " + std::to_string(NT) + " threads, " +
                          std::to_string(c->tresident) + " resident per CU x " + std::to_string(cus) + " CUs" +
                          (c->rglobal ? ", r in global memory" : "") + (xw ? ", exchange wave" : "") +
@@ -900,7 +917,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
   CK(dalloc(&c->y_d, n_obs));
   CK(dalloc(&c->tmp_d, (size_t)n * C));   // scratch vectors, chain-strided for batched solves
   CK(dalloc(&c->tmp2_d, (size_t)n * C));
-  CK(dalloc(&c->partials_d, 4 * kRedBlocks));
+  CK(dalloc(&c->partials_d, 4 * kRedBlocks * kRowJobsMax));
   CK(dalloc(&c->res_d, 4 * kMaxChains));
   CK(dalloc(&c->scal_d, C));
   CK(hipHostMalloc((void**)&c->scal_h, sizeof(SweepScalars) * C, hipHostMallocDefault));
@@ -1339,16 +1356,6 @@ int nngp_set_mu(nngp_ctx* c, const double* mu, double beta0) {
 }
 
 // ---------------------------------------------------------------- loglik
-// row statistics of chain k's field under factor `which` into res_d[4k..]
-static int rowstats_enqueue(nngp_ctx* c, int k, int which, double beta0) {
-  ChainState& S = c->ch[k];
-  if (!S.have_factor[which] || !S.have_field) return fail_msg(c, NNGP_ERR_STATE, "loglik: need factor and field");
-  int nb = launch_row_stats(c->st, S.linv_d[which], c->nn_d, c->n, c->b, S.field_d, beta0, nullptr, c->partials_d);
-  HIPCHK(c, hipGetLastError());
-  HIPCHK(c, launch_reduce4(c->st, c->partials_d, nb, c->res_d + 4 * k));
-  return NNGP_OK;
-}
-
 static void rowstats_store(nngp_ctx* c, int k, int which, double beta0, const double* r) {
   ChainState& S = c->ch[k];
   ChainState::RowStats& e = S.rs[S.rs_next];
@@ -1377,14 +1384,38 @@ int nngp_loglik_chains(nngp_ctx* c, int which, int chain_mask, const double* bet
   { int rs_ = replica_fresh(c); if (rs_) return rs_; }
   int rc;
   if ((rc = set_device(c))) return rc;
-  for (int k = 0; k < c->C; ++k)
-    if ((chain_mask >> k) & 1)
-      if ((rc = rowstats_enqueue(c, k, which, beta0[k]))) return rc;
+  // every chain of the mask in one pass over the rows (NNarray read once)
+  RowJobs J;
+  for (int k = 0; k < c->C; ++k) {
+    if (!((chain_mask >> k) & 1)) continue;
+    ChainState& S = c->ch[k];
+    if (!S.have_factor[which] || !S.have_field) return fail_msg(c, NNGP_ERR_STATE, "loglik: need factor and field");
+    J.linv[J.M] = S.linv_d[which];
+    J.x[J.M] = S.field_d;
+    J.shift[J.M] = beta0[k];
+    J.out[J.M] = nullptr;
+    J.res_slot[J.M] = k;
+    J.mode[J.M] = 1;
+    for (const ChainState::LogDet& e : S.ld)
+      if (e.lg == S.lgen[which]) J.mode[J.M] = 2;
+    ++J.M;
+  }
+  const int nb = launch_row_stats_jobs(c->st, J, c->nn_d, c->n, c->b, c->partials_d);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, launch_reduce4_jobs(c->st, J, c->partials_d, nb, c->res_d));
   HIPCHK(c, hipMemcpyAsync(c->res_h, c->res_d, 4 * c->C * sizeof(double), hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
   for (int k = 0; k < c->C; ++k) {
     if (!((chain_mask >> k) & 1)) continue;
-    const double* r = c->res_h + 4 * k;
+    ChainState& S = c->ch[k];
+    double* r = c->res_h + 4 * k;
+    bool cached = false;
+    for (const ChainState::LogDet& e : S.ld)
+      if (e.lg == S.lgen[which]) { r[0] = e.v; cached = true; }
+    if (!cached) {
+      S.ld[S.ld_next] = {S.lgen[which], r[0]};
+      S.ld_next ^= 1;
+    }
     ll[k] = r[0] - c->n * 0.5 * log_scale[k] - 0.5 * r[1] / std::exp(log_scale[k]);
     rowstats_store(c, k, which, beta0[k], r);
   }
@@ -1518,6 +1549,31 @@ static bool sharded_call(const nngp_ctx* c) { return c->shard && !(c->engine == 
 static int shard_ranks(const nngp_ctx* c) { return c->tG > 0 ? c->tG : c->sp.G; }
 static int shard_rank(const nngp_ctx* c) { return c->tG > 0 ? c->trank : c->sp.rank; }
 
+// the chains of mask can start from the slot-order w and r the last call
+// left (call BEFORE fields_written)
+static bool warm_call(const nngp_ctx* c, int mask, const double* beta0) {
+  if (!c->warm_on || c->engine != 1 || c->shard) return false;
+  for (int k = 0; k < c->C; ++k) {
+    if (!((mask >> k) & 1)) continue;
+    const ChainState& S = c->ch[k];
+    if (!S.warm || S.fgen != S.warm_fgen || S.lgen[0] != S.warm_lgen || beta0[k] != S.warm_beta0) return false;
+  }
+  return true;
+}
+
+// after a completed tile call (AFTER fields_written): slot-order w and r
+// match the chains' new fields
+static void warm_set(nngp_ctx* c, int mask, const double* beta0) {
+  for (int k = 0; k < c->C; ++k) {
+    if (!((mask >> k) & 1)) continue;
+    ChainState& S = c->ch[k];
+    S.warm = c->warm_on && c->engine == 1 && !c->shard;
+    S.warm_fgen = S.fgen;
+    S.warm_lgen = S.lgen[0];
+    S.warm_beta0 = beta0[k];
+  }
+}
+
 int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double lnv, uint64_t seed,
                uint64_t counter_base, const double* z) {
   if (!c || n_sweeps < 0) return NNGP_ERR_ARG;
@@ -1525,6 +1581,9 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
   int rc;
   if ((rc = set_device(c))) return rc;
   const int k = c->cur, mask = 1 << k;
+  double b0v[kMaxChains] = {0, 0, 0, 0};
+  b0v[k] = beta0;
+  const bool warm = !z && warm_call(c, mask, b0v);
   fields_written(c, mask);
   if ((rc = sweep_prepare(c, k, beta0, log_scale, lnv, seed, counter_base))) return rc;
   if ((rc = upload_scalars(c))) return rc;
@@ -1552,11 +1611,13 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
   } else {
     // replay a captured graph of the whole call (launch-bound at small n)
     hipGraphExec_t ex;
-    if ((rc = graph_for(c, n_sweeps, mask, &ex))) return rc;
+    if ((rc = graph_for(c, n_sweeps, mask, &ex, warm ? kColours | kEpilogue : kAll))) return rc;
     HIPCHK(c, hipGraphLaunch(ex, c->st));
   }
   HIPCHK(c, hipStreamSynchronize(c->st));
-  return tile_timeout_check(c);
+  if ((rc = tile_timeout_check(c))) return rc;
+  warm_set(c, mask, b0v);
+  return NNGP_OK;
 }
 
 int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const double* log_scale,
@@ -1565,16 +1626,19 @@ int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const doub
   if (n_sweeps == 0) return NNGP_OK;
   int rc;
   if ((rc = set_device(c))) return rc;
-  fields_written(c, (1 << c->C) - 1);
+  const int all = (1 << c->C) - 1;
+  const bool warm = warm_call(c, all, beta0);
+  fields_written(c, all);
   for (int k = 0; k < c->C; ++k)
     if ((rc = sweep_prepare(c, k, beta0[k], log_scale[k], lnv[k], seed[k], counter_base[k]))) return rc;
   if ((rc = upload_scalars(c))) return rc;
-  if (sharded_call(c)) return shard_call(c, n_sweeps, (1 << c->C) - 1);
+  if (sharded_call(c)) return shard_call(c, n_sweeps, all);
   hipGraphExec_t ex;
-  if ((rc = graph_for(c, n_sweeps, (1 << c->C) - 1, &ex))) return rc;
+  if ((rc = graph_for(c, n_sweeps, all, &ex, warm ? kColours | kEpilogue : kAll))) return rc;
   HIPCHK(c, hipGraphLaunch(ex, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
   if ((rc = tile_timeout_check(c))) return rc;
+  warm_set(c, all, beta0);
   if (c->tdbg_d) {
     if (const char* path = std::getenv("NNGP_DBG_OUT")) {
       std::vector<unsigned long long> h(c->tdbg_n);
@@ -2137,7 +2201,9 @@ int nngp_sweep_timed(nngp_ctx* c, int n_sweeps, const double* beta0, const doubl
   *ms = f;
   if (kernel_ms) *kernel_ms = g;
   for (auto& x : e) hipEventDestroy(x);
-  return tile_timeout_check(c);
+  if ((rc = tile_timeout_check(c))) return rc;
+  warm_set(c, mask, beta0);
+  return NNGP_OK;
 }
 
 // ---------------------------------------------------------------- MH helpers
@@ -2205,6 +2271,8 @@ int nngp_ancillary_propose_chains(nngp_ctx* c, int chain_mask, const double* bet
   TriArgs ta;
   std::memset(&ta, 0, sizeof ta);
   ta.stride = c->C;
+  RowJobs J;
+  J.out_stride = c->C;
   for (int k = 0; k < c->C; ++k) {
     if (!((chain_mask >> k) & 1)) continue;
     ChainState& S = c->ch[k];
@@ -2213,14 +2281,20 @@ int nngp_ancillary_propose_chains(nngp_ctx* c, int chain_mask, const double* bet
       std::snprintf(buf, sizeof buf, "ancillary_propose_chains: chain %d needs both factors and the field", k);
       return fail_msg(c, NNGP_ERR_STATE, buf);
     }
-    // tmp[d*C + k] = B_cur (field - beta0)
-    launch_row_stats(c->st, S.linv_d[0], c->nn_d, c->n, c->b, S.field_d, beta0[k], c->tmp_d + k, c->partials_d,
-                     nullptr, nullptr, c->C);
-    HIPCHK(c, hipGetLastError());
+    // tmp[d*C + k] = B_cur (field - beta0): every chain in one pass
+    J.linv[J.M] = S.linv_d[0];
+    J.x[J.M] = S.field_d;
+    J.shift[J.M] = beta0[k];
+    J.out[J.M] = c->tmp_d + k;
+    J.res_slot[J.M] = k;
+    J.mode[J.M] = 0;
+    ++J.M;
     ta.linv[ta.nc] = S.linv_d[1];
     ta.kidx[ta.nc] = k;
     ++ta.nc;
   }
+  launch_row_stats_jobs(c->st, J, c->nn_d, c->n, c->b, c->partials_d);
+  HIPCHK(c, hipGetLastError());
   if ((rc = tri_solve_dev(c, ta, c->tmp_d, c->tmp2_d))) return rc;
   for (int k = 0; k < c->C; ++k)
     if ((chain_mask >> k) & 1)

@@ -100,6 +100,28 @@ int launch_row_stats(hipStream_t st, const double* linv, const int* nn, int n, i
                      const double* shift_dev = nullptr /* overrides shift when set */,
                      const double* const* linv_dev = nullptr /* overrides linv when set */,
                      int out_stride = 1);
+// row statistics of up to kRowJobsMax (factor, field) jobs in ONE pass over
+// the rows: the NNarray entries are read once for all jobs; per job exactly
+// row_stats_kernel's products, butterfly and accumulation order (bitwise the
+// same partials), partials of job j at partials + j * kRedBlocks * 4, its
+// totals at res[4 * res_slot[j]] after launch_reduce4_jobs.  Returns #blocks.
+constexpr int kRowJobsMax = 4;
+struct RowJobs {
+  const double* linv[kRowJobsMax];
+  const double* x[kRowJobsMax];
+  double shift[kRowJobsMax];
+  double* out[kRowJobsMax];   // nullptr: no per-row output
+  int res_slot[kRowJobsMax];
+  // 0: per-row output only (no partials); 1: statistics incl. sum log L[k][0];
+  // 2: statistics without the log term (the caller has it: it depends on the
+  // factor only)
+  int mode[kRowJobsMax];
+  int M = 0;
+  int out_stride = 1;
+};
+int launch_row_stats_jobs(hipStream_t st, const RowJobs& J, const int* nn, int n, int b,
+                          double* partials /* kRowJobsMax x kRedBlocks x 4 */);
+hipError_t launch_reduce4_jobs(hipStream_t st, const RowJobs& J, const double* partials, int nblocks, double* res);
 // r = B (field_chain - beta0_chain) for every chain in mask: out[k*C + chain]
 // (factor of chain k: *linv_dev[k]; the row's NNarray read once)
 // field pointer of each chain (device row order)

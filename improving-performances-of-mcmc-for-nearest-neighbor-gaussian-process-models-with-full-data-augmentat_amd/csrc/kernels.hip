@@ -557,6 +557,23 @@ __device__ __forceinline__ void block_sum4(double v[4], double* out) {
   }
 }
 
+// sum over each aligned group of G lanes (G = 4, 8, 16, 32), every lane gets
+// it.  DPP inside a row of 16 lanes (quad_perm [1,0,3,2] and [2,3,0,1], then
+// row_half_mirror and row_mirror: the partner of every step holds a partial
+// over the same lane set as in the xor butterfly, and IEEE addition is
+// commutative, so the result is bitwise the butterfly's), one shuffle across
+// rows for G = 32.  The xor butterfly with __shfl_xor costs a ds_bpermute
+// (an LDS round trip) per 32-bit half and step; DPP moves are VALU.
+template <int G>
+__device__ __forceinline__ double group_sum(double v) {
+  v += dpp_f64<0xB1, 0xF, true>(v);
+  v += dpp_f64<0x4E, 0xF, true>(v);
+  if (G >= 8) v += dpp_f64<0x141, 0xF, true>(v);
+  if (G >= 16) v += dpp_f64<0x140, 0xF, true>(v);
+  if (G >= 32) v += __shfl_xor(v, 16, 64);
+  return v;
+}
+
 // G lanes per row (G >= b, power of two): lane g of a row reads entry g, so a
 // wave reads G*8 contiguous bytes of Linv per row; a G-lane butterfly sums it.
 template <int G>
@@ -594,13 +611,10 @@ __global__ __launch_bounds__(256) void row_stats_kernel(const double* __restrict
       xv2 = x[idx2] - shift;
     }
     double u = l * xv, a = l, u2 = l2 * xv2, a2 = l2;
-#pragma unroll
-    for (int off = 1; off < G; off <<= 1) {
-      u += __shfl_xor(u, off, 64);
-      a += __shfl_xor(a, off, 64);
-      u2 += __shfl_xor(u2, off, 64);
-      a2 += __shfl_xor(a2, off, 64);
-    }
+    u = group_sum<G>(u);
+    a = group_sum<G>(a);
+    u2 = group_sum<G>(u2);
+    a2 = group_sum<G>(a2);
     if (g == 0) {
       acc[0] += log(linv[(size_t)k * b]);
       acc[1] += u * u;
@@ -636,6 +650,120 @@ int launch_row_stats(hipStream_t st, const double* linv, const int* nn, int n, i
   return g;
 }
 
+// row_stats_kernel for several (factor, field) jobs in one pass: the row's
+// NNarray entries load once; per job the same loads, butterfly and
+// accumulation order as row_stats_kernel (so the same partials, bitwise).
+// Two rows per trip as there, i.e. 2 x M independent gathers in flight.
+template <int G, int MJ>
+__global__ __launch_bounds__(256) void row_stats_jobs_kernel(RowJobs J, const int* __restrict__ nn, int n, int b,
+                                                             double* __restrict__ partials) {
+  double acc[MJ][4];
+#pragma unroll
+  for (int j = 0; j < MJ; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[j][q] = 0.0;
+  const int g = threadIdx.x & (G - 1);
+  const int rows_per_grid = gridDim.x * (blockDim.x / G);
+  for (int k = blockIdx.x * (blockDim.x / G) + threadIdx.x / G; k < n; k += 2 * rows_per_grid) {
+    const int k2 = k + rows_per_grid;
+    const bool two = k2 < n;
+    int idx = -1, idx2 = -1;
+    if (g < b) {
+      idx = __builtin_nontemporal_load(nn + (size_t)k * b + g);
+      if (two) idx2 = __builtin_nontemporal_load(nn + (size_t)k2 * b + g);
+    }
+    double u[MJ], a[MJ], u2[MJ], a2[MJ];
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) {
+      double l = 0.0, xv = 0.0, l2 = 0.0, xv2 = 0.0;
+      if (j < J.M) {
+        if (idx >= 0) {
+          l = __builtin_nontemporal_load(J.linv[j] + (size_t)k * b + g);
+          xv = J.x[j][idx] - J.shift[j];
+        }
+        if (idx2 >= 0) {
+          l2 = __builtin_nontemporal_load(J.linv[j] + (size_t)k2 * b + g);
+          xv2 = J.x[j][idx2] - J.shift[j];
+        }
+      }
+      u[j] = l * xv; a[j] = l; u2[j] = l2 * xv2; a2[j] = l2;
+    }
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) {
+      u[j] = group_sum<G>(u[j]);
+      a[j] = group_sum<G>(a[j]);
+      u2[j] = group_sum<G>(u2[j]);
+      a2[j] = group_sum<G>(a2[j]);
+    }
+    if (g == 0) {
+#pragma unroll
+      for (int j = 0; j < MJ; ++j) {
+        if (j >= J.M) continue;
+        if (J.out[j]) J.out[j][(size_t)k * J.out_stride] = u[j];
+        if (two && J.out[j]) J.out[j][(size_t)k2 * J.out_stride] = u2[j];
+        if (J.mode[j] == 0) continue;
+        if (J.mode[j] == 1) acc[j][0] += log(J.linv[j][(size_t)k * b]);
+        acc[j][1] += u[j] * u[j];
+        acc[j][2] += a[j] * a[j];
+        acc[j][3] += a[j] * u[j];
+        if (two) {
+          if (J.mode[j] == 1) acc[j][0] += log(J.linv[j][(size_t)k2 * b]);
+          acc[j][1] += u2[j] * u2[j];
+          acc[j][2] += a2[j] * a2[j];
+          acc[j][3] += a2[j] * u2[j];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < MJ; ++j)
+    if (j < J.M && J.mode[j] != 0) {
+      block_sum4(acc[j], partials + (size_t)j * kRedBlocks * 4 + 4 * blockIdx.x);
+      __syncthreads();  // block_sum4's LDS is reused by the next job
+    }
+}
+
+int launch_row_stats_jobs(hipStream_t st, const RowJobs& J, const int* nn, int n, int b, double* partials) {
+  const int G = b <= 4 ? 4 : b <= 8 ? 8 : b <= 16 ? 16 : 32;
+  long long rows_per_block = kBlock / G;
+  int g = (int)((n + rows_per_block - 1) / rows_per_block);
+  if (g > kRedBlocks) g = kRedBlocks;
+  if (g < 1) g = 1;
+  if (J.M < 1 || J.M > kRowJobsMax) return -1;
+#define NNGP_RSJ(GG)                                                                                         \
+  switch (J.M) {                                                                                           \
+    case 1: hipLaunchKernelGGL((row_stats_jobs_kernel<GG, 1>), dim3(g), dim3(kBlock), 0, st, J, nn, n, b, partials); break; \
+    case 2: hipLaunchKernelGGL((row_stats_jobs_kernel<GG, 2>), dim3(g), dim3(kBlock), 0, st, J, nn, n, b, partials); break; \
+    case 3: hipLaunchKernelGGL((row_stats_jobs_kernel<GG, 3>), dim3(g), dim3(kBlock), 0, st, J, nn, n, b, partials); break; \
+    default: hipLaunchKernelGGL((row_stats_jobs_kernel<GG, 4>), dim3(g), dim3(kBlock), 0, st, J, nn, n, b, partials); break; \
+  }
+  switch (G) {
+    case 4: NNGP_RSJ(4) break;
+    case 8: NNGP_RSJ(8) break;
+    case 16: NNGP_RSJ(16) break;
+    default: NNGP_RSJ(32) break;
+  }
+#undef NNGP_RSJ
+  return g;
+}
+
+// one block per job: the job's partials in reduce4_kernel's order
+__global__ __launch_bounds__(256) void reduce4_jobs_kernel(RowJobs J, const double* __restrict__ partials,
+                                                           int nblocks, double* __restrict__ res) {
+  const int j = blockIdx.x;
+  const double* pj = partials + (size_t)j * kRedBlocks * 4;
+  double acc[4] = {0, 0, 0, 0};
+  for (int p = threadIdx.x; p < nblocks; p += blockDim.x)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] += pj[4 * p + k];
+  block_sum4(acc, res + 4 * J.res_slot[j]);
+}
+
+hipError_t launch_reduce4_jobs(hipStream_t st, const RowJobs& J, const double* partials, int nblocks, double* res) {
+  hipLaunchKernelGGL(reduce4_jobs_kernel, dim3(J.M), dim3(kBlock), 0, st, J, partials, nblocks, res);
+  return hipGetLastError();
+}
+
 // r = B (field - beta0) for every chain in mask in one pass: the row's
 // NNarray entries are read once for all chains; per chain the same products
 // and butterfly as row_stats_kernel (bitwise the same r).  Factor pointers
@@ -657,6 +785,8 @@ __global__ __launch_bounds__(256) void spmv_chains_kernel(const double* const* _
         l = linv_dev[ch][(size_t)k * b + g];
         xv = f.p[ch][idx] - sc[ch].beta0;
       }
+      // (shuffle butterfly: the DPP group_sum measured 134 vs 125 us here --
+      // one reduction per row and chain, latency-bound on the gathers)
       double u = l * xv;
 #pragma unroll
       for (int off = 1; off < G; off <<= 1) u += __shfl_xor(u, off, 64);

@@ -1087,6 +1087,17 @@ __device__ __forceinline__ void sweep_tiles_body(const TileDev& D0, TileLaunch a
     for (int ph = 0; ph < S.nph; ++ph) tile_phase<C, NT, RMAX, GMAX, DB, PROBE, SH, CS>(D, a, sh, S, ph, A, A, GA, GA);
   }
   }  // !XW
+  // r of the tile's local rows back to global memory: the next call can start
+  // from it instead of recomputing r = B w (capi.hip "warm" calls).  Every
+  // tile holding row k applied the same updates to it in the same (colour)
+  // order from the same start, so the copies written by different tiles are
+  // bitwise equal.
+  __syncthreads();
+  for (int lr = t; lr < nrows; lr += NT) {
+    double* rg = const_cast<double*>(D.r) + (size_t)D.erow[row0 + lr] * CS;
+#pragma unroll
+    for (int ch = 0; ch < C; ++ch) rg[ch] = S.r_s[lr * C + ch];
+  }
   if (PROBE == 1 && t == 0) {
     unsigned long long* o = D.dbg + (size_t)T * 8;
     for (int k = 0; k < 8; ++k) o[k] = S.tp[k];

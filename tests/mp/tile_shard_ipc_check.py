@@ -25,6 +25,9 @@ TILES = int(os.environ.get("TILE_SHARD_TILES", "32"))
 def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     os.environ["NNGP_TILES"] = str(TILES)
+    # the one-GPU reference rebuilds r = B w every call, as shard calls do
+    # (a warm call would start from the carried-over r: last bits apart)
+    os.environ["NNGP_SWEEP_WARM"] = "0"
     P = _pkgload.load()
     from conftest import make_problem
     from nngp_amd.shard import ShardContext, init_shard_comm

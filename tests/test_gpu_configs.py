@@ -129,6 +129,7 @@ def test_configs4_tile_shard_r_global_eight_ranks_bitwise(P, c4, capfd, monkeypa
     monkeypatch.delenv("NNGP_ENGINE", raising=False)
     monkeypatch.setenv("NNGP_TILE_R", "global")
     monkeypatch.setenv("NNGP_TILES", "256")
+    monkeypatch.setenv("NNGP_SWEEP_WARM", "0")  # shard calls rebuild r = B w every call: so does the reference
     t0 = time.time()
     n, G = 10_000_000, 8
     locs, NN, col, lm, y, field = (c4[k] for k in ("locs", "NN", "col", "lm", "y", "field"))

@@ -40,6 +40,9 @@ def _fields(ctx, C):
 @pytest.mark.parametrize("G", [2, 4, 8])
 def test_tile_shard_headline_equals_single_gpu_bitwise(P, headline, monkeypatch, G):
     monkeypatch.setenv("NNGP_TILES", "256")
+    # the one-GPU side rebuilds r = B w every call, as shard calls do (a warm
+    # call starts from the r the last call left: the same chain, last bits apart)
+    monkeypatch.setenv("NNGP_SWEEP_WARM", "0")
     locs, NN, col, lm, y = headline
     n, C = len(locs), 3
     cps = [[1.0, 0.05, 0.0], [1.2, 0.04, 0.0], [0.8, 0.06, 0.0]]
