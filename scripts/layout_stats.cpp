@@ -1,0 +1,55 @@
+// Tile-layout statistics (diagnostic): per colour, the rows per thread R of
+// each tile's own batch (mean, max over the tile's neighbourhood, max), ghost
+// cells and foreign slots, at the bench workload.  Build (host only):
+//   g++ -O3 -std=c++17 -I<pkg>/csrc scripts/layout_stats.cpp <pkg>/csrc/graph_prep.cpp -o /tmp/layout_stats
+// usage: layout_stats [n] [m] [tiles] [cell threads] [RMAX]
+#include "graph_prep.h"
+#include <cstdio>
+#include <random>
+#include <algorithm>
+#include <cmath>
+using namespace nngp;
+int main(int argc, char** argv) {
+  int n = argc > 1 ? atoi(argv[1]) : 1000000, m = argc > 2 ? atoi(argv[2]) : 15;
+  int T = argc > 3 ? atoi(argv[3]) : 256, NT = argc > 4 ? atoi(argv[4]) : 448, RMAX = argc > 5 ? atoi(argv[5]) : 8;
+  std::mt19937_64 g(1000); std::uniform_real_distribution<double> U(0, 1);
+  std::vector<double> xy(2 * (size_t)n);
+  for (auto& v : xy) v = U(g);
+  std::vector<int> ord; order_maxmin(xy.data(), n, 2, ord);
+  std::vector<double> lo(2 * (size_t)n);
+  for (int i = 0; i < n; ++i) { lo[i] = xy[ord[i]]; lo[n + i] = xy[n + ord[i]]; }
+  std::vector<int> nn; find_ordered_nn(lo.data(), n, 2, m, nn);
+  std::vector<int> col; int K = greedy_coloring(nn.data(), n, m + 1, col);
+  printf("K=%d\n", K);
+  std::vector<int> csz(K); for (int c : col) csz[c - 1]++;
+  for (int c = 0; c < K; ++c) printf("%d ", csz[c]); printf("\n");
+  TileLayout L; std::string err;
+  if (!build_tile_layout(nn.data(), n, m + 1, col.data(), lo.data(), 2, T, NT, RMAX, L, err)) { printf("err %s\n", err.c_str()); return 1; }
+  printf("max_rows %d max_batches %d max_gslots %d\n", L.max_rows, L.max_batches, L.max_gslots);
+  // per (tile, colour): cells, R, ghost cells, foreign slots
+  long sumR = 0, sumRmaxNb = 0; 
+  std::vector<int> Rtc((size_t)T * K, 0), ctc((size_t)T*K,0);
+  for (int t = 0; t < T; ++t) for (int c = 0; c < K; ++c) {
+    int R = 0, cells = 0;
+    for (int q = L.batch_ptr[t*K+c]; q < L.batch_ptr[t*K+c+1]; ++q) { R += L.batch[q].R; cells += L.batch[q].nthr; }
+    Rtc[t*K+c] = R;
+  }
+  // per colour: mean R, max R, mean over tiles of max R over neighbours
+  double tot_mean = 0, tot_nbmax = 0, tot_max = 0, gh = 0, fs = 0;
+  for (int c = 0; c < K; ++c) {
+    double mean = 0; int mx = 0; double nbm = 0; double gm = 0, fm = 0; int gmx = 0;
+    for (int t = 0; t < T; ++t) {
+      int R = Rtc[t*K+c]; mean += R; mx = std::max(mx, R);
+      int m2 = R;
+      for (int e = L.nb_ptr[t*K+c]; e < L.nb_ptr[t*K+c+1]; ++e) m2 = std::max(m2, Rtc[L.nb[e]*K+c]);
+      nbm += m2;
+      int ng = L.gptr[t*K+c+1]-L.gptr[t*K+c]; gm += ng; gmx = std::max(gmx, ng);
+      fm += L.gslot_ptr[t*K+c+1]-L.gslot_ptr[t*K+c];
+    }
+    printf("c%2d R mean %.2f nbmax %.2f max %d | ghost mean %.0f max %d | fslots mean %.0f\n", c, mean/T, nbm/T, mx, gm/T, gmx, fm/T);
+    tot_mean += mean/T; tot_nbmax += nbm/T; tot_max += mx; gh += gm/T; fs += fm/T;
+  }
+  printf("sum over colours: R mean %.1f nbmax %.1f max %.1f ghost %.0f fslots %.0f\n", tot_mean, tot_nbmax, tot_max, gh, fs);
+  long exported = 0; for (int x = 0; x < n; ++x) if (L.slot_f0[x] & kSlotExported) exported++;
+  printf("exported slots %ld (%.1f%%)\n", exported, 100.0*exported/n);
+}

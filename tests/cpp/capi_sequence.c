@@ -30,6 +30,109 @@ static double jit(int i, int k) {
   return (h & 0xFFFFFF) / (double)0x1000000 - 0.5;
 }
 
+/* The call sequence of the R drop-in's lockstep iteration
+ * (rpkg/R/mcmc_nngp_update_Gaussian.R, update_Gaussian.R:113-311) over 3
+ * chains of one context, 2 iterations, n_chromatic = 2, with the R side's
+ * random draws replaced by fixed numbers and its accept decisions by fixed
+ * log-uniforms (chain 0 always accepts, chain 1 never, chain 2 by the device
+ * value): every device result the host sees is printed in hex (the Python
+ * binding replays the same sequence, tests/test_gpu_capi_sequence.py). */
+static void pr3(const char* tag, int it, const double* v) {
+  printf("%s %d %a %a %a\n", tag, it, v[0], v[1], v[2]);
+}
+
+static int lockstep(nngp_ctx* ctx, int n, double* f) {
+  const int C = 3, all = 7, NC = 2, NIT = 2;
+  double ls[3] = {0.0, 0.2, -0.1}, shape[3] = {-2.3, -2.0, -2.6}, b0[3] = {0.1, -0.2, 0.0};
+  double lnv[3] = {-1.0, -0.7, -1.2};
+  const double lu_anc[3] = {-1e300, 1e300, -0.7}, lu_suf[3] = {1e300, -1e300, -0.3};
+  for (int k = 0; k < C; ++k) {
+    const double cp[3] = {1.0, exp(shape[k]), 0.0};
+    for (int i = 0; i < n; ++i) f[i] = 0.05 * k + sin(3.0 * i / n + k);
+    CHECK(nngp_set_chain(ctx, k), ctx);
+    CHECK(nngp_records_reserve(ctx, NIT), ctx);
+    CHECK(nngp_factor(ctx, 0, NNGP_EXPONENTIAL_ISOTROPIC, cp, 3), ctx);
+    CHECK(nngp_set_field(ctx, f), ctx);
+    CHECK(nngp_set_mu(ctx, NULL, b0[k]), ctx);
+  }
+  for (int it = 1; it <= NIT; ++it) {
+    double nls[3], nsh[3], cps[9], dls[3], v[3], l1[3], l0[3], ssr[3];
+    int st[3];
+    /* ancillary covariance update (:113-157) */
+    for (int k = 0; k < C; ++k) {
+      nls[k] = ls[k] + 0.05 * (k + 1) * (it % 2 ? 1.0 : -1.0);
+      nsh[k] = shape[k] + 0.02 * (k - 1);
+      cps[3 * k] = 1.0; cps[3 * k + 1] = exp(nsh[k]); cps[3 * k + 2] = 0.0;
+      dls[k] = nls[k] - ls[k];
+    }
+    CHECK(nngp_factor_chains(ctx, 1, all, NNGP_EXPONENTIAL_ISOTROPIC, cps, 3, st), ctx);
+    CHECK(nngp_ancillary_propose_chains(ctx, all, b0, dls), ctx);
+    CHECK(nngp_field_response_ratio_chains(ctx, all, b0, lnv, v), ctx);
+    pr3("ratio", it, v);
+    for (int k = 0; k < C; ++k)
+      if (st[k] == 0 && v[k] > lu_anc[k]) {
+        shape[k] = nsh[k]; ls[k] = nls[k];
+        CHECK(nngp_set_chain(ctx, k), ctx);
+        CHECK(nngp_accept_field(ctx), ctx);
+        CHECK(nngp_accept_factor(ctx), ctx);
+      }
+    /* sufficient covariance update (:165-213) */
+    for (int k = 0; k < C; ++k) {
+      nls[k] = ls[k] - 0.03 * (k + 1);
+      nsh[k] = shape[k] + 0.01 * (2 - k);
+      cps[3 * k] = 1.0; cps[3 * k + 1] = exp(nsh[k]); cps[3 * k + 2] = 0.0;
+    }
+    CHECK(nngp_factor_chains(ctx, 1, all, NNGP_EXPONENTIAL_ISOTROPIC, cps, 3, st), ctx);
+    CHECK(nngp_loglik_chains(ctx, 1, all, b0, nls, l1), ctx);
+    CHECK(nngp_loglik_chains(ctx, 0, all, b0, ls, l0), ctx);
+    pr3("l1", it, l1);
+    pr3("l0", it, l0);
+    for (int k = 0; k < C; ++k) {
+      if (st[k] == 0 && l1[k] - l0[k] > lu_suf[k]) {
+        shape[k] = nsh[k]; ls[k] = nls[k];
+        CHECK(nngp_set_chain(ctx, k), ctx);
+        CHECK(nngp_accept_factor(ctx), ctx);
+      }
+      /* field mean (:219-224) */
+      double oqo = 0, oqf = 0;
+      CHECK(nngp_set_chain(ctx, k), ctx);
+      CHECK(nngp_beta0_stats(ctx, &oqo, &oqf), ctx);
+      printf("beta0_stats %d %d %a %a\n", it, k, oqo, oqf);
+      b0[k] = 0.5 * oqf / oqo + 0.1 * k;
+      CHECK(nngp_set_mu(ctx, NULL, b0[k]), ctx);
+    }
+    /* chromatic sweeps of every chain, one call (:257-275) */
+    const uint64_t seed[3] = {11, 12, 13};
+    const uint64_t cb[3] = {(uint64_t)(it - 1) * NC, (uint64_t)(it - 1) * NC, (uint64_t)(it - 1) * NC};
+    CHECK(nngp_sweep_chains(ctx, NC, b0, ls, lnv, seed, cb), ctx);
+    /* noise variance (:281-293) */
+    CHECK(nngp_sum_squared_residuals_chains(ctx, all, b0, ssr), ctx);
+    pr3("ssr", it, ssr);
+    for (int k = 0; k < C; ++k) lnv[k] += ssr[k] > n * exp(lnv[k]) ? 0.01 : -0.01;
+    /* records (:305-311) */
+    for (int k = 0; k < C; ++k) {
+      CHECK(nngp_set_chain(ctx, k), ctx);
+      CHECK(nngp_record_field(ctx, it - 1), ctx);
+    }
+  }
+  double* rec = malloc(sizeof(double) * (size_t)NIT * n);
+  for (int k = 0; k < C; ++k) {
+    CHECK(nngp_set_chain(ctx, k), ctx);
+    CHECK(nngp_get_records(ctx, 0, NIT, rec), ctx);
+    for (int r = 0; r < NIT; ++r) {
+      printf("record %d %d", k, r);
+      for (int i = 0; i < n; ++i) printf(" %a", rec[(size_t)r * n + i]);
+      printf("\n");
+    }
+    CHECK(nngp_get_field(ctx, f), ctx);
+    printf("field %d", k);
+    for (int i = 0; i < n; ++i) printf(" %a", f[i]);
+    printf("\n");
+  }
+  free(rec);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 3000, m = argc > 2 ? atoi(argv[2]) : 10, d = 2, b = m + 1;
   const int side = (int)ceil(sqrt((double)n));
@@ -55,6 +158,14 @@ int main(int argc, char** argv) {
     lm[i] = i + 1;
     y[i] = sin(6 * locs[i]) + cos(4 * locs[i + n]) + 0.3 * jit(i, 2);
     f[i] = y[i] + 0.1 * jit(i, 3);
+  }
+  if (argc > 3) {  /* "lockstep": the R drop-in's 3-chain iteration */
+    CHECK(nngp_ctx_create(locs, n, d, NN, b, col, lm, y, n, 3, 0, &ctx), ctx);
+    printf("colours %d\n", K);
+    if (lockstep(ctx, n, f)) return 1;  /* (CHECK destroyed the context) */
+    nngp_ctx_destroy(ctx);
+    free(raw); free(locs); free(order); free(NN); free(col); free(lm); free(y); free(f);
+    return 0;
   }
   CHECK(nngp_ctx_create(locs, n, d, NN, b, col, lm, y, n, 2, 0, &ctx), ctx);
   const double cp[2][3] = {{1.0, 0.1, 0.0}, {0.8, 0.15, 0.0}};
