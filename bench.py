@@ -12,8 +12,14 @@ n_chains, initialize.R:9, which it runs concurrently with mclapply).  The
 chains of a GPU share one context and sweep in the same kernels
 (nngp_sweep_chains).  value = chain-sweeps/s over all GPUs.  The timed region
 runs the reference's per-iteration call shape: n_chromatic = 10 sweeps per
-call (r = B w refresh + 10 sweeps).  A single-chain context is timed too
-("single_chain" in config).
+call.  Calls back to back with the field, factor and beta_0 unchanged are
+"warm" (the call starts from the slot-order w and r = B w the previous call
+left; DESIGN.md §3 "Round 3", pinned to cold calls by
+tests/test_gpu_warm_calls.py); every call shape the timed region uses is
+captured as a hipGraph before it (cold and warm), so no capture lands inside
+t0..t1.  The cold rate (r = B w rebuilt every call, what an MCMC iteration
+runs since beta_0 is redrawn every iteration) is timed beside it
+("cold_calls" in config), and a single-chain context too ("single_chain").
 Multi-GPU (N > 1): the tile-sharded sweep of ONE field whose
 size grows with N (n = N x 1e6; every GPU keeps the tile geometry of the
 n=1e6 headline): weak scaling, value = chain-sweeps/s x n/1e6.  A small
@@ -438,7 +444,15 @@ def main():
     ap.add_argument("--shard", action="store_true", help="the sharded sweep even at N = 1 (strong)")
     ap.add_argument("--no-fallback", action="store_true",
                     help="(default; kept for old command lines) a failed sharded sweep prints a null value")
+    ap.add_argument("--workload", choices=["headline", "configs4"], default="headline",
+                    help="configs4: BASELINE.json configs[4] exactly -- ONE field of n = 1e7, m = 20 (Matern 3/2) "
+                         "swept by all N GPUs (the tile shard, strong scaling; at N = 1 the one-GPU engine): "
+                         "python -m torch.distributed.run --nproc-per-node 8 bench.py --gpus 8 --workload configs4")
     args = ap.parse_args()
+    if args.workload == "configs4":
+        args.n, args.m = 10_000_000, 20
+        args.multi = "shard-strong"
+        args.shard = True
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -488,18 +502,34 @@ def main():
     nc = args.n_chromatic
     b0, ls, lnv = wl["beta0"], wl["log_scale"], wl["log_noise_variance"]
 
-    def timed(ctx, steps, warmup):
-        """warmup + steps sweeps of every chain of ctx in calls of n_chromatic"""
+    def timed(ctx, steps, warmup, cold=False):
+        """warmup + steps sweeps of every chain of ctx in calls of n_chromatic.
+        cold: beta_0 alternates by 1e-9 between calls, so every call rebuilds
+        w -> slots and r = B w (the MCMC call shape) instead of running warm."""
         k = ctx.n_chains
+        calls = [0]
+
+        def call(s, base):
+            bb = b0 + (1e-9 if cold and calls[0] % 2 else 0.0)
+            calls[0] += 1
+            ctx.sweep_chains(s, [bb] * k, [ls] * k, [lnv] * k, seeds[:k], [base] * k)
 
         def run(nsw, base):
             done = 0
             while done < nsw:
                 s = min(nc, nsw - done)
-                ctx.sweep_chains(s, [b0] * k, [ls] * k, [lnv] * k, seeds[:k], [base + done] * k)
+                call(s, base + done)
                 done += s
             return base + done
 
+        # capture every call shape of the timed region before it: the first
+        # call of a shape (and of its warm form) captures and instantiates a
+        # hipGraph (capi.hip graph_for), which must not land inside t0..t1.
+        # Two calls per shape: the second is warm (warm mode) or cold (cold
+        # mode, beta_0 alternates) -- the form every timed call takes
+        for s in sorted({min(nc, steps)} | ({steps % nc} if steps % nc else set())):
+            for _ in range(2):
+                call(s, 1 << 40)
         sync = (lambda: torch.cuda.synchronize(local_rank)) if torch.cuda.is_available() else (lambda: None)
         return timed_region(run, steps, warmup, dist, sync)
 
@@ -518,6 +548,10 @@ def main():
         f"entries={info['n_entries']} engine={info['sweep_engine']} tiles={info['n_tiles']} chunks={info['n_chunks']} "
         f"max_collen={info['max_collen']}", rank)
     elapsed, ctr = timed(ctx, args.steps, args.warmup)
+    el_cold, ctr = timed(ctx, args.steps, args.warmup, cold=True)
+    cold_calls = {"value": args.steps * C * world / el_cold, "unit": "sweeps/s",
+                  "ms_per_step": el_cold * 1e3 / args.steps,
+                  "how": "beta_0 alternates by 1e-9 between calls: every call rebuilds w -> slots and r = B w"}
 
     # per-kernel timing with HIP events on the context's own stream: the
     # sweep kernel's launches alone (tile engine: one persistent launch per
@@ -588,6 +622,7 @@ def main():
                                         if os.environ.get("NNGP_SWEEP_WARM", "1") != "0" and info["sweep_engine"] == 1
                                         else "cold: w -> slots and r = B w rebuilt every call"),
                       "single_chain": single,
+                      "cold_calls": cold_calls,
                       "parallelism": f"chains {C} per GPU x {world} GPUs (independent)"},
            "roofline": roofline, "cpu_baseline": cpu, "secondary": mcmc}
     if rank == 0:

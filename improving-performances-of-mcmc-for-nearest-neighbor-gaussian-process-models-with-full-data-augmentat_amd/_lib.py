@@ -36,7 +36,7 @@ ABI_SYMBOLS = (
     "nngp_loglik", "nngp_sweep", "nngp_sweep_chains", "nngp_ancillary_propose", "nngp_ancillary_propose_chains",
     "nngp_field_response_ratio",
     "nngp_accept_field", "nngp_beta0_stats", "nngp_sum_squared_residuals", "nngp_spmv",
-    "nngp_tri_solve", "nngp_sweep_timed", "nngp_device_normals",
+    "nngp_tri_solve", "nngp_sweep_timed", "nngp_device_normals", "nngp_get_sweep_r",
     "nngp_ctx_create_shard", "nngp_shard_unique_id", "nngp_shard_comm_init", "nngp_sweep_chains_group",
     "nngp_records_reserve", "nngp_record_field", "nngp_get_records",
     "nngp_shard_ipc_handle", "nngp_shard_ipc_open", "nngp_shard_sync",
@@ -118,6 +118,7 @@ def _load():
     L.nngp_sweep_timed.argtypes = [_vp, C.c_int, _dp, _dp, _dp, _up, _up,
                                    C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.nngp_device_normals.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_int, _dp]
+    L.nngp_get_sweep_r.argtypes = [_vp, _dp]
     L.nngp_ctx_create_shard.argtypes = [_dp, C.c_int, C.c_int, _ip, C.c_int, _ip, _ip, _dp, C.c_int,
                                         C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_vp)]
     L.nngp_shard_unique_id.argtypes = [C.c_char_p, C.c_int]

@@ -175,6 +175,13 @@ class ChainContext:
                                        C.byref(kms) if per_kernel else None))
         return ms.value, (kms.value if per_kernel else None)
 
+    def get_sweep_r(self) -> np.ndarray:
+        """r = B (field - beta0) of the selected chain as the last sweep call
+        left it (location order): the state a warm tile call starts from."""
+        out = np.empty(self.n, np.float64)
+        self._chk(lib.nngp_get_sweep_r(self._h, out))
+        return out
+
     def ancillary_propose(self, beta0: float, dlog_scale: float) -> None:
         self._chk(lib.nngp_ancillary_propose(self._h, float(beta0), float(dlog_scale)))
 

@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -147,6 +148,7 @@ struct nngp_ctx {
   bool warm_on = false;           // warm sweep calls allowed (tile engine, not a shard; NNGP_SWEEP_WARM=0: off)
   bool tcs = false;               // chain-split tile launches (one chain per workgroup, kernels.hip sweep_tiles_cs_kernel)
   int txw = 0;                    // exchange-wave tiles (tiles.hip tile_phase_xw): layout cut for NT - 64 cell threads
+  int tpf = 0;                    // exchange-wave L2 prefetch bits (TileDev::pf; NNGP_TILE_PF)
   int cus = 0;                    // compute units of the device
   int tresident = 0;              // tile workgroups resident per CU (occupancy query of the instantiation)
   int engine_fallback = 0;        // 0: none, 1: tile layout unsuitable (LDS, shape), 2: residency, 3: forced colours
@@ -300,6 +302,7 @@ TileDev tile_dev(nngp_ctx* c) {
   D.dbg = c->tdbg_d;
   D.probe = c->tprobe;
   D.xw = c->txw;
+  D.pf = c->txw ? c->tpf : 0;
   D.K = c->tl.K;
   D.C = c->C;
   D.T = c->tl.T;
@@ -322,6 +325,20 @@ int refresh_sweep_values(nngp_ctx* c, int k) {
   c->linv_cur_h[k] = c->ch[k].linv_d[0];
   HIPCHK(c, launch_set_ptr(c->st, c->linv_cur_d, k, c->ch[k].linv_d[0]));
   return NNGP_OK;
+}
+
+// Persistent tile launches: every workgroup spins on its neighbours'
+// granules, so all workgroups of a launch must be resident at once.  Two such
+// launches on one device at the same time -- two contexts swept from two host
+// threads, each on its own stream -- could each hold part of the CUs and wait
+// for the rest forever.  A call of this process that launches tiles on a
+// device holds that device's lock from before the launch to the host sync
+// after it: one persistent tile launch per device at a time.  (Other work --
+// factor, solves -- is not held back: it does not wait on other workgroups of
+// another launch and drains by itself.)
+std::mutex& tile_lock(int device) {
+  static std::mutex locks[64];
+  return locks[device & 63];
 }
 
 // reduce partials to res_d and copy 4 doubles to the host (synchronises)
@@ -588,6 +605,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
                                   split);
       c->tl.NTK = NT;
       c->txw = xw ? xwm : 0;
+      if (const char* pf = std::getenv("NNGP_TILE_PF")) c->tpf = std::atoi(pf) & 7;
       if (ok && csplit) {
         // n_chains workgroups of one chain per CU
         const int need1 = tile_lds_bytes(c->tl.max_rows, 1, NT, c->tl.K, c->tl.max_batches, c->tl.max_gslots);
@@ -1591,6 +1609,8 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
     if (z) return fail_msg(c, NNGP_ERR_ARG, "sweep: injected normals are not supported on shard contexts");
     return shard_call(c, n_sweeps, mask);
   }
+  std::unique_lock<std::mutex> tlk;
+  if (c->engine == 1) tlk = std::unique_lock<std::mutex>(tile_lock(c->device));
   if (z) {
     // injected normals -> compact order, chain-interleaved
     const size_t need = (size_t)n_sweeps * c->C * c->n;
@@ -1633,10 +1653,13 @@ int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const doub
     if ((rc = sweep_prepare(c, k, beta0[k], log_scale[k], lnv[k], seed[k], counter_base[k]))) return rc;
   if ((rc = upload_scalars(c))) return rc;
   if (sharded_call(c)) return shard_call(c, n_sweeps, all);
+  std::unique_lock<std::mutex> tlk;
+  if (c->engine == 1) tlk = std::unique_lock<std::mutex>(tile_lock(c->device));
   hipGraphExec_t ex;
   if ((rc = graph_for(c, n_sweeps, all, &ex, warm ? kColours | kEpilogue : kAll))) return rc;
   HIPCHK(c, hipGraphLaunch(ex, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
+  tlk = std::unique_lock<std::mutex>();
   if ((rc = tile_timeout_check(c))) return rc;
   warm_set(c, all, beta0);
   if (c->tdbg_d) {
@@ -1841,6 +1864,7 @@ static int tile_shard_call(nngp_ctx* c, int n_sweeps, int mask) {
     return fail_msg(c, NNGP_ERR_STATE, "tile shard: the other ranks' granule buffers are not open (nngp_shard_ipc_open)");
   if (!c->rmask_d || c->tG < 2) return fail_msg(c, NNGP_ERR_STATE, "tile shard: no remote-reader plan");
   int rc;
+  std::lock_guard<std::mutex> tlk(tile_lock(c->device));
   if ((rc = enqueue_sweep_body(c, n_sweeps, mask, nullptr, kPrologue))) return rc;
   HIPCHK(c, launch_tile_call_bump(c->st, c->ctl_d));
   TileShard sh;
@@ -1996,6 +2020,13 @@ static int tile_group_call(nngp_ctx** ctxs, int G, int n_sweeps, const double* b
   if (n_sweeps == 0) return NNGP_OK;
   const int Tl = c0->tTl, mask = (1 << c0->C) - 1;
   int rc;
+  // every device of the group, in device order (no lock-order inversion)
+  std::vector<int> devs_used;
+  for (int g = 0; g < G; ++g) devs_used.push_back(ctxs[g]->device);
+  std::sort(devs_used.begin(), devs_used.end());
+  devs_used.erase(std::unique(devs_used.begin(), devs_used.end()), devs_used.end());
+  std::vector<std::unique_lock<std::mutex>> tlks;
+  for (int dv : devs_used) tlks.emplace_back(tile_lock(dv));
   std::vector<hipEvent_t> ev(2 * G, nullptr);  // [g]: prologue of rank g done; [G + g]: launch of rank g's device done
   auto cleanup = [&] {
     for (auto e : ev) if (e) hipEventDestroy(e);
@@ -2178,6 +2209,8 @@ int nngp_sweep_timed(nngp_ctx* c, int n_sweeps, const double* beta0, const doubl
     if ((rc = sweep_prepare(c, k, beta0[k], log_scale[k], lnv[k], seed[k], counter_base[k]))) return rc;
   if ((rc = upload_scalars(c))) return rc;
   const int mask = (1 << c->C) - 1;
+  std::unique_lock<std::mutex> tlk;
+  if (c->engine == 1) tlk = std::unique_lock<std::mutex>(tile_lock(c->device));
   hipGraphExec_t pro, col, epi;
   if ((rc = graph_for(c, n_sweeps, mask, &pro, kPrologue))) return rc;
   if ((rc = graph_for(c, n_sweeps, mask, &col, kColours))) return rc;
@@ -2203,6 +2236,17 @@ int nngp_sweep_timed(nngp_ctx* c, int n_sweeps, const double* beta0, const doubl
   for (auto& x : e) hipEventDestroy(x);
   if ((rc = tile_timeout_check(c))) return rc;
   warm_set(c, mask, beta0);
+  return NNGP_OK;
+}
+
+int nngp_get_sweep_r(nngp_ctx* c, double* r) {
+  if (!c || !r) return NNGP_ERR_ARG;
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  std::vector<double> h((size_t)c->n * c->C);
+  HIPCHK(c, hipMemcpyAsync(h.data(), c->r_d, h.size() * sizeof(double), hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  for (int i = 0; i < c->n; ++i) r[i] = h[(size_t)c->dpos[i] * c->C + c->cur];
   return NNGP_OK;
 }
 

@@ -104,6 +104,16 @@ constexpr uint32_t kCellEnd = 1u << 31;
 constexpr int kSlotExported = 1 << 30;  // slot_f0 flag: dw of the slot is read by other tiles
 constexpr int kTileSlotsMax = 256;      // slots per own batch
 
+// dynamic LDS of one sweep_tiles_kernel workgroup (tiles.hip sweep_tiles_body
+// lays it out in this order): r of max_rows local rows x C (0: r in global
+// memory), slot totals kTileSlotsMax x C, NT/64 wave totals x C, C x 4 scalars,
+// the dw of max_gslots foreign slots x C, max_batches batch records, 4 x (K+1)
+// colour pointers, NT/64 wave flags, 64 B of probe words.  Host code (the
+// engine choice at context creation, the layout checks of tests/cpp) and the
+// launch use this one definition.
+int tile_lds_bytes(int max_rows, int C, int NT, int K, int max_batches, int max_gslots);
+constexpr int kTileCuLds = 160 * 1024;  // LDS per CU (MI355X)
+
 // nthr = ceil(cells / R): threads holding cells (the others hold padding only)
 struct TileBatch { int off, R, nslots, slot0, nthr; };
 

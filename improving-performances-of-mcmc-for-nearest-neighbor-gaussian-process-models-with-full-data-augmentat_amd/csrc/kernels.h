@@ -193,6 +193,8 @@ struct TileDev {
   int probe = 0;              // dbg layout: 1 = per-tile segment sums (T x 8), 2 = timeline (T x 512 phases x 8)
   int xw = 0;                 // exchange-wave tiles: the last wave polls the hand-offs, the
                               // layout's batches are cut for NT - 64 cell threads
+  int pf = 0;                 // exchange-wave L2 prefetch during the own work (bit 1: the next
+                              // batch's cells, 2: its per-slot records, 4: this colour's ghost cells)
 };
 
 struct TileLaunch {
@@ -202,7 +204,6 @@ struct TileLaunch {
   int stagger = 0;            // chain-split: chain k starts k x stagger ticks (100 MHz) late
 };
 
-int tile_lds_bytes(int max_rows, int C, int NT, int K, int max_batches, int max_gslots);
 // cells per thread of an own batch (the layout's RMAX): two batches of C
 // chains stay in registers (C >= 3: fewer cells per batch)
 // double-buffered batch registers (the next colour's loads in flight during

@@ -3,6 +3,7 @@
 // exchange kernels and the tile-layout value refresh (A5).  gfx950.
 #include "kernels.h"
 #include "device_common.h"
+#include "graph_prep.h"
 
 namespace nngp {
 
@@ -35,18 +36,15 @@ namespace nngp {
 // reader sees a later value; the call id (bumped on the device before every
 // launch) keeps granules of earlier calls from matching.  Spins are bounded: a
 // timeout sets ctl[1] and the launch drains (the host reports an error).
-constexpr uint32_t kTPad = (1u << 17) - 1;
-constexpr uint32_t kTStart = 1u << 30, kTEnd = 1u << 31;
-constexpr int kTExported = 1 << 30;
-constexpr int kTSlots = 256;       // slots per own batch (graph_prep.h kTileSlotsMax)
+// the cell / slot encoding of the host layout (graph_prep.h), one definition
+constexpr uint32_t kTPad = kTilePadRow;
+constexpr uint32_t kTStart = kCellStart, kTEnd = kCellEnd;
+constexpr int kTExported = kSlotExported;
+constexpr int kTSlots = kTileSlotsMax;  // slots per own batch
+static_assert(kTileQShift == kTileRowBits && kTileQMask + 1 >= (uint32_t)kTSlots && kTileRowBits + 11 <= 30,
+              "cell_pk fields: local row | slot << kTileQShift | start << 30 | end << 31");
 constexpr int kTSpreadLds = 82 * 1024;  // LDS floor: at most one tile per CU
-constexpr int kTCuLds = 160 * 1024;     // LDS per CU
 
-int tile_lds_bytes(int max_rows, int C, int NT, int K, int max_batches, int max_gslots) {
-  const int rbytes = ((max_rows * C * 8 + 15) / 16) * 16;
-  return rbytes + kTSlots * C * 8 + (NT / 64) * C * 8 + 4 * C * 8 + ((max_gslots * C + 1) / 2) * 16 +
-         max_batches * 16 + 4 * (K + 1) * 4 + (NT / 64) * 4 + 64;
-}
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
@@ -354,7 +352,11 @@ __device__ __forceinline__ void seg_scan_step(double (&v)[C], int& f) {
 
 // one own batch of colour c (epoch): products -> slot totals -> draws ->
 // scatter.  LDS and registers only, plus the draws' stores: no global load
-// (a load here would wait behind the next batch's prefetch, vmcnt is in order)
+// (a load here would wait behind the next batch's prefetch, vmcnt is in order).
+// Workgroup barriers inside it: kOwnDrawBarriers -- the exchange wave, which
+// holds no cells, passes exactly as many per batch (tile_phase_xw); a barrier
+// added or removed here must change this count.
+constexpr int kOwnDrawBarriers = 3;
 template <int C, int NT, int RMAX, int PROBE, int SH, int CS = C>
 __device__ __forceinline__ void tile_own_draw(const TileDev& D, const TileLaunch& a, const TileShard& sh, TileState& S,
                                               TileBatchRegs<C, NT, RMAX>& b, unsigned epoch) {
@@ -388,7 +390,7 @@ __device__ __forceinline__ void tile_own_draw(const TileDev& D, const TileLaunch
       }
       seen_start |= st;
       if (b.pk[j] & kTEnd) {
-        const int q = (int)((b.pk[j] >> 17) & 0x7FF);
+        const int q = (int)((b.pk[j] >> kTileQShift) & kTileQMask);
         if (seen_start) {
 #pragma unroll
           for (int ch = 0; ch < C; ++ch) acc_s[q * C + ch] = run[ch];
@@ -496,7 +498,7 @@ __device__ __forceinline__ void tile_own_scatter(TileState& S, const TileBatchRe
       const int j = j0 + jj;
       const uint32_t lr = tile_lr(b.pk[j]);
       const bool ok = j < R && lr != kTPad;
-      const int row = ok ? (int)lr : 0, q = ok ? (int)((b.pk[j] >> 17) & 0x7FF) : 0;
+      const int row = ok ? (int)lr : 0, q = ok ? (int)((b.pk[j] >> kTileQShift) & kTileQMask) : 0;
 #pragma unroll
       for (int ch = 0; ch < C; ++ch) {
         rv[jj][ch] = r_s[row * C + ch];
@@ -799,6 +801,68 @@ __device__ __forceinline__ void tile_phase_ib(const TileDev& D, const TileLaunch
 // threads ("cell waves") scatter, prepare the next batch and stream its cells.
 // The layout's batches are cut for NT - 64 cell threads.
 
+// L2 prefetch by the exchange wave (TileDev::pf): the bytes the cell waves
+// load after this phase's draw -- the next phase's first batch (per-slot
+// records, cells) and this colour's ghost cells -- are touched at the phase
+// start, one 4-B load per 64-B segment (default cache policy: the lines
+// stay in the XCD's L2), so their HBM stream runs during the own work (LDS
+// only) instead of in one burst of every CU after the draw.  The values are
+// never used; the exchange wave's wait before its polls covers the loads.
+constexpr int kPfLoads = 40;  // per lane: 64 x 40 segments = 160 KB per phase at most
+template <int C, int NTC>
+__device__ __forceinline__ void tile_xw_prefetch(const TileDev& D, const TileState& S, int ph, int lane,
+                                                 uint32_t (&pf)[kPfLoads]) {
+  constexpr int NR = 4 + 2 * C + 1 + C;
+  uintptr_t base[NR];
+  int nseg[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) { base[r] = 0; nseg[r] = 0; }
+  int r = 0;
+  auto region = [&](const void* p, long long bytes, bool on) {
+    const uintptr_t b0 = reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)63;
+    const uintptr_t b1 = (reinterpret_cast<uintptr_t>(p) + (uintptr_t)bytes + 63) & ~(uintptr_t)63;
+    base[r] = b0;
+    nseg[r] = on && bytes > 0 ? (int)((b1 - b0) >> 6) : 0;
+    ++r;
+  };
+  const int K = S.K, c = ph % K, phn = ph + 1, cn = phn % K;
+  const bool more = phn < S.nph && S.bptr_s[cn] < S.bptr_s[cn + 1];
+  const int4 Bn = more ? S.batch_s[S.bptr_s[cn]] : make_int4(0, 0, 0, 0);
+  const bool rec = more && (D.pf & 2), cel = more && (D.pf & 1);
+  const long long ncell = (long long)(Bn.y & 0xFFFF) * NTC;
+  const int ns = Bn.z, x0 = Bn.w;
+  region(D.sinfo + x0, (long long)ns * 8, rec);
+  region(D.slot_loc + x0, (long long)ns * 4, rec);
+  region(D.dr + (size_t)x0 * C, (long long)ns * C * 16, rec);
+  region(D.w_slot + (size_t)x0 * C, (long long)ns * C * 8, rec);
+  region(D.cell_pk + Bn.x, ncell * 4, cel);
+#pragma unroll
+  for (int ch = 0; ch < C; ++ch) region(D.cell_val + ch * D.n_cells + Bn.x, ncell * 8, cel);
+  const int g0 = S.gptr_s[c], g1 = S.gptr_s[c + 1];
+  const bool gh = (D.pf & 4) && g1 > g0;
+  region(D.gcell + g0, (long long)(g1 - g0) * 8, gh);
+#pragma unroll
+  for (int ch = 0; ch < C; ++ch) region(D.gval + ch * D.n_gcells + g0, (long long)(g1 - g0) * 8, gh);
+  int tot = 0;
+#pragma unroll
+  for (int q = 0; q < NR; ++q) tot += nseg[q];
+#pragma unroll
+  for (int k = 0; k < kPfLoads; ++k) {
+    const int i = k * 64 + lane;
+    pf[k] = 0u;
+    if (k * 64 < tot && i < tot) {
+      int acc = 0;
+      uintptr_t a = 0;
+#pragma unroll
+      for (int q = 0; q < NR; ++q) {
+        if (i >= acc && i < acc + nseg[q]) a = base[q] + (uintptr_t)(i - acc) * 64;
+        acc += nseg[q];
+      }
+      pf[k] = *reinterpret_cast<const uint32_t*>(a);
+    }
+  }
+}
+
 // the exchange wave's phase: its share of the colour's ghost cells (static
 // data: loaded at the phase start, long in registers when the hand-off
 // ends), the own batches' barriers, then the hand-off polls -> gdw_s, and its
@@ -821,12 +885,18 @@ __device__ __forceinline__ void tile_phase_xw(const TileDev& D, TileState& S, in
     const int u = k * 64 + lane;
     gx[k] = u < nfi ? D.gslot[gs0 + u / C] : 0;
   }
-  // the own batches' barriers (tile_own_draw: 3 each, + 1 before a later batch)
+  uint32_t pfv[kPfLoads];
+  if (D.pf) tile_xw_prefetch<C, NT - 64>(D, S, ph, lane, pfv);
+  // the own batches' barriers (tile_own_draw: kOwnDrawBarriers each, + 1
+  // before a later batch, as tile_phase_cells)
   for (int bi = bfirst; bi < bend; ++bi) {
     if (bi != bfirst) __syncthreads();
-    __syncthreads();
-    __syncthreads();
-    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kOwnDrawBarriers; ++q) __syncthreads();
+  }
+  if (D.pf) {  // the prefetch has landed (its registers are free again) before the polls go out
+#pragma unroll
+    for (int k = 0; k < kPfLoads; ++k) asm volatile("" ::"v"(pfv[k]));
   }
   // hand-off: every (foreign slot, chain) of colour c until its granule
   // carries this epoch -> gdw_s (polls in flight per lane; a retry waits for
@@ -1219,9 +1289,9 @@ static hipError_t launch_tiles_cs(hipStream_t st, const TileDev& D, const TileLa
   constexpr int NT = 256;
   auto k = sweep_tiles_cs_kernel<CS, NT, tile_rmax_cs(NT), tile_gmax(NT)>;
   // LDS floor: at most CS workgroups per CU
-  const int floor = kTCuLds / (CS + 1) + 64;
+  const int floor = kTileCuLds / (CS + 1) + 64;
   lds = lds < floor ? floor : lds;
-  if (lds * CS > kTCuLds) return hipErrorInvalidValue;
+  if (lds * CS > kTileCuLds) return hipErrorInvalidValue;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return e;
   if (occ) return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, reinterpret_cast<const void*>(k), NT, lds);

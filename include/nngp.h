@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define NNGP_ABI_VERSION 9
+#define NNGP_ABI_VERSION 10
 #define NNGP_SHARD_ID_BYTES 128 /* RCCL unique id */
 #define NNGP_IPC_HANDLE_BYTES 192 /* HIP IPC handles of a tile shard's granule buffer, w replica, flags */
 
@@ -297,6 +297,11 @@ int nngp_sweep_timed(nngp_ctx* ctx, int n_sweeps, const double* beta0, const dou
                      const uint64_t* counter_base, double* ms, double* kernel_ms);
 /* Philox normals generated by the device code path (test hook). */
 int nngp_device_normals(int device, uint64_t seed, uint64_t sweep, int n, double* z);
+/* r = B (field - beta0) of the selected chain as the last sweep call left it
+ * (location order, length n): the state a warm tile call starts from (the
+ * tile kernel writes its r back).  Introspection for the
+ * warm-call drift tests -- nngp_spmv gives the fresh product to compare. */
+int nngp_get_sweep_r(nngp_ctx* ctx, double* r);
 
 #ifdef __cplusplus
 }

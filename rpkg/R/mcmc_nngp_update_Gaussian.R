@@ -233,6 +233,12 @@ mcmc_nngp_update_Gaussian <- function(locs, X, observed_field, space_time_model,
     # ---- chromatic sampling of every chain's field, one call (:257-275)
     nngp_sweep_chains(ctx, n_chromatic, vec("beta_0"), vec("log_scale"), vec("log_noise_variance"),
                       iter_start + seq_len(C), rep((iter_start + it - 1) * n_chromatic, C))
+    # a tile-shard context without a communicator (the same script run on
+    # every rank, one GPU each) has only its halo exchanged after the sweep:
+    # the full exchange of the field replicas is this explicit collective,
+    # at the same point on every rank, before anything below reads the field
+    # (a no-op on every other context)
+    nngp_shard_sync(ctx)
     # ---- noise variance (:281-293)
     ssr <- nngp_sum_squared_residuals_chains(ctx, all_chains, vec("beta_0"))
     for (i in seq_len(C)) {

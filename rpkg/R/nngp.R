@@ -92,6 +92,8 @@ nngp_spmv <- function(ctx, which, X) .Call(C_nngp_spmv, ctx, as.integer(which), 
 nngp_tri_solve <- function(ctx, which, u) .Call(C_nngp_tri_solve, ctx, as.integer(which), as.double(u))
 nngp_device_normals <- function(device, seed, sweep, n)
   .Call(C_nngp_device_normals, as.integer(device), as.double(seed), as.double(sweep), as.integer(n))
+# r = B (field - beta0) of the selected chain as the last sweep call left it (warm-call state)
+nngp_get_sweep_r <- function(ctx) .Call(C_nngp_get_sweep_r, ctx)
 
 nngp_shard_unique_id <- function() .Call(C_nngp_shard_unique_id)
 nngp_shard_comm_init <- function(ctx, id) invisible(.Call(C_nngp_shard_comm_init, ctx, id))

@@ -381,6 +381,14 @@ SEXP C_nngp_device_normals(SEXP device, SEXP seed, SEXP sweep, SEXP n) {
   return z;
 }
 
+SEXP C_nngp_get_sweep_r(SEXP p) {
+  nngp_ctx* c = get_ctx(p);
+  SEXP r = PROTECT(Rf_allocVector(REALSXP, ctx_n(c)));
+  check(nngp_get_sweep_r(c, REAL(r)), c);
+  UNPROTECT(1);
+  return r;
+}
+
 /* ---------- sharded sweep (colour shard / tile shard) ---------- */
 SEXP C_nngp_shard_unique_id(void) {
   SEXP id = PROTECT(Rf_allocVector(RAWSXP, NNGP_SHARD_ID_BYTES));
@@ -539,6 +547,7 @@ static const R_CallMethodDef call_methods[] = {
     E(C_nngp_spmv, 3),
     E(C_nngp_tri_solve, 3),
     E(C_nngp_device_normals, 4),
+    E(C_nngp_get_sweep_r, 1),
     E(C_nngp_shard_unique_id, 0),
     E(C_nngp_shard_comm_init, 2),
     E(C_nngp_sweep_chains_group, 7),

@@ -47,7 +47,8 @@ int main(int argc, char** argv) {
   const int RMAX = argc > 7 ? std::atoi(argv[7]) : 16;
   const int G = argc > 8 ? std::atoi(argv[8]) : 1;
   const bool SPLIT = argc > 9 && std::atoi(argv[9]) != 0;
-  const int d = 2, b = m + 1, sweeps = 3;
+  const int sweeps = argc > 10 ? std::atoi(argv[10]) : 3;
+  const int d = 2, b = m + 1;
   std::mt19937_64 g(seed);
   std::uniform_real_distribution<double> U(0, 1);
   std::normal_distribution<double> N01(0, 1);
@@ -346,7 +347,16 @@ int main(int argc, char** argv) {
   mixv(L.cell_pk); mixv(L.cell_src); mixv(L.gcell); mixv(L.gsrc); mixv(L.gptr); mixv(L.gslot); mixv(L.gslot_ptr);
   mixv(L.nb_ptr); mixv(L.nb); mixv(L.rmask); mixv(L.batch_split);
   for (const TileBatch& tb : L.batch) mix(&tb, sizeof tb);
+  // dynamic LDS of one 512-thread workgroup (exchange-wave tiles) at 1..4
+  // chains with r in LDS, and with r in global memory (RG tiles)
+  int lds[5], lds_rg[5];
+  for (int c = 1; c <= 4; ++c) {
+    lds[c] = tile_lds_bytes(L.max_rows, c, 512, K, L.max_batches, L.max_gslots);
+    lds_rg[c] = tile_lds_bytes(0, c, 512, K, L.max_batches, L.max_gslots);
+  }
   std::printf("ok K=%d T=%d G=%d max_rows=%d batches=%zu cells=%zu ghosts=%zu nb=%zu remote_puts=%lld maxrel=%.2e "
-              "layout=%016llx\n", K, L.T, G, L.max_rows, L.batch.size(), ncell, ng, L.nb.size(), remote_puts, maxrel, lh);
+              "layout=%016llx lds=%d,%d,%d,%d lds_rg=%d,%d,%d,%d cu_lds=%d\n", K, L.T, G, L.max_rows, L.batch.size(),
+              ncell, ng, L.nb.size(), remote_puts, maxrel, lh, lds[1], lds[2], lds[3], lds[4], lds_rg[1], lds_rg[2],
+              lds_rg[3], lds_rg[4], kTileCuLds);
   return 0;
 }

@@ -78,6 +78,17 @@ def main():
     b0, ls, lnv, seed, cb, ns = calls[0]
     ctx.sweep_chains(ns, b0, ls, lnv, seed, [x + 5 for x in cb])
     got.append(read(ctx))
+    # the R drop-in's order on the raw C ABI (rpkg/R/mcmc_nngp_update_Gaussian.R:
+    # sweep_chains, nngp_shard_sync, sum_squared_residuals_chains; no hidden
+    # sync in the readers): the SSR read after the explicit sync succeeds
+    # and equals the one-context SSR; without it the reader refuses
+    mask = (1 << C) - 1
+    ctx.sweep_chains(ns, b0, ls, lnv, seed, [x + 9 for x in cb])
+    ssr = np.zeros(C)
+    assert lib.nngp_sum_squared_residuals_chains(ctx._h, mask, np.asarray(b0, np.float64), ssr) != 0
+    assert lib.nngp_shard_sync(ctx._h) == 0
+    assert lib.nngp_sum_squared_residuals_chains(ctx._h, mask, np.asarray(b0, np.float64), ssr) == 0
+    got.append(read(ctx))
     dist.barrier()
     ctx.close()
     if rank == 0:
@@ -92,6 +103,11 @@ def main():
         ref.sweep_chains(ns, b0, ls, lnv, seed, [x + 5 for x in cb])
         for k, f in enumerate(read(ref)):
             assert np.array_equal(f, got[1][k]), (k, np.abs(f - got[1][k]).max())
+        ref.sweep_chains(ns, b0, ls, lnv, seed, [x + 9 for x in cb])
+        for k, f in enumerate(read(ref)):
+            assert np.array_equal(f, got[2][k]), (k, np.abs(f - got[2][k]).max())
+        ssr_ref = ref.sum_squared_residuals_chains(mask, b0)
+        assert np.array_equal(ssr_ref, ssr), (ssr_ref, ssr)
         ref.close()
         print(f"ok tile shard over {world} processes on one GPU == one context, bitwise "
               f"(n={n}, {C} chains, {TILES} tiles, {info['shard_exchange_slots']} exchanged slots)", flush=True)

@@ -20,7 +20,7 @@ def test_header_symbols_exported(P):
     lib = C.CDLL(str(_lib.LIB_PATH))
     for s in sorted(declared):
         assert hasattr(lib, s), s
-    assert P.lib.nngp_abi_version() == 9
+    assert P.lib.nngp_abi_version() == 10
 
 
 def test_library_has_gfx950_code_object():
@@ -213,6 +213,54 @@ def test_tile_shard_plan_emulation(tile_check_exe, n, m, tiles, G, chains, seed)
                           str(G)], capture_output=True, text=True)
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
     assert G == 1 or int(out.stdout.split("remote_puts=")[1].split()[0]) > 0 or n < 16
+
+
+def test_exchange_wave_barrier_count_matches_own_draw():
+    """The exchange wave of a tile (tiles.hip tile_phase_xw) holds no cells and
+    passes the own batches' workgroup barriers by count: kOwnDrawBarriers must
+    equal the __syncthreads() in tile_own_draw (a mismatch pairs the barriers
+    wrongly: an LDS race or a spin timeout), and tile_phase_xw must use it."""
+    import re
+
+    src = (next(ROOT.glob("*_amd")) / "csrc" / "tiles.hip").read_text()
+    k = int(re.search(r"constexpr int kOwnDrawBarriers = (\d+);", src).group(1))
+    body = src.split("void tile_own_draw(", 1)[1].split("\ntemplate", 1)[0]
+    assert body.count("__syncthreads()") == k, (body.count("__syncthreads()"), k)
+    xw = src.split("void tile_phase_xw(", 1)[1].split("\ntemplate", 1)[0]
+    assert "q < kOwnDrawBarriers; ++q) __syncthreads();" in xw
+
+
+def test_configs4_tile_shard_geometry(tile_check_exe):
+    """configs[4] (BASELINE.json: n = 1e7, m = 20, colour classes sharded over
+    8 GPUs) at its per-rank tile shape, scaled down: a G = 8 tile shard of
+    n = 1.25e6 with 32 tiles per rank has the tiles of the real layout (8 x 256
+    tiles of n/T = 4,883 locations, m = 20); at n = 1e7 itself the largest
+    tile holds 6,907 local rows (scripts/layout_stats.cpp 1e7 20 2048: 2m44s
+    on the host, too long for this suite) against 6,568 here.  The emulation
+    (one chain, one sweep) checks the remote-reader plan and the sweep at that
+    geometry.  The LDS a 512-thread workgroup needs with r in LDS: 3 chains
+    (the bench's chain count) exceed a CU's 160 KiB, 2 chains fit -- so
+    configs[4] at 3 chains runs the tile shard with r in global memory (RG
+    tiles, whose LDS is far below the CU's) and a 2-chain context the LDS
+    tiles (DESIGN.md §6 "configs[4] on eight GPUs")."""
+    import subprocess
+
+    out = subprocess.run([str(tile_check_exe), "1250000", "20", "256", "1", "11", "448", "8", "8", "0", "1"],
+                         capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
+    kv = dict(x.split("=", 1) for x in out.stdout.split()[1:])
+    assert kv["G"] == "8" and kv["T"] == "256" and int(kv["remote_puts"]) > 0
+    lds = [0] + [int(v) for v in kv["lds"].split(",")]
+    lds_rg = [0] + [int(v) for v in kv["lds_rg"].split(",")]
+    cu = int(kv["cu_lds"])
+    assert cu == 160 * 1024
+    rows = int(kv["max_rows"])
+    assert 6000 < rows <= 6907, rows
+    assert lds[3] > cu, (lds, cu)      # 3 chains: r alone is rows x 24 B
+    assert lds[2] <= cu, (lds, cu)     # 2 chains fit
+    assert lds_rg[3] <= cu // 4, lds_rg
+    # the real layout's largest tile only widens the gap at 3 chains
+    assert 6907 * 3 * 8 > cu
 
 
 @pytest.mark.parametrize("n,m,G,sweeps,seed", [(3000, 10, 2, 2, 1), (5000, 15, 3, 2, 2), (2000, 5, 8, 2, 3),
