@@ -597,14 +597,19 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       const char* txe = std::getenv("NNGP_TILE_XW");
       const int xwm = txe ? std::atoi(txe) : 1;
       const bool xw = !csplit && !split && !rg_forced && NT == 512 && xwm == 1;
-      const int NTL = xw ? NT - 64 : NT;  // the layout's cell threads
+      // wave-local batches (NNGP_TILE_WL=1, exchange-wave tiles): one wave per
+      // batch, the layout cut for 64-lane batches in rounds of the NT/64 - 1
+      // cell waves (tiles.hip tile_phase_wl)
+      const char* twl = std::getenv("NNGP_TILE_WL");
+      const bool wl = xw && twl && std::string(twl) == "1";
+      const int NTL = wl ? 64 : (xw ? NT - 64 : NT);  // the layout's cell threads of a batch
       if (const char* bc = std::getenv("NNGP_TILE_BATCH_CELLS"))
         rmax_l = std::max(1, std::min(rmax_l, std::atoi(bc) / NTL));
       bool ok = cus > 0 && T <= n && !hopeless &&
                 build_tile_layout(nn.data(), n, b, coloring, locs, d, T, NTL, rmax_l, c->tl, terr, G,
-                                  split);
+                                  split, wl ? NT / 64 - 1 : 0);
       c->tl.NTK = NT;
-      c->txw = xw ? xwm : 0;
+      c->txw = xw ? (wl ? 2 : 1) : 0;
       if (const char* pf = std::getenv("NNGP_TILE_PF")) c->tpf = std::atoi(pf) & 7;
       if (ok && csplit) {
         // n_chains workgroups of one chain per CU
@@ -650,7 +655,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
         Dq.K = c->tl.K;
         Dq.rg = c->rglobal ? reinterpret_cast<double*>(16) : nullptr;
         Dq.batch_split = c->tl.split ? reinterpret_cast<const int*>(16) : nullptr;
-        Dq.xw = xw ? xwm : 0;
+        Dq.xw = c->txw;
         if (const char* pr = std::getenv("NNGP_PROBE"))
           if ((std::atoi(pr) == 9 || std::atoi(pr) == 2) && (n_chains == 1 || n_chains == 3)) {
             Dq.dbg = reinterpret_cast<unsigned long long*>(16);

@@ -543,10 +543,14 @@ bool build_sweep_layout(const int* nn, int n, int b, const int* colors, const do
 
 // ---------------------------------------------------------------- tile layout
 bool build_tile_layout(const int* nn, int n, int b, const int* colors, const double* locs, int d, int T,
-                       int NT, int RMAX, TileLayout& L, std::string& err, int G, bool split) {
+                       int NT, int RMAX, TileLayout& L, std::string& err, int G, bool split, int waves) {
   L = TileLayout();
-  L.n = n; L.b = b; L.NT = NT; L.RMAX = RMAX;
+  L.n = n; L.b = b; L.NT = NT; L.RMAX = RMAX; L.W = waves;
   if (NT < 64 || NT > 1024 || RMAX < 1 || (long long)NT * RMAX > (1 << 20)) { err = "tile layout: bad NT/RMAX"; return false; }
+  if (waves < 0 || (waves > 0 && (NT != 64 || split || waves * kWaveSlotsMax > kTileSlotsMax))) {
+    err = "tile layout: wave-local batches need NT = 64, no split, waves x kWaveSlotsMax <= kTileSlotsMax";
+    return false;
+  }
   if (T < 1) T = 1;
   if (T > n) T = n;
   if (G < 1 || G > kMaxTileRanks || T % G != 0) { err = "tile layout: need 1 <= G <= 16 ranks dividing the tile count"; return false; }
@@ -714,14 +718,35 @@ bool build_tile_layout(const int* nn, int n, int b, const int* colors, const dou
         for (int run = 0; run < (split ? 2 : 1); ++run) {
           const int xe = split && run == 0 ? tc_split[pc] : xe_all;
           if (split && run == 1) o.bsplit[c] = (int)o.batch.size();
+          // wave-local: the run's batches in rounds of `waves`, cut where the
+          // prefix of the run's cells crosses g/nb of its total (balanced
+          // waves), capped at kWaveSlotsMax slots and NT*RMAX cells
+          long long run_cells = 0;
+          int nbw = 0, bw = 0;
+          long long acc_cells = 0;
+          if (waves > 0 && x < xe) {
+            for (int y = x; y < xe; ++y) run_cells += cptr[L.compact_loc[y] + 1] - cptr[L.compact_loc[y]];
+            const long long by_cells = (run_cells + (long long)NT * RMAX * 7 / 8 - 1) / ((long long)NT * RMAX * 7 / 8);
+            const long long by_slots = (xe - x + kWaveSlotsMax - 1) / kWaveSlotsMax;
+            nbw = (int)std::max<long long>(1, std::max(by_cells, by_slots));
+            nbw = (nbw + waves - 1) / waves * waves;
+            nbw = std::min(nbw, xe - x);
+          }
           while (x < xe) {
             int cells = 0, ns = 0;
-            while (x + ns < xe && ns < std::min(NT, kTileSlotsMax)) {
+            const int smax = waves > 0 ? kWaveSlotsMax : std::min(NT, kTileSlotsMax);
+            while (x + ns < xe && ns < smax) {
               const int len = (int)(cptr[L.compact_loc[x + ns] + 1] - cptr[L.compact_loc[x + ns]]);
               if (cells + len > NT * RMAX) break;
+              // balanced cut: stop once this batch reaches its share of the run
+              if (waves > 0 && ns > 0 && bw + 1 < nbw &&
+                  2 * (acc_cells + cells) + len > 2 * run_cells * (bw + 1) / nbw)
+                break;
               cells += len;
               ++ns;
             }
+            acc_cells += cells;
+            ++bw;
             const int R = std::max(1, (cells + NT - 1) / NT);
             TileBatch tb{(int)o.cell_pk.size(), R, ns, x, (cells + R - 1) / R};
             o.cell_pk.resize(o.cell_pk.size() + (size_t)R * NT, kTilePadRow);

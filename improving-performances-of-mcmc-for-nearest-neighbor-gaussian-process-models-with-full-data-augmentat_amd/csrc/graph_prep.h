@@ -151,7 +151,14 @@ struct TileLayout {
   int G = 1;
   std::vector<int> rank_slot0;       // G + 1
   std::vector<uint32_t> rmask;       // n (G > 1): bit h = a tile of rank h != the owner's reads the slot's dw
+  // wave-local layouts (W = waves > 0; NT = 64): every batch is one wave's
+  // (<= kWaveSlotsMax slots, 64 lanes x R cells), and the batches of a (tile,
+  // colour) come in rounds of W balanced by cells -- wave w of the tile runs
+  // batches first + w, first + w + W, ... with no workgroup barrier inside a
+  // colour (the batches of one colour touch disjoint rows of B)
+  int W = 0;
 };
+constexpr int kWaveSlotsMax = 36;  // slots of a wave-local batch (W x 36 <= kTileSlotsMax for W <= 7)
 
 // Fails (returns false, err set) when the layout does not fit the packed
 // formats; the caller checks the LDS budget (max_rows).
@@ -160,7 +167,7 @@ struct TileLayout {
 constexpr int kMaxTileRanks = 16;
 bool build_tile_layout(const int* nn_rowmajor, int n, int b, const int* colors, const double* locs_colmajor,
                        int d, int T, int NT, int RMAX, TileLayout& L, std::string& err, int G = 1,
-                       bool split = false);
+                       bool split = false, int waves = 0);
 
 // Colour-sharded sweep over G ranks on top of a
 // SweepLayout (every rank builds the same layout from the same inputs):

@@ -144,7 +144,10 @@ constexpr int kGranAux = 16, kGranAuxSys = 17;
 // after tile_prep_items (in place: two batches stay in registers).
 template <int C, int NT, int RMAX>
 struct TileBatchRegs {
-  static constexpr int IMAX = (kTSlots * C + NT - 1) / NT;
+  // slots of a batch: NT == 64 is a wave-local batch (TileLayout::W), at most
+  // kWaveSlotsMax slots; otherwise a workgroup's, at most kTSlots
+  static constexpr int SMAX = NT == 64 ? kWaveSlotsMax : kTSlots;
+  static constexpr int IMAX = (SMAX * C + NT - 1) / NT;
   int R, ns, x0;
   uint32_t rm[IMAX];          // tile shard: remote readers of the slot
   uint32_t pk[RMAX];
@@ -485,10 +488,11 @@ __device__ __forceinline__ void tile_own_draw(const TileDev& D, const TileLaunch
 // one LDS round trip per group instead of one per cell (the compiler cannot
 // see the distinctness and would order every read after the previous write)
 template <int C, int NT, int RMAX, int PROBE>
-__device__ __forceinline__ void tile_own_scatter(TileState& S, const TileBatchRegs<C, NT, RMAX>& b, int R) {
+__device__ __forceinline__ void tile_own_scatter(TileState& S, const TileBatchRegs<C, NT, RMAX>& b, int R,
+                                                 const double* acc_base = nullptr) {
   constexpr int GRP = RMAX < 4 ? RMAX : 4;  // rows per group (registers: 2 x GRP x C doubles)
   double* r_s = S.r_s;
-  const double* acc_s = S.acc_s;
+  const double* acc_s = acc_base ? acc_base : S.acc_s;
 #pragma unroll
   for (int j0 = 0; j0 < RMAX; j0 += GRP) {
     if (j0 >= R) break;
@@ -789,6 +793,159 @@ __device__ __forceinline__ void tile_phase_ib(const TileDev& D, const TileLaunch
   TLSTAMP(S, 3);
 }
 
+// ---- wave-local batches (XW == 2; TileLayout::W): every own batch is ONE
+// wave's -- whole slots, 64 lanes x R cells, at most kWaveSlotsMax slots --
+// and the W cell waves run the batches of a colour side by side, wave w the
+// batches first + w, first + w + W, ...  A wave's slots start at its lane 0
+// and end inside the wave, so the slot totals need no cross-wave carry and
+// the draw and the scatter read only what this wave wrote into its own part
+// of acc_s: no workgroup barrier inside a colour (the batches of one colour
+// touch disjoint rows of B: a row has at most one member per colour), two per
+// colour phase (the hand-off, the ghost adds).  LDS accesses of one wave
+// complete in issue order; wave_lds_order keeps the compiler from moving them.
+__device__ __forceinline__ void wave_lds_order() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+template <int C, int RMAX, int PROBE, int SH>
+__device__ __forceinline__ void tile_own_wl(const TileDev& D, const TileLaunch& a, const TileShard& sh, TileState& S,
+                                            TileBatchRegs<C, 64, RMAX>& b, unsigned epoch, double* acc_w) {
+  constexpr int IMAX = TileBatchRegs<C, 64, RMAX>::IMAX;
+  const int lane = S.lane;
+  const double* __restrict__ r_s = S.r_s;
+  double* __restrict__ acc_s = acc_w;
+  const int R = b.R, nit = b.ns * C;
+  tile_cells_landed(b);
+  double run[C], cont[C];
+  int cont_q = -1;
+  bool seen_start = false;
+#pragma unroll
+  for (int ch = 0; ch < C; ++ch) { run[ch] = 0.0; cont[ch] = 0.0; }
+#pragma unroll
+  for (int j = 0; j < RMAX; ++j) {
+    if (j < R) {
+      const uint32_t lr = tile_lr(b.pk[j]);
+      const bool st = (b.pk[j] & kTStart) != 0;
+#pragma unroll
+      for (int ch = 0; ch < C; ++ch) {
+        const double p = (lr != kTPad) ? b.v[j][ch] * r_s[lr * C + ch] : 0.0;
+        run[ch] = st ? p : run[ch] + p;
+      }
+      seen_start |= st;
+      if (b.pk[j] & kTEnd) {
+        const int q = (int)((b.pk[j] >> kTileQShift) & kTileQMask);
+        if (seen_start) {
+#pragma unroll
+          for (int ch = 0; ch < C; ++ch) acc_s[q * C + ch] = run[ch];
+        } else {
+          cont_q = q;
+#pragma unroll
+          for (int ch = 0; ch < C; ++ch) cont[ch] = run[ch];
+        }
+      }
+    }
+  }
+  // segmented inclusive scan of the lane tails inside the wave (as
+  // tile_own_draw's); lane 0 holds the first cell of the wave's first slot,
+  // so nothing is carried in from another wave
+  double v[C];
+  int f = seen_start ? 1 : 0;
+#pragma unroll
+  for (int ch = 0; ch < C; ++ch) v[ch] = run[ch];
+  seg_scan_step<0x111, 0xF, true, C>(v, f);  // row_shr:1
+  seg_scan_step<0x112, 0xF, true, C>(v, f);  // row_shr:2
+  seg_scan_step<0x114, 0xF, true, C>(v, f);  // row_shr:4
+  seg_scan_step<0x118, 0xF, true, C>(v, f);  // row_shr:8
+  seg_scan_step<0x142, 0xA, false, C>(v, f); // row_bcast:15 -> rows 1, 3
+  seg_scan_step<0x143, 0xC, false, C>(v, f); // row_bcast:31 -> rows 2, 3
+#pragma unroll
+  for (int ch = 0; ch < C; ++ch) {
+    const double up = dpp_f64<0x138, 0xF, true>(v[ch]);  // wave_shr:1
+    const double cp = lane ? up : 0.0;
+    if (cont_q >= 0) acc_s[cont_q * C + ch] = cont[ch] + cp;
+  }
+  wave_lds_order();
+#pragma unroll
+  for (int k = 0; k < IMAX; ++k) {
+    const int u = lane + k * 64;
+    if (u < nit) {
+      const int ch = u % C;
+      double dw = 0.0;
+      const size_t xu = tile_xu<C, C>(b.x0, u);
+      if ((a.chain_mask >> ch) & 1) {
+        const double wn = (b.a0[k] - S.sc_s[2 * ch] * acc_s[u]) * b.a1[k] + b.zs[k];
+        dw = wn - b.w[k];
+        D.w_slot[xu] = wn;
+      }
+      acc_s[u] = dw;
+      if (b.flag[k] & kTExported) {
+        const unsigned long long uu = __builtin_bit_cast(unsigned long long, dw);
+        u32x4_t g;
+        g.x = (unsigned)uu; g.y = (unsigned)(uu >> 32); g.z = epoch; g.w = S.call ^ g.x ^ g.y;
+        __builtin_amdgcn_raw_buffer_store_b128(g, S.gran, (int)(xu * 16), 0, SH ? kGranAuxSys : kGranAux);
+        if (SH) {
+#pragma unroll
+          for (int h = 0; h < kTileRanksMax; ++h)
+            if (h < S.G && ((b.rm[k] >> h) & 1u))
+              __builtin_amdgcn_raw_buffer_store_b128(
+                  g, __builtin_amdgcn_make_buffer_rsrc(sh.gx[h], 0, 0x7FFFFFFF, 0x00020000), (int)(xu * 16), 0,
+                  kGranAuxSys);
+        }
+      }
+    }
+  }
+  wave_lds_order();
+  TLSTAMP(S, 1);
+}
+
+// the cell waves' colour phase on wave-local batches
+template <int C, int NT, int RMAX, int GMAX, int PROBE, int SH>
+__device__ __forceinline__ void tile_phase_wl(const TileDev& D, const TileLaunch& a, const TileShard& sh,
+                                              TileState& S, int ph, TileBatchRegs<C, 64, RMAX>& cur,
+                                              TileGhostRegs<C, GMAX>& gr) {
+  constexpr int W = NT / 64 - 1;  // cell waves
+  const int K = S.K, t = S.t, lane = S.lane;
+  const int s = ph / K, c = ph - s * K;
+  const unsigned epoch = (unsigned)ph + 1;
+  S.ph = ph;
+  TLSTAMP(S, 0);
+  const int phn = ph + 1;
+  const int cn = phn % K, sn = phn / K;
+  const bool has_next = phn < S.nph;
+  const int bnext = S.bptr_s[cn] + S.wv;
+  const bool more = has_next && bnext < S.bptr_s[cn + 1];
+  const int bfirst = S.bptr_s[c] + S.wv, bend = S.bptr_s[c + 1];
+  const int g0 = S.gptr_s[c], g1 = S.gptr_s[c + 1];
+  double* acc_w = S.acc_s + S.wv * (kWaveSlotsMax * C);
+  for (int bi = bfirst; bi < bend; bi += W) {
+    if (bi != bfirst) {  // a later round of this colour (large colours only): independent rows, no barrier
+      tile_load_batch<C, 64, RMAX, SH>(D, S.batch_s[bi], cur, lane);
+      tile_prep_items<C, 64, RMAX>(D, a, S.sc_s, S.seed_s, s, cur, lane);
+    }
+    tile_own_wl<C, RMAX, PROBE, SH>(D, a, sh, S, cur, epoch, acc_w);
+    const int R = cur.R;
+    if (bi + W >= bend) {  // this wave's last batch of the colour: its records are dead
+      if (more) tile_load_items<C, 64, RMAX, SH>(D, S.batch_s[bnext], cur, lane);
+      if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
+    }
+    tile_own_scatter<C, 64, RMAX, PROBE>(S, cur, R, acc_w);
+  }
+  if (bfirst >= bend) {  // no batch of this colour for this wave
+    if (more) tile_load_items<C, 64, RMAX, SH>(D, S.batch_s[bnext], cur, lane);
+    if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
+  }
+  TLSTAMP(S, 6);
+  if (more) tile_prep_items<C, 64, RMAX>(D, a, S.sc_s, S.seed_s, sn, cur, lane);
+  if (more) tile_load_cells<C, 64, RMAX>(D, S.batch_s[bnext], cur, lane);
+  TLSTAMP(S, 4);
+  __syncthreads();  // the exchange wave has every dw of the colour in gdw_s
+  TLSTAMP(S, 2);
+  for (int gb = g0; gb < g1; gb += NT * GMAX) {
+    if (gb != g0) tile_load_ghosts<C, NT, GMAX>(D, gb, g1, gr, t);
+    tile_ghost_adds<C, GMAX>(S, gr);
+  }
+  __syncthreads();
+  TLSTAMP(S, 3);
+}
+
 // ---- exchange-wave tiles (XW; TileDev::xw).  vmcnt counts a wave's
 // vector-memory operations in issue order, loads and stores together, so in
 // a wave that streams the next batch's cells every poll of a granule -- and
@@ -867,7 +1024,7 @@ __device__ __forceinline__ void tile_xw_prefetch(const TileDev& D, const TileSta
 // data: loaded at the phase start, long in registers when the hand-off
 // ends), the own batches' barriers, then the hand-off polls -> gdw_s, and its
 // share of the ghost adds
-template <int C, int NT, int GMAX, int PROBE, int SH>
+template <int C, int NT, int GMAX, int PROBE, int SH, int WL = 0>
 __device__ __forceinline__ void tile_phase_xw(const TileDev& D, TileState& S, int ph, TileGhostRegs<C, GMAX>& gr) {
   constexpr int PB = 4;  // granule polls in flight per lane
   const int K = S.K, t = S.t, lane = S.lane;
@@ -888,8 +1045,8 @@ __device__ __forceinline__ void tile_phase_xw(const TileDev& D, TileState& S, in
   uint32_t pfv[kPfLoads];
   if (D.pf) tile_xw_prefetch<C, NT - 64>(D, S, ph, lane, pfv);
   // the own batches' barriers (tile_own_draw: kOwnDrawBarriers each, + 1
-  // before a later batch, as tile_phase_cells)
-  for (int bi = bfirst; bi < bend; ++bi) {
+  // before a later batch, as tile_phase_cells; wave-local batches have none)
+  for (int bi = bfirst; bi < (WL ? bfirst : bend); ++bi) {
     if (bi != bfirst) __syncthreads();
 #pragma unroll
     for (int q = 0; q < kOwnDrawBarriers; ++q) __syncthreads();
@@ -1111,7 +1268,16 @@ __device__ __forceinline__ void sweep_tiles_body(const TileDev& D0, TileLaunch a
     if (S.wv == NW - 1) {  // the exchange wave
       TileGhostRegs<C, GMAX> GX;
       __syncthreads();
-      for (int ph = 0; ph < S.nph; ++ph) tile_phase_xw<C, NT, GMAX, PROBE, SH>(D, S, ph, GX);
+      for (int ph = 0; ph < S.nph; ++ph) tile_phase_xw<C, NT, GMAX, PROBE, SH, XW == 2>(D, S, ph, GX);
+    } else if constexpr (XW == 2) {  // wave-local batches: wave w runs batches first + w, + W, ...
+      TileBatchRegs<C, 64, RMAX> A;
+      TileGhostRegs<C, GMAX> GA;
+      if (S.nph > 0 && S.bptr_s[0] + S.wv < S.bptr_s[1]) {
+        tile_load_batch<C, 64, RMAX, SH>(D, S.batch_s[S.bptr_s[0] + S.wv], A, S.lane);
+        tile_prep_items<C, 64, RMAX>(D, a, S.sc_s, S.seed_s, 0, A, S.lane);
+      }
+      __syncthreads();
+      for (int ph = 0; ph < S.nph; ++ph) tile_phase_wl<C, NT, RMAX, GMAX, PROBE, SH>(D, a, sh, S, ph, A, GA);
     } else {
       BR A, B;
       TileGhostRegs<C, GMAX> GA;
@@ -1208,7 +1374,8 @@ static hipError_t launch_tiles_c(hipStream_t st, const TileDev& D, const TileLau
   if (D.batch_split && !IB) return hipErrorInvalidValue;  // split layout: double-buffered path not for it
   auto k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE, SH, RG, IB, 0>;
   if constexpr (NT == 512 && !RG && !IB) {
-    if (D.xw) k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE, SH, RG, IB, 1>;
+    if (D.xw == 1) k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE, SH, RG, IB, 1>;
+    if (D.xw == 2) k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE, SH, RG, IB, 2>;
   }
   if (D.xw && (NT != 512 || RG || IB)) return hipErrorInvalidValue;
   lds = lds < kTSpreadLds ? kTSpreadLds : lds;

@@ -12,6 +12,7 @@ using namespace nngp;
 int main(int argc, char** argv) {
   int n = argc > 1 ? atoi(argv[1]) : 1000000, m = argc > 2 ? atoi(argv[2]) : 15;
   int T = argc > 3 ? atoi(argv[3]) : 256, NT = argc > 4 ? atoi(argv[4]) : 448, RMAX = argc > 5 ? atoi(argv[5]) : 8;
+  const int WAVES = argc > 6 ? atoi(argv[6]) : 0;  // wave-local batches (NT = 64)
   std::mt19937_64 g(1000); std::uniform_real_distribution<double> U(0, 1);
   std::vector<double> xy(2 * (size_t)n);
   for (auto& v : xy) v = U(g);
@@ -24,8 +25,9 @@ int main(int argc, char** argv) {
   std::vector<int> csz(K); for (int c : col) csz[c - 1]++;
   for (int c = 0; c < K; ++c) printf("%d ", csz[c]); printf("\n");
   TileLayout L; std::string err;
-  if (!build_tile_layout(nn.data(), n, m + 1, col.data(), lo.data(), 2, T, NT, RMAX, L, err)) { printf("err %s\n", err.c_str()); return 1; }
-  printf("max_rows %d max_batches %d max_gslots %d\n", L.max_rows, L.max_batches, L.max_gslots);
+  if (!build_tile_layout(nn.data(), n, m + 1, col.data(), lo.data(), 2, T, NT, RMAX, L, err, 1, false, WAVES)) { printf("err %s\n", err.c_str()); return 1; }
+  printf("max_rows %d max_batches %d max_gslots %d cells %zu (nnz %lld, x%.3f) batches %zu\n", L.max_rows, L.max_batches,
+         L.max_gslots, L.cell_pk.size(), L.nnz, (double)L.cell_pk.size() / L.nnz, L.batch.size());
   // per (tile, colour): cells, R, ghost cells, foreign slots
   long sumR = 0, sumRmaxNb = 0; 
   std::vector<int> Rtc((size_t)T * K, 0), ctc((size_t)T*K,0);

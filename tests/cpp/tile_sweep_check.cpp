@@ -15,7 +15,10 @@
 // interior batches of colour c, then the ghost cells of colour c-1 (their
 // hand-off), then the boundary batches of c -- an interior slot must not read
 // a row still missing its colour-(c-1) ghost update.
-// Usage: tile_sweep_check <n> <m> <tiles> <chains> <seed> [NT RMAX G SPLIT]  (prints "ok <stats>")
+// With WAVES > 0 (NT = 64): wave-local batches (one wave's each, rounds of
+// WAVES per colour, tiles.hip tile_phase_wl); the batches of a colour touch
+// disjoint rows, so emulating them one after another is the kernel's result.
+// Usage: tile_sweep_check <n> <m> <tiles> <chains> <seed> [NT RMAX G SPLIT SWEEPS WAVES]  (prints "ok <stats>")
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -48,6 +51,7 @@ int main(int argc, char** argv) {
   const int G = argc > 8 ? std::atoi(argv[8]) : 1;
   const bool SPLIT = argc > 9 && std::atoi(argv[9]) != 0;
   const int sweeps = argc > 10 ? std::atoi(argv[10]) : 3;
+  const int WAVES = argc > 11 ? std::atoi(argv[11]) : 0;  // wave-local batches (NT = 64) in rounds of WAVES
   const int d = 2, b = m + 1;
   std::mt19937_64 g(seed);
   std::uniform_real_distribution<double> U(0, 1);
@@ -63,7 +67,7 @@ int main(int argc, char** argv) {
   const int K = greedy_coloring(nn.data(), n, b, col);
   TileLayout L;
   std::string err;
-  if (!build_tile_layout(nn.data(), n, b, col.data(), locs.data(), d, T, NT, RMAX, L, err, G, SPLIT)) {
+  if (!build_tile_layout(nn.data(), n, b, col.data(), locs.data(), d, T, NT, RMAX, L, err, G, SPLIT, WAVES)) {
     std::printf("FAIL build: %s\n", err.c_str());
     return 1;
   }
@@ -213,6 +217,7 @@ int main(int argc, char** argv) {
         for (int bi = bi_lo; bi < bi_hi; ++bi) {
           const TileBatch B = L.batch[bi];
           REQUIRE(B.nslots <= NT && B.R <= RMAX);
+          REQUIRE(WAVES == 0 || B.nslots <= kWaveSlotsMax);
           // threads past nthr hold padding only (the kernel skips their loads)
           REQUIRE(B.nthr >= 1 && B.nthr <= NT);
           for (int j = 0; j < B.R; ++j)

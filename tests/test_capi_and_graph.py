@@ -215,6 +215,24 @@ def test_tile_shard_plan_emulation(tile_check_exe, n, m, tiles, G, chains, seed)
     assert G == 1 or int(out.stdout.split("remote_puts=")[1].split()[0]) > 0 or n < 16
 
 
+@pytest.mark.parametrize("n,m,tiles,chains,seed,rmax,G,waves", [
+    (3000, 10, 16, 3, 1, 8, 1, 7), (60000, 15, 64, 3, 5, 8, 1, 7), (20000, 10, 40, 1, 2, 8, 4, 7),
+    (5000, 15, 24, 2, 6, 4, 8, 3), (400, 5, 16, 4, 7, 1, 2, 7)])
+def test_tile_sweep_emulation_wave_local(tile_check_exe, n, m, tiles, chains, seed, rmax, G, waves):
+    """Wave-local layouts (NNGP_TILE_WL=1, tiles.hip tile_phase_wl): 64-lane
+    batches of at most kWaveSlotsMax slots in rounds of `waves` balanced by
+    cells.  The emulation applies the batches of a colour one after another
+    -- the kernel's waves run them side by side, which gives the same result
+    because the batches of one colour touch disjoint rows -- and checks the
+    field against the serial sweep (1e-11) and the layout, incl. the tile
+    shard's remote puts (G > 1)."""
+    import subprocess
+
+    out = subprocess.run([str(tile_check_exe), str(n), str(m), str(tiles), str(chains), str(seed), "64", str(rmax),
+                          str(G), "0", "2", str(waves)], capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
+
+
 def test_exchange_wave_barrier_count_matches_own_draw():
     """The exchange wave of a tile (tiles.hip tile_phase_xw) holds no cells and
     passes the own batches' workgroup barriers by count: kOwnDrawBarriers must
