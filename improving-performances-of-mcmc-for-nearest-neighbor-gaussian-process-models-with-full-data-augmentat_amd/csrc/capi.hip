@@ -59,6 +59,11 @@ struct ChainState {
   uint64_t warm_fgen = 0, warm_lgen = 0;
   double warm_beta0 = 0.0;
   int rs_next = 0;
+  // the sweep's copy of the current factor (tile cells / colour entries and
+  // precision_diag) is behind it: refreshed before the next reader (a sweep,
+  // nngp_get_precision_diag), so a chain that accepts two proposals in one
+  // MCMC iteration refreshes once
+  bool vals_stale = false;
 };
 
 struct nngp_ctx {
@@ -310,8 +315,18 @@ TileDev tile_dev(nngp_ctx* c) {
   return D;
 }
 
-// sweep values of B + precision_diag of chain k from its current factor
+// chain k's current factor changed: the pointer table of captured graphs
+// now (stream order, no host buffer), the sweep values at the next reader
+// (flush_sweep_values)
 int refresh_sweep_values(nngp_ctx* c, int k) {
+  c->linv_cur_h[k] = c->ch[k].linv_d[0];
+  HIPCHK(c, launch_set_ptr(c->st, c->linv_cur_d, k, c->ch[k].linv_d[0]));
+  c->ch[k].vals_stale = true;
+  return NNGP_OK;
+}
+
+// sweep values of B + precision_diag of chain k from its current factor
+int flush_one(nngp_ctx* c, int k) {
   if (c->engine == 1)
     HIPCHK(c, launch_tile_refresh(c->st, tile_dev(c), c->rorder_d, c->rorder_len, c->tl.NT, c->cell_src_d,
                                   c->gsrc_d, c->ch[k].linv_d[0], k));
@@ -321,9 +336,17 @@ int refresh_sweep_values(nngp_ctx* c, int k) {
     const int ng = (int)c->sp.grow.size();
     HIPCHK(c, launch_permute_gather(c->st, ng, c->sg_src_d, c->ch[k].linv_d[0], c->sg_val_d + (size_t)k * ng));
   }
-  // the table entry travels as a kernel argument: no host sync needed
-  c->linv_cur_h[k] = c->ch[k].linv_d[0];
-  HIPCHK(c, launch_set_ptr(c->st, c->linv_cur_d, k, c->ch[k].linv_d[0]));
+  c->ch[k].vals_stale = false;
+  return NNGP_OK;
+}
+
+// the sweep values of the chains in mask, where behind their current factor
+int flush_sweep_values(nngp_ctx* c, int mask) {
+  for (int k = 0; k < c->C; ++k)
+    if (((mask >> k) & 1) && c->ch[k].vals_stale) {
+      int rc = flush_one(c, k);
+      if (rc) return rc;
+    }
   return NNGP_OK;
 }
 
@@ -1256,6 +1279,7 @@ int nngp_get_precision_diag(nngp_ctx* c, double* D) {
   if (!c->ch[c->cur].have_factor[0]) return fail_msg(c, NNGP_ERR_STATE, "precision_diag: no factor");
   int rc;
   if ((rc = set_device(c))) return rc;
+  if ((rc = flush_sweep_values(c, 1 << c->cur))) return rc;
   std::vector<double2> dr((size_t)c->n * c->C);
   HIPCHK(c, hipMemcpyAsync(dr.data(), c->dr_d, dr.size() * sizeof(double2), hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
@@ -1609,6 +1633,7 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
   const bool warm = !z && warm_call(c, mask, b0v);
   fields_written(c, mask);
   if ((rc = sweep_prepare(c, k, beta0, log_scale, lnv, seed, counter_base))) return rc;
+  if ((rc = flush_sweep_values(c, mask))) return rc;
   if ((rc = upload_scalars(c))) return rc;
   if (sharded_call(c)) {
     if (z) return fail_msg(c, NNGP_ERR_ARG, "sweep: injected normals are not supported on shard contexts");
@@ -1656,6 +1681,7 @@ int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const doub
   fields_written(c, all);
   for (int k = 0; k < c->C; ++k)
     if ((rc = sweep_prepare(c, k, beta0[k], log_scale[k], lnv[k], seed[k], counter_base[k]))) return rc;
+  if ((rc = flush_sweep_values(c, all))) return rc;
   if ((rc = upload_scalars(c))) return rc;
   if (sharded_call(c)) return shard_call(c, n_sweeps, all);
   std::unique_lock<std::mutex> tlk;
@@ -2048,6 +2074,7 @@ static int tile_group_call(nngp_ctx** ctxs, int G, int n_sweeps, const double* b
     GCHK(c, hipEventCreateWithFlags(&ev[G + g], hipEventDisableTiming));
     for (int k = 0; k < c->C; ++k)
       if ((rc = sweep_prepare(c, k, beta0[k], log_scale[k], lnv[k], seed[k], counter_base[k]))) { cleanup(); return rc; }
+    if ((rc = flush_sweep_values(c, mask))) { cleanup(); return rc; }
     if ((rc = upload_scalars(c))) { cleanup(); return rc; }
     if ((rc = enqueue_sweep_body(c, n_sweeps, mask, nullptr, kPrologue))) { cleanup(); return rc; }
     GCHK(c, launch_tile_call_bump(c->st, c->ctl_d));  // every rank's call id and timeout word
@@ -2137,6 +2164,7 @@ int nngp_sweep_chains_group(nngp_ctx** ctxs, int G, int n_sweeps, const double* 
     if ((rc = set_device(c))) return rc;
     for (int k = 0; k < c->C; ++k)
       if ((rc = sweep_prepare(c, k, beta0[k], log_scale[k], lnv[k], seed[k], counter_base[k]))) return rc;
+    if ((rc = flush_sweep_values(c, mask))) return rc;
     if ((rc = upload_scalars(c))) return rc;
     if ((rc = enqueue_sweep_body(c, n_sweeps, mask, nullptr, kPrologue))) return rc;
   }
@@ -2212,6 +2240,7 @@ int nngp_sweep_timed(nngp_ctx* c, int n_sweeps, const double* beta0, const doubl
   fields_written(c, (1 << c->C) - 1);
   for (int k = 0; k < c->C; ++k)
     if ((rc = sweep_prepare(c, k, beta0[k], log_scale[k], lnv[k], seed[k], counter_base[k]))) return rc;
+  if ((rc = flush_sweep_values(c, (1 << c->C) - 1))) return rc;
   if ((rc = upload_scalars(c))) return rc;
   const int mask = (1 << c->C) - 1;
   std::unique_lock<std::mutex> tlk;

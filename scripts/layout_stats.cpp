@@ -54,4 +54,19 @@ int main(int argc, char** argv) {
   printf("sum over colours: R mean %.1f nbmax %.1f max %.1f ghost %.0f fslots %.0f\n", tot_mean, tot_nbmax, tot_max, gh, fs);
   long exported = 0; for (int x = 0; x < n; ++x) if (L.slot_f0[x] & kSlotExported) exported++;
   printf("exported slots %ld (%.1f%%)\n", exported, 100.0*exported/n);
+  // HBM bytes per sweep by stream at C chains (what the kernel loads and
+  // stores; DESIGN.md §3 "traffic budget"), against SURVEY §8d's algorithmic
+  // C*(8*nnz + 40*n) + 4*nnz
+  const int C = argc > 7 ? atoi(argv[7]) : 3;
+  long long live = 0;  // cells the kernel loads: rows < R of threads < nthr
+  for (const TileBatch& tb : L.batch) live += (long long)tb.R * tb.nthr;
+  const double MB = 1e6;
+  const double cells = live * (4.0 + 8.0 * C), ghosts = (double)L.gsrc.size() * (8.0 + 8.0 * C);
+  const double recs = (double)n * (8 + 4 + C * (16 + 8 + 8));  // sinfo, loc, dr, w read, w write
+  long long fsl = (long long)L.gslot.size();
+  const double gran = (double)exported * C * 16 + (double)fsl * C * 16 + (double)fsl * 4;  // stores, polls, indices
+  const double alg = C * (8.0 * L.nnz + 40.0 * n) + 4.0 * L.nnz;
+  printf("per sweep at C=%d (MB): cells %.1f (padding %.1f) ghosts %.1f records %.1f granules %.1f | total %.1f "
+         "algorithmic %.1f ratio %.3f\n", C, cells / MB, (live - L.nnz) * (4.0 + 8.0 * C) / MB, ghosts / MB, recs / MB,
+         gran / MB, (cells + ghosts + recs + gran) / MB, alg / MB, (cells + ghosts + recs + gran) / alg);
 }

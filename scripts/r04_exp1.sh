@@ -18,3 +18,5 @@ grep -E "PASS|FAIL|Error|assert|passed|failed" gpurun_out/warm_tests.log | tail 
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 NNGP_AB_N=1250000 NNGP_AB_M=20 timeout -k 10 300 python -u scripts/ab_env.py 3 100 1 'col:NNGP_ENGINE=colors' 'rg:NNGP_TILE_R=global' > gpurun_out/ab_c4share_c3.txt 2>&1 || { tail -20 gpurun_out/ab_c4share_c3.txt; exit 1; }
 grep rep gpurun_out/ab_c4share_c3.txt
+timeout -k 10 300 python -u bench.py --steps 100 --warmup 10 --no-cpu-baseline --mcmc-iters 20 > gpurun_out/bench_exp1.json 2> gpurun_out/bench_exp1.err || { tail -20 gpurun_out/bench_exp1.err; exit 1; }
+python3 -c "import json; d=json.loads(open('gpurun_out/bench_exp1.json').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d['config']['cold_calls'], d['config']['single_chain']['value'], d['roofline']['kernel_avg_us'], d['secondary'] and d['secondary']['value'])"

@@ -62,10 +62,12 @@ def test_heavy_metals_device_path_matches_oracle(P, O, heavy, m):
     # ill-conditioned (rows checked against the bound where 1e-10 fails)
     err = np.abs(Ld - Lo).max(1)
     scale = np.abs(Lo).max(1)
+    kmax = 1.0
     for i in np.nonzero(err > 1e-10 * scale)[0]:
         NN = va["NNarray"]
         idx = NN[i][NN[i] != O.NA] - 1
         kappa = np.linalg.cond(O.covmat("exponential_sphere", cp, L["locs"][idx]))
+        kmax = max(kmax, kappa)
         assert err[i] <= max(1e-10, 1e-14 * kappa) * scale[i], (i, kappa, err[i])
     iters, nc = 5, 3
     res = _run_chain(0, st, ctx, L["X"], L["observed_field"], L["space_time_model"], va, iters, 1.0, True, nc, 0, 1)
@@ -76,6 +78,16 @@ def test_heavy_metals_device_path_matches_oracle(P, O, heavy, m):
     np.testing.assert_array_equal(res["acceptance"]["covariance_acceptance_ancillary"], ref["acceptance"]["ancillary"])
     np.testing.assert_allclose(res["records"]["log_scale"][:, 0], ref["records"]["log_scale"], rtol=1e-6, atol=1e-8)
     np.testing.assert_allclose(res["records"]["beta_0"][:, 0], ref["records"]["beta_0"], rtol=1e-5, atol=1e-7)
-    np.testing.assert_allclose(res["state"]["params"]["field"], ref["params"]["field"], rtol=1e-4, atol=1e-5)
+    # the field after 5 iterations: rows of B agree to 1e-14 x cond(local
+    # covariance) (above); near-coincident real locations reach cond ~ kmax,
+    # and each sweep is a linear map of the field whose gain carries a row's
+    # relative error into its neighbours' draws -- the bound is that
+    # conditioning term with two decades for 5 x 3 sweeps, never looser than
+    # the 1e-4 this test carried before it was derived
+    ftol = min(1e-4, max(1e-8, 100 * 1e-14 * kmax))
+    fd, fr = res["state"]["params"]["field"], ref["params"]["field"]
+    rel = np.abs(fd - fr).max() / np.abs(fr).max()
+    print(f"heavy metals m={m}: cond max {kmax:.3g}, field max rel diff {rel:.3g}, tolerance {ftol:.3g}")
+    assert rel <= ftol, (rel, ftol, kmax)
     assert np.all(np.isfinite(res["records"]["beta"]))
     ctx.close()
