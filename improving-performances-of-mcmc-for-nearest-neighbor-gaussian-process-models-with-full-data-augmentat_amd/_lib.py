@@ -41,7 +41,7 @@ ABI_SYMBOLS = (
     "nngp_records_reserve", "nngp_record_field", "nngp_get_records",
     "nngp_shard_ipc_handle", "nngp_shard_ipc_open", "nngp_shard_sync",
     "nngp_factor_chains", "nngp_loglik_chains", "nngp_field_response_ratio_chains",
-    "nngp_sum_squared_residuals_chains",
+    "nngp_sum_squared_residuals_chains", "nngp_loglik_pair_chains",
 )
 SHARD_ID_BYTES = 128  # NNGP_SHARD_ID_BYTES
 IPC_HANDLE_BYTES = 192  # NNGP_IPC_HANDLE_BYTES
@@ -128,6 +128,7 @@ def _load():
     L.nngp_loglik_chains.argtypes = [_vp, C.c_int, C.c_int, _dp, _dp, _dp]
     L.nngp_field_response_ratio_chains.argtypes = [_vp, C.c_int, _dp, _dp, _dp]
     L.nngp_sum_squared_residuals_chains.argtypes = [_vp, C.c_int, _dp, _dp]
+    L.nngp_loglik_pair_chains.argtypes = [_vp, C.c_int, _dp, _dp, _dp, _dp, _dp]
     L.nngp_shard_ipc_handle.argtypes = [_vp, C.c_char_p, C.c_int]
     L.nngp_shard_ipc_open.argtypes = [_vp, C.c_char_p, C.c_int]
     L.nngp_shard_sync.argtypes = [_vp]

@@ -213,6 +213,13 @@ class ChainContext:
                                          out))
         return out
 
+    def loglik_pair_chains(self, chain_mask: int, beta0, log_scale_prop, log_scale_cur):
+        """(loglik_chains(1, ...), loglik_chains(0, ...)) in one pass over the rows."""
+        lp, lc = np.zeros(self.n_chains), np.zeros(self.n_chains)
+        self._chk(lib.nngp_loglik_pair_chains(self._h, int(chain_mask), self._vec(beta0), self._vec(log_scale_prop),
+                                              self._vec(log_scale_cur), lp, lc))
+        return lp, lc
+
     def field_response_ratio_chains(self, chain_mask: int, beta0, log_noise_variance) -> np.ndarray:
         out = np.zeros(self.n_chains)
         self._chk(lib.nngp_field_response_ratio_chains(self._h, int(chain_mask), self._vec(beta0),
@@ -270,7 +277,8 @@ class ChainView:
         attr = getattr(self.ctx, name)
         if not callable(attr) or name in ("close", "view", "sweep_chains", "sweep_timed",
                                                      "ancillary_propose_chains", "factor_chains", "loglik_chains",
-                                                     "field_response_ratio_chains", "sum_squared_residuals_chains"):
+                                                     "field_response_ratio_chains", "sum_squared_residuals_chains",
+                                                     "loglik_pair_chains"):
             return attr
 
         def bound(*a, **kw):

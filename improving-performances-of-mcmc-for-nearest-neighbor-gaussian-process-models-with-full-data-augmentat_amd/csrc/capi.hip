@@ -124,7 +124,7 @@ struct nngp_ctx {
   size_t z_cap = 0;
   SweepScalars* scal_d = nullptr;  // C
   SweepScalars* scal_h = nullptr;  // pinned, C
-  double* res_h = nullptr;         // pinned, 4 x kMaxChains doubles
+  double* res_h = nullptr;         // pinned, 4 x kRowJobsMax doubles
   int* fail_h = nullptr;           // pinned, kMaxChains failure rows of the factors
   unsigned long long* dbg_d = nullptr;  // NNGP_PROBE=9: per-chunk timestamps
   // tile-resident sweep engine (engine == 1; graph_prep.h TileLayout)
@@ -964,11 +964,11 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
   CK(dalloc(&c->tmp_d, (size_t)n * C));   // scratch vectors, chain-strided for batched solves
   CK(dalloc(&c->tmp2_d, (size_t)n * C));
   CK(dalloc(&c->partials_d, 4 * kRedBlocks * kRowJobsMax));
-  CK(dalloc(&c->res_d, 4 * kMaxChains));
+  CK(dalloc(&c->res_d, 4 * kRowJobsMax));
   CK(dalloc(&c->scal_d, C));
   CK(hipHostMalloc((void**)&c->scal_h, sizeof(SweepScalars) * C, hipHostMallocDefault));
   std::memset(c->scal_h, 0, sizeof(SweepScalars) * C);
-  CK(hipHostMalloc((void**)&c->res_h, 4 * kMaxChains * sizeof(double), hipHostMallocDefault));
+  CK(hipHostMalloc((void**)&c->res_h, 4 * kRowJobsMax * sizeof(double), hipHostMallocDefault));
   CK(hipHostMalloc((void**)&c->fail_h, kMaxChains * sizeof(int), hipHostMallocDefault));
   CK(upload(c->locs_d, locs_rm.data(), locs_rm.size(), c->st));
   CK(upload(c->nn_d, nn_dev.data(), nn_dev.size(), c->st));
@@ -1423,25 +1423,27 @@ int nngp_loglik(nngp_ctx* c, int which, double beta0, double log_scale, double* 
   return rc;
 }
 
-int nngp_loglik_chains(nngp_ctx* c, int which, int chain_mask, const double* beta0, const double* log_scale,
-                       double* ll) {
-  if (!c || !ll || !beta0 || !log_scale || (which != 0 && which != 1) || chain_mask <= 0 ||
-      chain_mask >= (1 << c->C))
-    return NNGP_ERR_ARG;
+// log-likelihood jobs (chain k, factor `which`) in ONE pass over the rows
+// (NNarray read once): per job exactly the single-job arithmetic, so any
+// grouping of jobs gives the same bits.  The factors' log-determinant and
+// row-statistics caches are updated in job order.
+struct LLJob { int k, which; double beta0, log_scale; double* out; };
+
+static int loglik_jobs(nngp_ctx* c, const LLJob* jobs, int nj) {
   { int rs_ = replica_fresh(c); if (rs_) return rs_; }
   int rc;
   if ((rc = set_device(c))) return rc;
-  // every chain of the mask in one pass over the rows (NNarray read once)
+  if (nj < 1 || nj > kRowJobsMax) return fail_msg(c, NNGP_ERR_ARG, "loglik: too many jobs");
   RowJobs J;
-  for (int k = 0; k < c->C; ++k) {
-    if (!((chain_mask >> k) & 1)) continue;
-    ChainState& S = c->ch[k];
+  for (int j = 0; j < nj; ++j) {
+    ChainState& S = c->ch[jobs[j].k];
+    const int which = jobs[j].which;
     if (!S.have_factor[which] || !S.have_field) return fail_msg(c, NNGP_ERR_STATE, "loglik: need factor and field");
     J.linv[J.M] = S.linv_d[which];
     J.x[J.M] = S.field_d;
-    J.shift[J.M] = beta0[k];
+    J.shift[J.M] = jobs[j].beta0;
     J.out[J.M] = nullptr;
-    J.res_slot[J.M] = k;
+    J.res_slot[J.M] = j;
     J.mode[J.M] = 1;
     for (const ChainState::LogDet& e : S.ld)
       if (e.lg == S.lgen[which]) J.mode[J.M] = 2;
@@ -1450,12 +1452,12 @@ int nngp_loglik_chains(nngp_ctx* c, int which, int chain_mask, const double* bet
   const int nb = launch_row_stats_jobs(c->st, J, c->nn_d, c->n, c->b, c->partials_d);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, launch_reduce4_jobs(c->st, J, c->partials_d, nb, c->res_d));
-  HIPCHK(c, hipMemcpyAsync(c->res_h, c->res_d, 4 * c->C * sizeof(double), hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipMemcpyAsync(c->res_h, c->res_d, 4 * nj * sizeof(double), hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
-  for (int k = 0; k < c->C; ++k) {
-    if (!((chain_mask >> k) & 1)) continue;
+  for (int j = 0; j < nj; ++j) {
+    const int k = jobs[j].k, which = jobs[j].which;
     ChainState& S = c->ch[k];
-    double* r = c->res_h + 4 * k;
+    double* r = c->res_h + 4 * j;
     bool cached = false;
     for (const ChainState::LogDet& e : S.ld)
       if (e.lg == S.lgen[which]) { r[0] = e.v; cached = true; }
@@ -1463,10 +1465,38 @@ int nngp_loglik_chains(nngp_ctx* c, int which, int chain_mask, const double* bet
       S.ld[S.ld_next] = {S.lgen[which], r[0]};
       S.ld_next ^= 1;
     }
-    ll[k] = r[0] - c->n * 0.5 * log_scale[k] - 0.5 * r[1] / std::exp(log_scale[k]);
-    rowstats_store(c, k, which, beta0[k], r);
+    *jobs[j].out = r[0] - c->n * 0.5 * jobs[j].log_scale - 0.5 * r[1] / std::exp(jobs[j].log_scale);
+    rowstats_store(c, k, which, jobs[j].beta0, r);
   }
   return NNGP_OK;
+}
+
+int nngp_loglik_chains(nngp_ctx* c, int which, int chain_mask, const double* beta0, const double* log_scale,
+                       double* ll) {
+  if (!c || !ll || !beta0 || !log_scale || (which != 0 && which != 1) || chain_mask <= 0 ||
+      chain_mask >= (1 << c->C))
+    return NNGP_ERR_ARG;
+  LLJob jobs[kRowJobsMax];
+  int nj = 0;
+  for (int k = 0; k < c->C; ++k)
+    if ((chain_mask >> k) & 1) jobs[nj++] = {k, which, beta0[k], log_scale[k], ll + k};
+  return loglik_jobs(c, jobs, nj);
+}
+
+int nngp_loglik_pair_chains(nngp_ctx* c, int chain_mask, const double* beta0, const double* log_scale_prop,
+                            const double* log_scale_cur, double* ll_prop, double* ll_cur) {
+  if (!c || !beta0 || !log_scale_prop || !log_scale_cur || !ll_prop || !ll_cur || chain_mask <= 0 ||
+      chain_mask >= (1 << c->C))
+    return NNGP_ERR_ARG;
+  // the proposal's jobs first, then the current factor's: the cache updates of
+  // nngp_loglik_chains(1, ...) followed by nngp_loglik_chains(0, ...)
+  LLJob jobs[kRowJobsMax];
+  int nj = 0;
+  for (int k = 0; k < c->C; ++k)
+    if ((chain_mask >> k) & 1) jobs[nj++] = {k, 1, beta0[k], log_scale_prop[k], ll_prop + k};
+  for (int k = 0; k < c->C; ++k)
+    if ((chain_mask >> k) & 1) jobs[nj++] = {k, 0, beta0[k], log_scale_cur[k], ll_cur + k};
+  return loglik_jobs(c, jobs, nj);
 }
 
 // ---------------------------------------------------------------- sweep

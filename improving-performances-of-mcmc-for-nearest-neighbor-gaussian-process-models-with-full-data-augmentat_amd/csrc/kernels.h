@@ -105,7 +105,7 @@ int launch_row_stats(hipStream_t st, const double* linv, const int* nn, int n, i
 // row_stats_kernel's products, butterfly and accumulation order (bitwise the
 // same partials), partials of job j at partials + j * kRedBlocks * 4, its
 // totals at res[4 * res_slot[j]] after launch_reduce4_jobs.  Returns #blocks.
-constexpr int kRowJobsMax = 4;
+constexpr int kRowJobsMax = 8;  // e.g. 4 chains x (proposal, current factor)
 struct RowJobs {
   const double* linv[kRowJobsMax];
   const double* x[kRowJobsMax];

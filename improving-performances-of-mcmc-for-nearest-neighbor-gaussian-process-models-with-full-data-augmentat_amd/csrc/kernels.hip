@@ -735,7 +735,10 @@ int launch_row_stats_jobs(hipStream_t st, const RowJobs& J, const int* nn, int n
     case 1: hipLaunchKernelGGL((row_stats_jobs_kernel<GG, 1>), dim3(g), dim3(kBlock), 0, st, J, nn, n, b, partials); break; \
     case 2: hipLaunchKernelGGL((row_stats_jobs_kernel<GG, 2>), dim3(g), dim3(kBlock), 0, st, J, nn, n, b, partials); break; \
     case 3: hipLaunchKernelGGL((row_stats_jobs_kernel<GG, 3>), dim3(g), dim3(kBlock), 0, st, J, nn, n, b, partials); break; \
-    default: hipLaunchKernelGGL((row_stats_jobs_kernel<GG, 4>), dim3(g), dim3(kBlock), 0, st, J, nn, n, b, partials); break; \
+    case 4: hipLaunchKernelGGL((row_stats_jobs_kernel<GG, 4>), dim3(g), dim3(kBlock), 0, st, J, nn, n, b, partials); break; \
+    case 5: hipLaunchKernelGGL((row_stats_jobs_kernel<GG, 5>), dim3(g), dim3(kBlock), 0, st, J, nn, n, b, partials); break; \
+    case 6: hipLaunchKernelGGL((row_stats_jobs_kernel<GG, 6>), dim3(g), dim3(kBlock), 0, st, J, nn, n, b, partials); break; \
+    default: hipLaunchKernelGGL((row_stats_jobs_kernel<GG, 8>), dim3(g), dim3(kBlock), 0, st, J, nn, n, b, partials); break; \
   }
   switch (G) {
     case 4: NNGP_RSJ(4) break;

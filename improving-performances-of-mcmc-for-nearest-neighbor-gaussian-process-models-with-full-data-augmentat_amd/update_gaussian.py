@@ -358,8 +358,7 @@ def _serve_group(owner, ids, reqs, contexts, out):
             r = owner.sum_squared_residuals_chains(mask, cols[0])
             res = {i: float(r[contexts[i].chain]) for i in live}
         else:
-            l1 = owner.loglik_chains(1, mask, cols[0], cols[1])
-            l0 = owner.loglik_chains(0, mask, cols[0], cols[2])
+            l1, l0 = owner.loglik_pair_chains(mask, cols[0], cols[1], cols[2])
             res = {i: (float(l1[contexts[i].chain]), float(l0[contexts[i].chain])) for i in live}
         out.update(res)
         return True

@@ -224,6 +224,13 @@ int nngp_loglik_chains(nngp_ctx* ctx, int which, int chain_mask, const double* b
 int nngp_field_response_ratio_chains(nngp_ctx* ctx, int chain_mask, const double* beta0,
                                      const double* log_noise_variance, double* ratio);
 int nngp_sum_squared_residuals_chains(nngp_ctx* ctx, int chain_mask, const double* beta0, double* ssr);
+/* The sufficient MH step's two log-likelihoods (update_Gaussian.R:184-186:
+ * ll_compressed_sparse_chol of the proposal minus that of the current factor)
+ * for the chains in chain_mask in ONE pass over the rows: ll_prop[k] =
+ * nngp_loglik_chains(1, ...) with log_scale_prop, ll_cur[k] =
+ * nngp_loglik_chains(0, ...) with log_scale_cur, bitwise. */
+int nngp_loglik_pair_chains(nngp_ctx* ctx, int chain_mask, const double* beta0, const double* log_scale_prop,
+                            const double* log_scale_cur, double* ll_prop, double* ll_cur);
 /* Y = B X for X n x ncols column-major (host buffers) */
 int nngp_spmv(nngp_ctx* ctx, int which, const double* X, int ncols, double* Y);
 /* x = B^{-1} u (host buffers, length n) */

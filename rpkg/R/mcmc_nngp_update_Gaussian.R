@@ -7,7 +7,7 @@
 #   precision_diag (:74,142,197)                          -> inside nngp_factor / nngp_accept_factor
 #   solve(new_B, B (field - beta_0)) (:127)                -> nngp_ancillary_propose_chains
 #   dnorm ratio (:129-131)                                 -> nngp_field_response_ratio_chains
-#   ll_compressed_sparse_chol (:8-12,184-186)              -> nngp_loglik_chains
+#   ll_compressed_sparse_chol (:8-12,184-186)              -> nngp_loglik_pair_chains (both factors, one pass)
 #   crossprod(B 1), (B field, B 1) (:221-222)              -> nngp_beta0_stats
 #   chromatic sampling (:257-275)                          -> nngp_sweep_chains (Philox normals on the device)
 #   SSR (:281)                                             -> nngp_sum_squared_residuals_chains
@@ -19,7 +19,7 @@
 # the context (one kernel pass, one host synchronisation), in the order of the
 # Python host mirror (update_gaussian.py): per iteration factor_chains,
 # ancillary_propose_chains, field_response_ratio_chains, chain by chain the
-# acceptances, factor_chains, loglik_chains (proposal, current), chain by chain
+# acceptances, factor_chains, loglik_pair_chains (proposal, current), chain by chain
 # the acceptances, beta_0 and mu, sweep_chains, sum_squared_residuals_chains,
 # chain by chain the field records -- the sequence the C client
 # tests/cpp/capi_sequence.c replays against the Python binding.  Each chain
@@ -178,8 +178,9 @@ mcmc_nngp_update_Gaussian <- function(locs, X, observed_field, space_time_model,
     if (any(ok)) {
       m <- .nngp_mask(which(ok))
       b0 <- ifelse(ok, vec("beta_0"), 0)
-      l1 <- nngp_loglik_chains(ctx, 1L, m, b0, ifelse(ok, new_ls, 0))
-      l0 <- nngp_loglik_chains(ctx, 0L, m, b0, ifelse(ok, vec("log_scale"), 0))
+      ll <- nngp_loglik_pair_chains(ctx, m, b0, ifelse(ok, new_ls, 0), ifelse(ok, vec("log_scale"), 0))
+      l1 <- ll$proposal
+      l0 <- ll$current
     }
     for (i in seq_len(C)) {
       if (ok[i] && l1[i] - l0[i] > log(draw(i, function() runif(1)))) {

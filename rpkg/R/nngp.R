@@ -102,6 +102,10 @@ nngp_factor_chains <- function(ctx, which, chain_mask, covfun, covparms)
         as.matrix(covparms) + 0)
 nngp_loglik_chains <- function(ctx, which, chain_mask, beta_0, log_scale)
   .Call(C_nngp_loglik_chains, ctx, as.integer(which), as.integer(chain_mask), as.double(beta_0), as.double(log_scale))
+# list(proposal = loglik_chains(1, ...), current = loglik_chains(0, ...)) in one pass over the rows
+nngp_loglik_pair_chains <- function(ctx, chain_mask, beta_0, log_scale_prop, log_scale_cur)
+  .Call(C_nngp_loglik_pair_chains, ctx, as.integer(chain_mask), as.double(beta_0), as.double(log_scale_prop),
+        as.double(log_scale_cur))
 nngp_field_response_ratio_chains <- function(ctx, chain_mask, beta_0, log_noise_variance)
   .Call(C_nngp_field_response_ratio_chains, ctx, as.integer(chain_mask), as.double(beta_0),
         as.double(log_noise_variance))

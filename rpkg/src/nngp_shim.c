@@ -486,6 +486,29 @@ SEXP C_nngp_loglik_chains(SEXP p, SEXP which, SEXP mask, SEXP beta0, SEXP log_sc
   return out;
 }
 
+SEXP C_nngp_loglik_pair_chains(SEXP p, SEXP mask, SEXP beta0, SEXP ls_prop, SEXP ls_cur) {
+  nngp_ctx* c = get_ctx(p);
+  const int k = ctx_chains(c);
+  const double *b0 = per_chain(beta0, k, "beta0"), *lp = per_chain(ls_prop, k, "log_scale_prop"),
+               *lc = per_chain(ls_cur, k, "log_scale_cur");
+  SEXP prop = PROTECT(chains_out(c));
+  SEXP cur = PROTECT(chains_out(c));
+  const int rc = nngp_loglik_pair_chains(c, as_int(mask), b0, lp, lc, REAL(prop), REAL(cur));
+  if (rc) {
+    UNPROTECT(2);
+    check(rc, c);
+  }
+  SEXP out = PROTECT(Rf_allocVector(VECSXP, 2));
+  SEXP nm = PROTECT(Rf_allocVector(STRSXP, 2));
+  SET_VECTOR_ELT(out, 0, prop);
+  SET_VECTOR_ELT(out, 1, cur);
+  SET_STRING_ELT(nm, 0, Rf_mkChar("proposal"));
+  SET_STRING_ELT(nm, 1, Rf_mkChar("current"));
+  Rf_setAttrib(out, R_NamesSymbol, nm);
+  UNPROTECT(4);
+  return out;
+}
+
 SEXP C_nngp_field_response_ratio_chains(SEXP p, SEXP mask, SEXP beta0, SEXP lnv) {
   nngp_ctx* c = get_ctx(p);
   const int k = ctx_chains(c);
@@ -555,6 +578,7 @@ static const R_CallMethodDef call_methods[] = {
     E(C_nngp_shard_ipc_open, 2),
     E(C_nngp_factor_chains, 5),
     E(C_nngp_loglik_chains, 5),
+    E(C_nngp_loglik_pair_chains, 5),
     E(C_nngp_field_response_ratio_chains, 4),
     E(C_nngp_sum_squared_residuals_chains, 3),
     {NULL, NULL, 0}};

@@ -83,8 +83,7 @@ static int lockstep(nngp_ctx* ctx, int n, double* f) {
       cps[3 * k] = 1.0; cps[3 * k + 1] = exp(nsh[k]); cps[3 * k + 2] = 0.0;
     }
     CHECK(nngp_factor_chains(ctx, 1, all, NNGP_EXPONENTIAL_ISOTROPIC, cps, 3, st), ctx);
-    CHECK(nngp_loglik_chains(ctx, 1, all, b0, nls, l1), ctx);
-    CHECK(nngp_loglik_chains(ctx, 0, all, b0, ls, l0), ctx);
+    CHECK(nngp_loglik_pair_chains(ctx, all, b0, nls, ls, l1, l0), ctx);
     pr3("l1", it, l1);
     pr3("l0", it, l0);
     for (int k = 0; k < C; ++k) {

@@ -19,6 +19,7 @@ int* INTEGER(SEXP);
 Rbyte* RAW(SEXP);
 R_xlen_t XLENGTH(SEXP);
 SEXP VECTOR_ELT(SEXP, R_xlen_t);
+SEXP SET_VECTOR_ELT(SEXP, R_xlen_t, SEXP);
 void SET_STRING_ELT(SEXP, R_xlen_t, SEXP);
 SEXP Rf_allocVector(int, R_xlen_t);
 SEXP Rf_allocMatrix(int, int, int);

@@ -180,3 +180,34 @@ def test_update_records_field_thinning(P, toy):
     assert np.all(np.abs(rec).sum(axis=1) > 0)
     for c in L["_contexts"]:
         c.close()
+
+
+def test_loglik_pair_equals_two_loglik_calls_bitwise(P, O):
+    """nngp_loglik_pair_chains (the sufficient MH step's proposal and current
+    log-likelihoods, update_Gaussian.R:184-186, in one pass over the rows) ==
+    nngp_loglik_chains(1, ...) and nngp_loglik_chains(0, ...), bitwise, for
+    every chain of a 4-chain context; the oracle's log-likelihood to 1e-10."""
+    n, m, C = 20_000, 10, 4
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=44)
+    rng = np.random.default_rng(45)
+    b0, lsp, lsc = rng.normal(size=C), rng.normal(size=C) * 0.1, rng.normal(size=C) * 0.1
+    res = []
+    for pair in (True, False):
+        with P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=C) as ctx:
+            Ls = []
+            for k in range(C):
+                ctx.select(k)
+                ctx.factor(0, "exponential_isotropic", [1.0, 0.08 + 0.01 * k, 0.0])
+                ctx.factor(1, "exponential_isotropic", [1.1, 0.07 + 0.01 * k, 0.0])
+                ctx.set_field(np.random.default_rng(k).normal(size=n))
+                Ls.append((ctx.get_linv(1), ctx.get_linv(0), ctx.get_field()))
+            if pair:
+                res.append(ctx.loglik_pair_chains((1 << C) - 1, b0, lsp, lsc))
+            else:
+                res.append((ctx.loglik_chains(1, (1 << C) - 1, b0, lsp), ctx.loglik_chains(0, (1 << C) - 1, b0, lsc)))
+    assert np.array_equal(res[0][0], res[1][0]) and np.array_equal(res[0][1], res[1][1])
+    for k in range(C):
+        L1, L0, f = Ls[k]
+        for ll, L, ls in ((res[0][0][k], L1, lsp[k]), (res[0][1][k], L0, lsc[k])):
+            llo = O.loglik(L, f - b0[k], NN, ls)
+            assert abs(ll - llo) <= 1e-10 * abs(llo)
