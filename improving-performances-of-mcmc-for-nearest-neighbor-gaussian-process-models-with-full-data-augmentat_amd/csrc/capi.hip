@@ -655,15 +655,29 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       // batches per phase, each behind dependent global round trips -- so the
       // colour engine stays the default there
       const char* trg = std::getenv("NNGP_TILE_R");
-      const bool force_rg = trg && std::string(trg) == "global";
-      if (ok && xw && need > lds_max) { ok = false; terr = "exchange-wave tiles exceed the LDS"; }
-      if (ok && (need > lds_max || force_rg)) {
+      bool force_rg = trg && std::string(trg) == "global";
+      int need_now = need;
+      // a tile shard (G > 1) whose LDS tiles do not fit runs tiles with r in
+      // global memory instead of the colour shard (configs[4]: n = 1e7, m = 20,
+      // 3 chains over 8 GPUs, tests/test_capi_and_graph.py
+      // test_configs4_tile_shard_geometry): the layout is rebuilt
+      // for the RG kernel's 512 cell threads
+      if (ok && shard_G > 1 && !force_rg && need > lds_max && NT == 512 && !csplit && !split) {
+        ok = build_tile_layout(nn.data(), n, b, coloring, locs, d, T, NT, tile_rmax(n_chains, NT), c->tl, terr, G,
+                               false, 0);
+        c->tl.NTK = NT;
+        c->txw = 0;
+        force_rg = true;
+        need_now = ok ? tile_lds_bytes(c->tl.max_rows, n_chains, NT, c->tl.K, c->tl.max_batches, c->tl.max_gslots) : 0;
+      }
+      if (ok && c->txw && need_now > lds_max) { ok = false; terr = "exchange-wave tiles exceed the LDS"; }
+      if (ok && (need_now > lds_max || force_rg)) {
         const int need_rg = tile_lds_bytes(0, n_chains, NT, c->tl.K, c->tl.max_batches, c->tl.max_gslots);
         if (force_rg && (NT == 512 || (NT == 1024 && shard_G == 0)) && need_rg <= lds_max) {
           c->rglobal = true;
         } else {
           ok = false;
-          terr = "tile layout needs " + std::to_string(need) +
+          terr = "tile layout needs " + std::to_string(need_now) +
                  " B of LDS per tile (device: " + std::to_string(lds_max) + ")";
         }
       }
@@ -715,7 +729,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
         }
         c->engine_note = "tiles: " + std::to_string(T) + " tiles of " + std::to_string(NT) + " threads, " +
                          std::to_string(c->tresident) + " resident per CU x " + std::to_string(cus) + " CUs" +
-                         (c->rglobal ? ", r in global memory" : "") + (xw ? ", exchange wave" : "") +
+                         (c->rglobal ? ", r in global memory" : "") + (c->txw == 2 ? ", exchange wave, wave-local batches" : c->txw ? ", exchange wave" : "") +
                          (c->tcs ? ", chain-split" : "");
         if (shard_G > 0) {
           c->shard = true;

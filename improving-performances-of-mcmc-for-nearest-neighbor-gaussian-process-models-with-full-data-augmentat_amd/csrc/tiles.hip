@@ -966,7 +966,7 @@ __device__ __forceinline__ void tile_phase_wl(const TileDev& D, const TileLaunch
 // only) instead of in one burst of every CU after the draw.  The values are
 // never used; the exchange wave's wait before its polls covers the loads.
 constexpr int kPfLoads = 40;  // per lane: 64 x 40 segments = 160 KB per phase at most
-template <int C, int NTC>
+template <int C, int NTC, int WL = 0, int NW = 8>
 __device__ __forceinline__ void tile_xw_prefetch(const TileDev& D, const TileState& S, int ph, int lane,
                                                  uint32_t (&pf)[kPfLoads]) {
   constexpr int NR = 4 + 2 * C + 1 + C;
@@ -986,8 +986,15 @@ __device__ __forceinline__ void tile_xw_prefetch(const TileDev& D, const TileSta
   const bool more = phn < S.nph && S.bptr_s[cn] < S.bptr_s[cn + 1];
   const int4 Bn = more ? S.batch_s[S.bptr_s[cn]] : make_int4(0, 0, 0, 0);
   const bool rec = more && (D.pf & 2), cel = more && (D.pf & 1);
-  const long long ncell = (long long)(Bn.y & 0xFFFF) * NTC;
-  const int ns = Bn.z, x0 = Bn.w;
+  long long ncell = (long long)(Bn.y & 0xFFFF) * NTC;
+  int ns = Bn.z;
+  const int x0 = Bn.w;
+  if (WL && more) {  // the next colour's first round: its W wave batches are contiguous in cells and slots
+    const int lb = min(S.bptr_s[cn] + (NW - 1) - 1, S.bptr_s[cn + 1] - 1);  // NW - 1 cell waves
+    const int4 Bl = S.batch_s[lb];
+    ncell = (long long)Bl.x + (long long)(Bl.y & 0xFFFF) * 64 - Bn.x;
+    ns = Bl.w + Bl.z - x0;
+  }
   region(D.sinfo + x0, (long long)ns * 8, rec);
   region(D.slot_loc + x0, (long long)ns * 4, rec);
   region(D.dr + (size_t)x0 * C, (long long)ns * C * 16, rec);
@@ -1043,7 +1050,7 @@ __device__ __forceinline__ void tile_phase_xw(const TileDev& D, TileState& S, in
     gx[k] = u < nfi ? D.gslot[gs0 + u / C] : 0;
   }
   uint32_t pfv[kPfLoads];
-  if (D.pf) tile_xw_prefetch<C, NT - 64>(D, S, ph, lane, pfv);
+  if (D.pf) tile_xw_prefetch<C, WL ? 64 : NT - 64, WL, NT / 64>(D, S, ph, lane, pfv);
   // the own batches' barriers (tile_own_draw: kOwnDrawBarriers each, + 1
   // before a later batch, as tile_phase_cells; wave-local batches have none)
   for (int bi = bfirst; bi < (WL ? bfirst : bend); ++bi) {

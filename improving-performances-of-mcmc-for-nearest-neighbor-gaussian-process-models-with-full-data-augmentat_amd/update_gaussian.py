@@ -36,6 +36,7 @@ reproducible.
 from __future__ import annotations
 
 import ctypes
+import math
 import threading
 
 import numpy as np
@@ -157,7 +158,7 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
     for it in range(1, n_iterations_update + 1):
         # ---- ancillary covariance update (:113-157)
         if ancillary:
-            innov = rng.normal(0.0, np.exp(0.5 * tk["covariance_params_ancillary"]["logvar"]), n_shape + 1)
+            innov = rng.normal(0.0, math.exp(0.5 * tk["covariance_params_ancillary"]["logvar"]), n_shape + 1)
             new_ls = params["log_scale"] + innov[0]
             new_shape = params["shape"] + innov[1:]
             st = yield ("fac", covfun, covparms(sp_names, new_shape))
@@ -167,7 +168,7 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
             yield ("anc", params["beta_0"], new_ls - params["log_scale"], ok)
             ratio = yield (("ratio", params["beta_0"], params["log_noise_variance"]) if ok else ("ratio", None))
             if ok:
-                if ratio > np.log(rng.uniform()):
+                if ratio > math.log(rng.uniform()):
                     params["shape"] = new_shape
                     params["log_scale"] = new_ls
                     ctx.accept_field()
@@ -183,16 +184,16 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
                     tk["covariance_params_ancillary"]["logvar"] += rng.normal(0.4, 0.05)
 
         # ---- sufficient covariance update (:165-213)
-        innov = rng.normal(0.0, np.exp(0.5 * tk["covariance_params_sufficient"]["logvar"]), n_shape + 1)
+        innov = rng.normal(0.0, math.exp(0.5 * tk["covariance_params_sufficient"]["logvar"]), n_shape + 1)
         new_ls = params["log_scale"] + innov[0]
-        propose = np.exp(new_ls) < var_y
+        propose = math.exp(new_ls) < var_y
         new_shape = params["shape"] + innov[1:] if propose else None
         st = yield ("fac", covfun, covparms(sp_names, new_shape) if propose else None)
         ok = propose and _proposal_ok(st, on_chol_error)
         lls = yield (("llpair", params["beta_0"], new_ls, params["log_scale"]) if ok else ("llpair", None))
         if ok:
             gp_ratio = lls[0] - lls[1]
-            if gp_ratio > np.log(rng.uniform()):
+            if gp_ratio > math.log(rng.uniform()):
                 params["shape"] = new_shape
                 params["log_scale"] = new_ls
                 ctx.accept_factor()
@@ -209,15 +210,15 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
         # ---- field mean (:219-247)
         if (not has_locs) or (not has_X):
             oqo, oqf = ctx.beta0_stats()
-            beta_covmat = np.exp(params["log_scale"]) / oqo
-            beta_mean = np.exp(-params["log_scale"]) * oqf * beta_covmat
-            params["beta_0"] = float(beta_mean + np.sqrt(beta_covmat) * rng.normal())
+            beta_covmat = math.exp(params["log_scale"]) / oqo
+            beta_mean = math.exp(-params["log_scale"]) * oqf * beta_covmat
+            params["beta_0"] = float(beta_mean + math.sqrt(beta_covmat) * rng.normal())
         if has_X:
             field = ctx.get_field()
             X1 = np.column_stack([np.ones(n_obs), X["X"]])
             resid = observed_field - field[va["locs_match"] - 1] + params["beta_0"]
             beta_mean = (resid @ X1) @ X["solve_1XT1X"]
-            innov = beta_mean + np.exp(0.5 * params["log_noise_variance"]) * (
+            innov = beta_mean + math.exp(0.5 * params["log_noise_variance"]) * (
                 X["chol_solve_1XT1X"].T @ rng.normal(size=X1.shape[1]))
             field = field - params["beta_0"] + innov[0]
             params["beta_0"] = float(innov[0])
@@ -227,7 +228,7 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
                 other = field + iw["Xl"] @ params["beta"][locs_cols]
                 Bo = ctx.spmv(0, other)
                 bm = iw["covmat"] @ (Bo @ iw["SX"])
-                innov = bm + np.exp(0.5 * params["log_scale"]) * (iw["covmat_chol"].T @ rng.normal(size=len(locs_cols) + 1))
+                innov = bm + math.exp(0.5 * params["log_scale"]) * (iw["covmat_chol"].T @ rng.normal(size=len(locs_cols) + 1))
                 params["beta_0"] = float(innov[0])
                 params["beta"][locs_cols] = innov[1:]
                 field = other - iw["Xl"] @ params["beta"][locs_cols]
@@ -242,9 +243,9 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
         ssr = yield ("ssr", params["beta_0"])
         for _ in range(10):
             innov = rng.normal(0.0, 0.01)
-            if np.exp(params["log_noise_variance"] + innov) < var_y:
+            if math.exp(params["log_noise_variance"] + innov) < var_y:
                 lnv = params["log_noise_variance"]
-                if -0.5 * n_obs * innov - 0.5 * ssr * (np.exp(-lnv - innov) - np.exp(-lnv)) > np.log(rng.uniform()):
+                if -0.5 * n_obs * innov - 0.5 * ssr * (math.exp(-lnv - innov) - math.exp(-lnv)) > math.log(rng.uniform()):
                     params["log_noise_variance"] = lnv + innov
 
         # ---- records (:305-311)

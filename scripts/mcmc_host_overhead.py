@@ -77,6 +77,9 @@ class FakeCtx:
     def loglik_chains(self, which, mask, b0, ls):
         return self.rng.normal(size=self.n_chains)
 
+    def loglik_pair_chains(self, mask, b0, lsp, lsc):
+        return self.rng.normal(size=self.n_chains), self.rng.normal(size=self.n_chains)
+
     def sum_squared_residuals_chains(self, mask, b0):
         return np.full(self.n_chains, 0.25 * self.n)
 
