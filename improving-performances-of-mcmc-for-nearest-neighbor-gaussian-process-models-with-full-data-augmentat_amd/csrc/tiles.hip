@@ -896,11 +896,14 @@ __device__ __forceinline__ void tile_own_wl(const TileDev& D, const TileLaunch& 
   TLSTAMP(S, 1);
 }
 
-// the cell waves' colour phase on wave-local batches
-template <int C, int NT, int RMAX, int GMAX, int PROBE, int SH>
+// the cell waves' colour phase on wave-local batches.  DB (<= 2 chains, two
+// register sets): the wave's next batch loads at the phase start, its HBM
+// stream overlapping this colour's work; otherwise its records after the
+// draw and its cells after the scatter and the draw preparation.
+template <int C, int NT, int RMAX, int GMAX, int PROBE, int SH, int DB>
 __device__ __forceinline__ void tile_phase_wl(const TileDev& D, const TileLaunch& a, const TileShard& sh,
                                               TileState& S, int ph, TileBatchRegs<C, 64, RMAX>& cur,
-                                              TileGhostRegs<C, GMAX>& gr) {
+                                              TileBatchRegs<C, 64, RMAX>& nxt, TileGhostRegs<C, GMAX>& gr) {
   constexpr int W = NT / 64 - 1;  // cell waves
   const int K = S.K, t = S.t, lane = S.lane;
   const int s = ph / K, c = ph - s * K;
@@ -915,6 +918,7 @@ __device__ __forceinline__ void tile_phase_wl(const TileDev& D, const TileLaunch
   const int bfirst = S.bptr_s[c] + S.wv, bend = S.bptr_s[c + 1];
   const int g0 = S.gptr_s[c], g1 = S.gptr_s[c + 1];
   double* acc_w = S.acc_s + S.wv * (kWaveSlotsMax * C);
+  if (DB && more) tile_load_batch<C, 64, RMAX, SH>(D, S.batch_s[bnext], nxt, lane);
   for (int bi = bfirst; bi < bend; bi += W) {
     if (bi != bfirst) {  // a later round of this colour (large colours only): independent rows, no barrier
       tile_load_batch<C, 64, RMAX, SH>(D, S.batch_s[bi], cur, lane);
@@ -923,18 +927,18 @@ __device__ __forceinline__ void tile_phase_wl(const TileDev& D, const TileLaunch
     tile_own_wl<C, RMAX, PROBE, SH>(D, a, sh, S, cur, epoch, acc_w);
     const int R = cur.R;
     if (bi + W >= bend) {  // this wave's last batch of the colour: its records are dead
-      if (more) tile_load_items<C, 64, RMAX, SH>(D, S.batch_s[bnext], cur, lane);
+      if (!DB && more) tile_load_items<C, 64, RMAX, SH>(D, S.batch_s[bnext], nxt, lane);
       if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
     }
     tile_own_scatter<C, 64, RMAX, PROBE>(S, cur, R, acc_w);
   }
   if (bfirst >= bend) {  // no batch of this colour for this wave
-    if (more) tile_load_items<C, 64, RMAX, SH>(D, S.batch_s[bnext], cur, lane);
+    if (!DB && more) tile_load_items<C, 64, RMAX, SH>(D, S.batch_s[bnext], nxt, lane);
     if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
   }
   TLSTAMP(S, 6);
-  if (more) tile_prep_items<C, 64, RMAX>(D, a, S.sc_s, S.seed_s, sn, cur, lane);
-  if (more) tile_load_cells<C, 64, RMAX>(D, S.batch_s[bnext], cur, lane);
+  if (more) tile_prep_items<C, 64, RMAX>(D, a, S.sc_s, S.seed_s, sn, nxt, lane);
+  if (!DB && more) tile_load_cells<C, 64, RMAX>(D, S.batch_s[bnext], nxt, lane);
   TLSTAMP(S, 4);
   __syncthreads();  // the exchange wave has every dw of the colour in gdw_s
   TLSTAMP(S, 2);
@@ -1277,14 +1281,21 @@ __device__ __forceinline__ void sweep_tiles_body(const TileDev& D0, TileLaunch a
       __syncthreads();
       for (int ph = 0; ph < S.nph; ++ph) tile_phase_xw<C, NT, GMAX, PROBE, SH, XW == 2>(D, S, ph, GX);
     } else if constexpr (XW == 2) {  // wave-local batches: wave w runs batches first + w, + W, ...
-      TileBatchRegs<C, 64, RMAX> A;
+      TileBatchRegs<C, 64, RMAX> A, B;
       TileGhostRegs<C, GMAX> GA;
       if (S.nph > 0 && S.bptr_s[0] + S.wv < S.bptr_s[1]) {
         tile_load_batch<C, 64, RMAX, SH>(D, S.batch_s[S.bptr_s[0] + S.wv], A, S.lane);
         tile_prep_items<C, 64, RMAX>(D, a, S.sc_s, S.seed_s, 0, A, S.lane);
       }
       __syncthreads();
-      for (int ph = 0; ph < S.nph; ++ph) tile_phase_wl<C, NT, RMAX, GMAX, PROBE, SH>(D, a, sh, S, ph, A, GA);
+      if (DB) {
+        for (int ph = 0; ph < S.nph; ph += 2) {
+          tile_phase_wl<C, NT, RMAX, GMAX, PROBE, SH, DB>(D, a, sh, S, ph, A, B, GA);
+          if (ph + 1 < S.nph) tile_phase_wl<C, NT, RMAX, GMAX, PROBE, SH, DB>(D, a, sh, S, ph + 1, B, A, GA);
+        }
+      } else {
+        for (int ph = 0; ph < S.nph; ++ph) tile_phase_wl<C, NT, RMAX, GMAX, PROBE, SH, DB>(D, a, sh, S, ph, A, A, GA);
+      }
     } else {
       BR A, B;
       TileGhostRegs<C, GMAX> GA;
