@@ -619,12 +619,13 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       // at 1 chain (tiles.hip tile_phase_xw)
       const char* txe = std::getenv("NNGP_TILE_XW");
       const int xwm = txe ? std::atoi(txe) : 1;
-      const bool xw = !csplit && !split && !rg_forced && NT == 512 && xwm == 1;
       // wave-local batches (NNGP_TILE_WL=1, exchange-wave tiles): one wave per
       // batch, the layout cut for 64-lane batches in rounds of the NT/64 - 1
-      // cell waves (tiles.hip tile_phase_wl)
+      // cell waves (tiles.hip tile_phase_wl); with r in global memory too
       const char* twl = std::getenv("NNGP_TILE_WL");
-      const bool wl = xw && twl && std::string(twl) == "1";
+      const bool wl_env = twl && std::string(twl) == "1";
+      const bool xw = !csplit && !split && (!rg_forced || wl_env) && NT == 512 && xwm == 1;
+      const bool wl = xw && wl_env;
       const int NTL = wl ? 64 : (xw ? NT - 64 : NT);  // the layout's cell threads of a batch
       if (const char* bc = std::getenv("NNGP_TILE_BATCH_CELLS"))
         rmax_l = std::max(1, std::min(rmax_l, std::atoi(bc) / NTL));
@@ -670,7 +671,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
         force_rg = true;
         need_now = ok ? tile_lds_bytes(c->tl.max_rows, n_chains, NT, c->tl.K, c->tl.max_batches, c->tl.max_gslots) : 0;
       }
-      if (ok && c->txw && need_now > lds_max) { ok = false; terr = "exchange-wave tiles exceed the LDS"; }
+      if (ok && c->txw && !force_rg && need_now > lds_max) { ok = false; terr = "exchange-wave tiles exceed the LDS"; }
       if (ok && (need_now > lds_max || force_rg)) {
         const int need_rg = tile_lds_bytes(0, n_chains, NT, c->tl.K, c->tl.max_batches, c->tl.max_gslots);
         if (force_rg && (NT == 512 || (NT == 1024 && shard_G == 0)) && need_rg <= lds_max) {

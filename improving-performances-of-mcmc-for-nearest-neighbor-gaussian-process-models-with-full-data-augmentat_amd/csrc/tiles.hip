@@ -1202,7 +1202,8 @@ __device__ __forceinline__ void tile_phase_cells(const TileDev& D, const TileLau
 // chain never waits on a tile of its own that is not resident.
 template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE, int SH, int RG, int IB, int CS, int XW = 0>
 __device__ __forceinline__ void sweep_tiles_body(const TileDev& D0, TileLaunch a, const TileShard& sh) {
-  static_assert(!XW || (!RG && !IB && CS == C), "exchange-wave tiles: r in LDS, joint chains, no split layout");
+  static_assert(!XW || ((!RG || XW == 2) && !IB && CS == C),
+                "exchange-wave tiles: joint chains, no split layout; r in global memory only with wave-local batches");
   constexpr int NTC = XW ? NT - 64 : NT;  // cell threads
   using BR = TileBatchRegs<C, NTC, RMAX>;
   constexpr int NW = NT / 64;
@@ -1395,7 +1396,10 @@ static hipError_t launch_tiles_c(hipStream_t st, const TileDev& D, const TileLau
     if (D.xw == 1) k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE, SH, RG, IB, 1>;
     if (D.xw == 2) k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE, SH, RG, IB, 2>;
   }
-  if (D.xw && (NT != 512 || RG || IB)) return hipErrorInvalidValue;
+  if constexpr (NT == 512 && RG && !IB && !PROBE) {  // r in global memory on wave-local batches
+    if (D.xw == 2) k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE, SH, RG, IB, 2>;
+  }
+  if (D.xw && (NT != 512 || (RG && D.xw != 2) || IB)) return hipErrorInvalidValue;
   lds = lds < kTSpreadLds ? kTSpreadLds : lds;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return e;
