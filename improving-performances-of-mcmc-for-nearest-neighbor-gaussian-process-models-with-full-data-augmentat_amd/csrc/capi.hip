@@ -153,7 +153,6 @@ struct nngp_ctx {
   bool warm_on = false;           // warm sweep calls allowed (tile engine, not a shard; NNGP_SWEEP_WARM=0: off)
   bool tcs = false;               // chain-split tile launches (one chain per workgroup, kernels.hip sweep_tiles_cs_kernel)
   int txw = 0;                    // exchange-wave tiles (tiles.hip tile_phase_xw): layout cut for NT - 64 cell threads
-  int tpf = 0;                    // exchange-wave L2 prefetch bits (TileDev::pf; NNGP_TILE_PF)
   int cus = 0;                    // compute units of the device
   int tresident = 0;              // tile workgroups resident per CU (occupancy query of the instantiation)
   int engine_fallback = 0;        // 0: none, 1: tile layout unsuitable (LDS, shape), 2: residency, 3: forced colours
@@ -307,7 +306,6 @@ TileDev tile_dev(nngp_ctx* c) {
   D.dbg = c->tdbg_d;
   D.probe = c->tprobe;
   D.xw = c->txw;
-  D.pf = c->txw ? c->tpf : 0;
   D.K = c->tl.K;
   D.C = c->C;
   D.T = c->tl.T;
@@ -605,8 +603,22 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       const bool split = !csplit && tile_double_buffer(n_chains, NT) == 0 && tsp && std::string(tsp) == "1";
       // a tile's own rows alone beyond the LDS: no layout to build (n = 8e6 on
       // one GPU would spend ~30 s building one that cannot run)
-      const bool rg_forced = std::getenv("NNGP_TILE_R") && std::string(std::getenv("NNGP_TILE_R")) == "global";
-      const bool hopeless = !rg_forced && (long long)(n / std::max(T, 1)) * n_chains * 8 > (long long)lds_max;
+      // The colour engine refuses a column of B longer than its sweep chunk
+      // (LW x kRowsMax entries, 256 at 3-4 chains: configs[4]'s m = 20 graph
+      // at 3 chains); tiles whose r does not fit the LDS then run with r in
+      // global memory rather than fail
+      const int col_cap = (n_chains == 1 ? 64 : (n_chains == 2 ? 32 : 16)) * kRowsMax;
+      int max_col = 0;
+      {
+        std::vector<int> cl(n, 0);
+        for (long long e = 0; e < (long long)n * b; ++e)
+          if (nn[e] >= 0) max_col = std::max(max_col, ++cl[nn[e]]);
+      }
+      const bool colours_refuse = max_col > col_cap;
+      const bool rows_beyond_lds = (long long)(n / std::max(T, 1)) * n_chains * 8 > (long long)lds_max;
+      const bool rg_forced = (std::getenv("NNGP_TILE_R") && std::string(std::getenv("NNGP_TILE_R")) == "global") ||
+                             (rows_beyond_lds && colours_refuse && NT == 512);
+      const bool hopeless = !rg_forced && rows_beyond_lds;
       if (hopeless) terr = "tile layout: a tile's own rows exceed the LDS";
       // cells per own batch: NT x RMAX of the kernel; NNGP_TILE_BATCH_CELLS
       // may lower it (e.g. joint tiles cut like chain-split ones, for bitwise
@@ -619,11 +631,15 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       // at 1 chain (tiles.hip tile_phase_xw)
       const char* txe = std::getenv("NNGP_TILE_XW");
       const int xwm = txe ? std::atoi(txe) : 1;
-      // wave-local batches (NNGP_TILE_WL=1, exchange-wave tiles): one wave per
-      // batch, the layout cut for 64-lane batches in rounds of the NT/64 - 1
-      // cell waves (tiles.hip tile_phase_wl); with r in global memory too
+      // wave-local batches (exchange-wave tiles): one wave per batch, the
+      // layout cut for 64-lane batches in rounds of the NT/64 - 1 cell waves
+      // (tiles.hip tile_phase_wl); with r in global memory too.  Default at 3+
+      // chains (NNGP_TILE_WL=0 turns them off, =1 asks for them at any chain
+      // count).  Measured at the headline: 12.96k vs 12.47k chain-sweeps/s at
+      // 3 chains (2,218 vs 2,275 us per 10-sweep launch), 5.76k vs 7.09k at 1
+      // chain
       const char* twl = std::getenv("NNGP_TILE_WL");
-      const bool wl_env = twl && std::string(twl) == "1";
+      const bool wl_env = twl ? std::string(twl) == "1" : n_chains >= 3;
       const bool xw = !csplit && !split && (!rg_forced || wl_env) && NT == 512 && xwm == 1;
       const bool wl = xw && wl_env;
       const int NTL = wl ? 64 : (xw ? NT - 64 : NT);  // the layout's cell threads of a batch
@@ -634,7 +650,6 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
                                   split, wl ? NT / 64 - 1 : 0);
       c->tl.NTK = NT;
       c->txw = xw ? (wl ? 2 : 1) : 0;
-      if (const char* pf = std::getenv("NNGP_TILE_PF")) c->tpf = std::atoi(pf) & 7;
       if (ok && csplit) {
         // n_chains workgroups of one chain per CU
         const int need1 = tile_lds_bytes(c->tl.max_rows, 1, NT, c->tl.K, c->tl.max_batches, c->tl.max_gslots);
@@ -655,15 +670,15 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       // 1024 threads: 341) against the colour engine's 449 -- five serial
       // batches per phase, each behind dependent global round trips -- so the
       // colour engine stays the default there
-      const char* trg = std::getenv("NNGP_TILE_R");
-      bool force_rg = trg && std::string(trg) == "global";
+      bool force_rg = rg_forced;
       int need_now = need;
       // a tile shard (G > 1) whose LDS tiles do not fit runs tiles with r in
       // global memory instead of the colour shard (configs[4]: n = 1e7, m = 20,
       // 3 chains over 8 GPUs, tests/test_capi_and_graph.py
       // test_configs4_tile_shard_geometry): the layout is rebuilt
       // for the RG kernel's 512 cell threads
-      if (ok && shard_G > 1 && !force_rg && need > lds_max && NT == 512 && !csplit && !split) {
+      // One GPU takes the same route when the colour engine cannot either
+      if (ok && (shard_G > 1 || colours_refuse) && !force_rg && need > lds_max && NT == 512 && !csplit && !split) {
         ok = build_tile_layout(nn.data(), n, b, coloring, locs, d, T, NT, tile_rmax(n_chains, NT), c->tl, terr, G,
                                false, 0);
         c->tl.NTK = NT;

@@ -547,8 +547,8 @@ bool build_tile_layout(const int* nn, int n, int b, const int* colors, const dou
   L = TileLayout();
   L.n = n; L.b = b; L.NT = NT; L.RMAX = RMAX; L.W = waves;
   if (NT < 64 || NT > 1024 || RMAX < 1 || (long long)NT * RMAX > (1 << 20)) { err = "tile layout: bad NT/RMAX"; return false; }
-  if (waves < 0 || (waves > 0 && (NT != 64 || split || waves * kWaveSlotsMax > kTileSlotsMax))) {
-    err = "tile layout: wave-local batches need NT = 64, no split, waves x kWaveSlotsMax <= kTileSlotsMax";
+  if (waves < 0 || (waves > 0 && (NT != 64 || split || waves * kWaveSlotsMax > kAccSlots))) {
+    err = "tile layout: wave-local batches need NT = 64, no split, waves x kWaveSlotsMax <= kAccSlots";
     return false;
   }
   if (T < 1) T = 1;
@@ -967,7 +967,7 @@ void dag_levels(const int* nn, int n, int b, std::vector<int>& level_ptr, std::v
 
 int tile_lds_bytes(int max_rows, int C, int NT, int K, int max_batches, int max_gslots) {
   const int rbytes = ((max_rows * C * 8 + 15) / 16) * 16;
-  return rbytes + kTileSlotsMax * C * 8 + (NT / 64) * C * 8 + 4 * C * 8 + ((max_gslots * C + 1) / 2) * 16 +
+  return rbytes + kAccSlots * C * 8 + (NT / 64) * C * 8 + 4 * C * 8 + ((max_gslots * C + 1) / 2) * 16 +
          max_batches * 16 + 4 * (K + 1) * 4 + (NT / 64) * 4 + 64;
 }
 

@@ -158,7 +158,11 @@ struct TileLayout {
   // colour (the batches of one colour touch disjoint rows of B)
   int W = 0;
 };
-constexpr int kWaveSlotsMax = 36;  // slots of a wave-local batch (W x 36 <= kTileSlotsMax for W <= 7)
+constexpr int kWaveSlotsMax = 42;  // slots of a wave-local batch (7 x 42 = 294 >= the 257 slots of the
+                                   // largest colour of a headline tile: one round)
+// slot totals a tile workgroup keeps in LDS (acc_s): a workgroup batch's
+// kTileSlotsMax, or the 7 cell waves' wave-local batches of a 512-thread tile
+constexpr int kAccSlots = 7 * kWaveSlotsMax > kTileSlotsMax ? 7 * kWaveSlotsMax : kTileSlotsMax;
 
 // Fails (returns false, err set) when the layout does not fit the packed
 // formats; the caller checks the LDS budget (max_rows).

@@ -193,8 +193,6 @@ struct TileDev {
   int probe = 0;              // dbg layout: 1 = per-tile segment sums (T x 8), 2 = timeline (T x 512 phases x 8)
   int xw = 0;                 // exchange-wave tiles: the last wave polls the hand-offs, the
                               // layout's batches are cut for NT - 64 cell threads
-  int pf = 0;                 // exchange-wave L2 prefetch during the own work (bit 1: the next
-                              // batch's cells, 2: its per-slot records, 4: this colour's ghost cells)
 };
 
 struct TileLaunch {

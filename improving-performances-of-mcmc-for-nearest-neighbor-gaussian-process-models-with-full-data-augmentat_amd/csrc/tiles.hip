@@ -962,75 +962,6 @@ __device__ __forceinline__ void tile_phase_wl(const TileDev& D, const TileLaunch
 // threads ("cell waves") scatter, prepare the next batch and stream its cells.
 // The layout's batches are cut for NT - 64 cell threads.
 
-// L2 prefetch by the exchange wave (TileDev::pf): the bytes the cell waves
-// load after this phase's draw -- the next phase's first batch (per-slot
-// records, cells) and this colour's ghost cells -- are touched at the phase
-// start, one 4-B load per 64-B segment (default cache policy: the lines
-// stay in the XCD's L2), so their HBM stream runs during the own work (LDS
-// only) instead of in one burst of every CU after the draw.  The values are
-// never used; the exchange wave's wait before its polls covers the loads.
-constexpr int kPfLoads = 40;  // per lane: 64 x 40 segments = 160 KB per phase at most
-template <int C, int NTC, int WL = 0, int NW = 8>
-__device__ __forceinline__ void tile_xw_prefetch(const TileDev& D, const TileState& S, int ph, int lane,
-                                                 uint32_t (&pf)[kPfLoads]) {
-  constexpr int NR = 4 + 2 * C + 1 + C;
-  uintptr_t base[NR];
-  int nseg[NR];
-#pragma unroll
-  for (int r = 0; r < NR; ++r) { base[r] = 0; nseg[r] = 0; }
-  int r = 0;
-  auto region = [&](const void* p, long long bytes, bool on) {
-    const uintptr_t b0 = reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)63;
-    const uintptr_t b1 = (reinterpret_cast<uintptr_t>(p) + (uintptr_t)bytes + 63) & ~(uintptr_t)63;
-    base[r] = b0;
-    nseg[r] = on && bytes > 0 ? (int)((b1 - b0) >> 6) : 0;
-    ++r;
-  };
-  const int K = S.K, c = ph % K, phn = ph + 1, cn = phn % K;
-  const bool more = phn < S.nph && S.bptr_s[cn] < S.bptr_s[cn + 1];
-  const int4 Bn = more ? S.batch_s[S.bptr_s[cn]] : make_int4(0, 0, 0, 0);
-  const bool rec = more && (D.pf & 2), cel = more && (D.pf & 1);
-  long long ncell = (long long)(Bn.y & 0xFFFF) * NTC;
-  int ns = Bn.z;
-  const int x0 = Bn.w;
-  if (WL && more) {  // the next colour's first round: its W wave batches are contiguous in cells and slots
-    const int lb = min(S.bptr_s[cn] + (NW - 1) - 1, S.bptr_s[cn + 1] - 1);  // NW - 1 cell waves
-    const int4 Bl = S.batch_s[lb];
-    ncell = (long long)Bl.x + (long long)(Bl.y & 0xFFFF) * 64 - Bn.x;
-    ns = Bl.w + Bl.z - x0;
-  }
-  region(D.sinfo + x0, (long long)ns * 8, rec);
-  region(D.slot_loc + x0, (long long)ns * 4, rec);
-  region(D.dr + (size_t)x0 * C, (long long)ns * C * 16, rec);
-  region(D.w_slot + (size_t)x0 * C, (long long)ns * C * 8, rec);
-  region(D.cell_pk + Bn.x, ncell * 4, cel);
-#pragma unroll
-  for (int ch = 0; ch < C; ++ch) region(D.cell_val + ch * D.n_cells + Bn.x, ncell * 8, cel);
-  const int g0 = S.gptr_s[c], g1 = S.gptr_s[c + 1];
-  const bool gh = (D.pf & 4) && g1 > g0;
-  region(D.gcell + g0, (long long)(g1 - g0) * 8, gh);
-#pragma unroll
-  for (int ch = 0; ch < C; ++ch) region(D.gval + ch * D.n_gcells + g0, (long long)(g1 - g0) * 8, gh);
-  int tot = 0;
-#pragma unroll
-  for (int q = 0; q < NR; ++q) tot += nseg[q];
-#pragma unroll
-  for (int k = 0; k < kPfLoads; ++k) {
-    const int i = k * 64 + lane;
-    pf[k] = 0u;
-    if (k * 64 < tot && i < tot) {
-      int acc = 0;
-      uintptr_t a = 0;
-#pragma unroll
-      for (int q = 0; q < NR; ++q) {
-        if (i >= acc && i < acc + nseg[q]) a = base[q] + (uintptr_t)(i - acc) * 64;
-        acc += nseg[q];
-      }
-      pf[k] = *reinterpret_cast<const uint32_t*>(a);
-    }
-  }
-}
-
 // the exchange wave's phase: its share of the colour's ghost cells (static
 // data: loaded at the phase start, long in registers when the hand-off
 // ends), the own batches' barriers, then the hand-off polls -> gdw_s, and its
@@ -1053,8 +984,6 @@ __device__ __forceinline__ void tile_phase_xw(const TileDev& D, TileState& S, in
     const int u = k * 64 + lane;
     gx[k] = u < nfi ? D.gslot[gs0 + u / C] : 0;
   }
-  uint32_t pfv[kPfLoads];
-  if (D.pf) tile_xw_prefetch<C, WL ? 64 : NT - 64, WL, NT / 64>(D, S, ph, lane, pfv);
   // the own batches' barriers (tile_own_draw: kOwnDrawBarriers each, + 1
   // before a later batch, as tile_phase_cells; wave-local batches have none)
   for (int bi = bfirst; bi < (WL ? bfirst : bend); ++bi) {
@@ -1062,10 +991,10 @@ __device__ __forceinline__ void tile_phase_xw(const TileDev& D, TileState& S, in
 #pragma unroll
     for (int q = 0; q < kOwnDrawBarriers; ++q) __syncthreads();
   }
-  if (D.pf) {  // the prefetch has landed (its registers are free again) before the polls go out
-#pragma unroll
-    for (int k = 0; k < kPfLoads; ++k) asm volatile("" ::"v"(pfv[k]));
-  }
+  // (Measured and dropped: an L2 prefetch of the next batch's records and
+  // cells and the colour's ghost cells by this wave at the phase start, one
+  // 4-B load per 64-B segment: 3,160-3,400 vs 2,275 us per 10-sweep launch at
+  // the headline -- the polls wait behind the prefetch.)
   // hand-off: every (foreign slot, chain) of colour c until its granule
   // carries this epoch -> gdw_s (polls in flight per lane; a retry waits for
   // this wave's own polls only).  (Measured and dropped: a train of 3 poll
@@ -1238,8 +1167,8 @@ __device__ __forceinline__ void sweep_tiles_body(const TileDev& D0, TileLaunch a
   const int row0 = D.erow_ptr[T], nrows = D.erow_ptr[T + 1] - row0;
   const int b_lo = D.batch_ptr[T * K], nbt = D.batch_ptr[T * K + K] - b_lo;
   S.r_s = RG ? D.rg + (size_t)row0 * C : smem;
-  S.acc_s = RG ? smem : smem + ((nrows * C + 1) / 2) * 2;  // kTSlots x C: slot totals, then dw
-  S.wsum = S.acc_s + kTSlots * C;                // NW x C: segmented wave totals
+  S.acc_s = RG ? smem : smem + ((nrows * C + 1) / 2) * 2;  // kAccSlots x C: slot totals, then dw
+  S.wsum = S.acc_s + kAccSlots * C;              // NW x C: segmented wave totals
   S.sc_s = S.wsum + NW * C;                      // C x {inv_s2, inv_t2}
   S.seed_s = reinterpret_cast<unsigned long long*>(S.sc_s + 2 * C);
   S.gdw_s = reinterpret_cast<double*>(S.seed_s + 2 * C);  // max foreign slots x C (even count)

@@ -61,8 +61,8 @@ for rep in range(reps):
                "engine": ctx.info["sweep_engine"]}
         ctx.close()
         res[name].append(out)
-        print(f"rep {rep} {name:12s} {out['chain_sweeps_s']:9.1f} chain-sweeps/s  kernel {out['kernel_us']:8.1f} us",
-              flush=True)
+        print(f"rep {rep} {name:12s} {out['chain_sweeps_s']:9.1f} chain-sweeps/s  kernel {out['kernel_us']:8.1f} us"
+              + (f"  [{out['engine']}]" if rep == 0 else ""), flush=True)
 summ = {name: {"chain_sweeps_s": [r["chain_sweeps_s"] for r in v], "kernel_us": [r["kernel_us"] for r in v]}
         for name, v in res.items()}
 print(json.dumps(summ))
