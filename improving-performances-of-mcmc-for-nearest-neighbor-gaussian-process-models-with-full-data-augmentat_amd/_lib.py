@@ -42,6 +42,7 @@ ABI_SYMBOLS = (
     "nngp_shard_ipc_handle", "nngp_shard_ipc_open", "nngp_shard_sync",
     "nngp_factor_chains", "nngp_loglik_chains", "nngp_field_response_ratio_chains",
     "nngp_sum_squared_residuals_chains", "nngp_loglik_pair_chains",
+    "nngp_ancillary_step_chains", "nngp_sufficient_step_chains",
 )
 SHARD_ID_BYTES = 128  # NNGP_SHARD_ID_BYTES
 IPC_HANDLE_BYTES = 192  # NNGP_IPC_HANDLE_BYTES
@@ -129,6 +130,8 @@ def _load():
     L.nngp_field_response_ratio_chains.argtypes = [_vp, C.c_int, _dp, _dp, _dp]
     L.nngp_sum_squared_residuals_chains.argtypes = [_vp, C.c_int, _dp, _dp]
     L.nngp_loglik_pair_chains.argtypes = [_vp, C.c_int, _dp, _dp, _dp, _dp, _dp]
+    L.nngp_ancillary_step_chains.argtypes = [_vp, C.c_int, C.c_int, _dp, C.c_int, _dp, _dp, _dp, _ip, _dp]
+    L.nngp_sufficient_step_chains.argtypes = [_vp, C.c_int, C.c_int, _dp, C.c_int, _dp, _dp, _dp, _ip, _dp, _dp]
     L.nngp_shard_ipc_handle.argtypes = [_vp, C.c_char_p, C.c_int]
     L.nngp_shard_ipc_open.argtypes = [_vp, C.c_char_p, C.c_int]
     L.nngp_shard_sync.argtypes = [_vp]

@@ -220,6 +220,29 @@ class ChainContext:
                                               self._vec(log_scale_cur), lp, lc))
         return lp, lc
 
+    def ancillary_step_chains(self, chain_mask: int, covfun: str, covparms, beta0, dlog_scale, log_noise_variance):
+        """factor_chains(1, ...) + ancillary_propose_chains +
+        field_response_ratio_chains behind one host sync -> (status, ratio);
+        a chain whose proposal factor fails: NNGP_ERR_CHOL and ratio NaN."""
+        cps = np.ascontiguousarray(np.asarray(covparms, np.float64).reshape(self.n_chains, -1))
+        st = np.zeros(self.n_chains, np.int32)
+        out = np.zeros(self.n_chains)
+        self._chk(lib.nngp_ancillary_step_chains(self._h, int(chain_mask), COVFUNS[covfun], cps.reshape(-1),
+                                                 cps.shape[1], self._vec(beta0), self._vec(dlog_scale),
+                                                 self._vec(log_noise_variance), st, out))
+        return st, out
+
+    def sufficient_step_chains(self, chain_mask: int, covfun: str, covparms, beta0, log_scale_prop, log_scale_cur):
+        """factor_chains(1, ...) + loglik_pair_chains behind one host sync ->
+        (status, ll_prop, ll_cur); a failed proposal factor: NaN values."""
+        cps = np.ascontiguousarray(np.asarray(covparms, np.float64).reshape(self.n_chains, -1))
+        st = np.zeros(self.n_chains, np.int32)
+        lp, lc = np.zeros(self.n_chains), np.zeros(self.n_chains)
+        self._chk(lib.nngp_sufficient_step_chains(self._h, int(chain_mask), COVFUNS[covfun], cps.reshape(-1),
+                                                  cps.shape[1], self._vec(beta0), self._vec(log_scale_prop),
+                                                  self._vec(log_scale_cur), st, lp, lc))
+        return st, lp, lc
+
     def field_response_ratio_chains(self, chain_mask: int, beta0, log_noise_variance) -> np.ndarray:
         out = np.zeros(self.n_chains)
         self._chk(lib.nngp_field_response_ratio_chains(self._h, int(chain_mask), self._vec(beta0),
@@ -278,7 +301,8 @@ class ChainView:
         if not callable(attr) or name in ("close", "view", "sweep_chains", "sweep_timed",
                                                      "ancillary_propose_chains", "factor_chains", "loglik_chains",
                                                      "field_response_ratio_chains", "sum_squared_residuals_chains",
-                                                     "loglik_pair_chains"):
+                                                     "loglik_pair_chains", "ancillary_step_chains",
+                                                     "sufficient_step_chains"):
             return attr
 
         def bound(*a, **kw):

@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <atomic>
 #include <mutex>
 #include <new>
 #include <string>
@@ -66,7 +67,27 @@ struct ChainState {
   bool vals_stale = false;
 };
 
+// res_d / res_h: 4 x kRowJobsMax reduction results, then the kMaxChains
+// failure flags of the factors (fail_d / fail_h)
+constexpr int kResFailOff = 4 * kRowJobsMax;
+constexpr size_t kResBytes = kResFailOff * sizeof(double) + kMaxChains * sizeof(int);
+static_assert(kResBytes % sizeof(double) == 0, "res_d holds whole doubles");
+
+// tile-engine contexts per device (persistent launches of two contexts on one
+// device must not overlap: see tile_lock)
+std::atomic<int>& tile_ctx_count(int device) {
+  static std::atomic<int> counts[64];
+  return counts[device & 63];
+}
+
 struct nngp_ctx {
+  ~nngp_ctx() {
+    if (tile_counted) tile_ctx_count(device)--;
+  }
+  bool tile_counted = false;  // counted in tile_ctx_count(device)
+  // a sweep returned without a host sync: its tile timeout word is checked
+  // after the next one (sync_stream)
+  bool tile_pending = false;
   uint64_t gen = 1;  // generation counter of ChainState::fgen / lgen
   int device = 0;
   hipStream_t st = nullptr;
@@ -83,7 +104,7 @@ struct nngp_ctx {
   int* nn_d = nullptr;       // n x b row-major, 0-based, -1 = NA
   const double** linv_cur_d = nullptr;  // C pointers: current factor of each chain
   const double** linv_cur_h = nullptr;  // pinned mirror
-  int* fail_d = nullptr;
+  int* fail_d = nullptr;         // inside res_d (kResFailOff)
   int2* sinfo_d = nullptr;       // n compact: {obs_per_loc, f0 | collen << 16}
   int* compact_loc_d = nullptr;  // n
   double2* dr_d = nullptr;
@@ -124,8 +145,8 @@ struct nngp_ctx {
   size_t z_cap = 0;
   SweepScalars* scal_d = nullptr;  // C
   SweepScalars* scal_h = nullptr;  // pinned, C
-  double* res_h = nullptr;         // pinned, 4 x kRowJobsMax doubles
-  int* fail_h = nullptr;           // pinned, kMaxChains failure rows of the factors
+  double* res_h = nullptr;         // pinned, 4 x kRowJobsMax doubles, then fail_h
+  int* fail_h = nullptr;           // pinned, kMaxChains failure rows of the factors (inside res_h)
   unsigned long long* dbg_d = nullptr;  // NNGP_PROBE=9: per-chunk timestamps
   // tile-resident sweep engine (engine == 1; graph_prep.h TileLayout)
   int engine = 0;                 // 0: colour launches, 1: tiles
@@ -246,6 +267,25 @@ hipError_t upload(T* dst, const T* src, size_t count, hipStream_t st) {
   return hipMemcpyAsync(dst, src, sizeof(T) * count, hipMemcpyHostToDevice, st);
 }
 
+static int tile_timeout_check(nngp_ctx* c) {
+  if (c->engine == 1 && c->tmo_h && *c->tmo_h != 0) {
+    *c->tmo_h = 0;
+    return fail_msg(c, NNGP_ERR_HIP, "tile sweep: neighbour wait timed out (tiles not co-resident?)");
+  }
+  return NNGP_OK;
+}
+
+// host sync of the context's stream; then the timeout word of a sweep that
+// returned without one
+int sync_stream(nngp_ctx* c) {
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  if (c->tile_pending) {
+    c->tile_pending = false;
+    return tile_timeout_check(c);
+  }
+  return NNGP_OK;
+}
+
 int set_device(nngp_ctx* c) {
   hipError_t e = hipSetDevice(c->device);
   if (e != hipSuccess) return fail_hip(c, e, "hipSetDevice");
@@ -313,14 +353,23 @@ TileDev tile_dev(nngp_ctx* c) {
   return D;
 }
 
-// chain k's current factor changed: the pointer table of captured graphs
-// now (stream order, no host buffer), the sweep values at the next reader
-// (flush_sweep_values)
+int flush_one(nngp_ctx* c, int k);
+
+// chain k's current factor changed: the pointer table of captured graphs and
+// the sweep values, now (stream order, no host buffer).  NNGP_REFRESH=deferred
+// refreshes the values at their next reader instead (flush_sweep_values: a
+// chain accepting two proposals refreshes once) -- measured slower in the
+// MCMC iteration, 1.5 refreshes of 334 us against 1.7 of 208 us: right after
+// the factor its Linv is still in the Infinity Cache.
 int refresh_sweep_values(nngp_ctx* c, int k) {
   c->linv_cur_h[k] = c->ch[k].linv_d[0];
   HIPCHK(c, launch_set_ptr(c->st, c->linv_cur_d, k, c->ch[k].linv_d[0]));
   c->ch[k].vals_stale = true;
-  return NNGP_OK;
+  static const bool deferred = [] {
+    const char* e = std::getenv("NNGP_REFRESH");
+    return e && std::string(e) == "deferred";
+  }();
+  return deferred ? NNGP_OK : flush_one(c, k);
 }
 
 // sweep values of B + precision_diag of chain k from its current factor
@@ -366,7 +415,7 @@ std::mutex& tile_lock(int device) {
 int fetch4(nngp_ctx* c, int nblocks, double out[4]) {
   HIPCHK(c, launch_reduce4(c->st, c->partials_d, nblocks, c->res_d));
   HIPCHK(c, hipMemcpyAsync(c->res_h, c->res_d, 4 * sizeof(double), hipMemcpyDeviceToHost, c->st));
-  HIPCHK(c, hipStreamSynchronize(c->st));
+  { int ss_ = sync_stream(c); if (ss_) return ss_; }
   for (int k = 0; k < 4; ++k) out[k] = c->res_h[k];
   return NNGP_OK;
 }
@@ -460,7 +509,7 @@ void nngp_ctx_destroy(nngp_ctx* c) {
   if (c->st) hipStreamSynchronize(c->st);
   for (auto& kv : c->graphs) hipGraphExecDestroy(kv.second);
   for (auto g : c->graph_objs) hipGraphDestroy(g);
-  std::vector<void*> ptrs = {c->locs_d, c->sc_d, c->nn_d, c->linv_cur_d, c->fail_d, c->sinfo_d, c->compact_loc_d,
+  std::vector<void*> ptrs = {c->locs_d, c->sc_d, c->nn_d, c->linv_cur_d, c->sinfo_d, c->compact_loc_d,
                              c->dr_d, c->slot_dpos_d, c->ent_pk_d, c->ent_src_d, c->ent_val_d, c->w_slot_d,
                              c->r_d, c->level_rows_d, c->obs_ptr_d, c->obs_idx_d, c->lm_d, c->y_d, c->tmp_d,
                              c->tmp2_d, c->partials_d, c->res_d, c->z_d, c->scal_d, c->dbg_d,
@@ -489,7 +538,6 @@ void nngp_ctx_destroy(nngp_ctx* c) {
   for (void* p : ptrs) if (p) hipFree(p);
   if (c->scal_h) hipHostFree(c->scal_h);
   if (c->res_h) hipHostFree(c->res_h);
-  if (c->fail_h) hipHostFree(c->fail_h);
   if (c->linv_cur_h) hipHostFree(c->linv_cur_h);
   if (c->stage_h) hipHostFree(c->stage_h);
   if (c->mu_stage_h) hipHostFree(c->mu_stage_h);
@@ -640,7 +688,9 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       // chain
       const char* twl = std::getenv("NNGP_TILE_WL");
       const bool wl_env = twl ? std::string(twl) == "1" : n_chains >= 3;
-      const bool xw = !csplit && !split && (!rg_forced || wl_env) && NT == 512 && xwm == 1;
+      // interior-first layouts run on wave-local batches (tiles.hip
+      // tile_phase_wlib) or, without the exchange wave, on workgroup batches
+      const bool xw = !csplit && (!split || wl_env) && (!rg_forced || wl_env) && NT == 512 && xwm == 1;
       const bool wl = xw && wl_env;
       const int NTL = wl ? 64 : (xw ? NT - 64 : NT);  // the layout's cell threads of a batch
       if (const char* bc = std::getenv("NNGP_TILE_BATCH_CELLS"))
@@ -740,12 +790,21 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       if (ok) {
         c->engine = 1;
         {
+          // a sweep of another tile context of this device may still be in
+          // flight (it returned without a sync while it was the only one):
+          // drain it before two contexts can launch
+          std::lock_guard<std::mutex> lk(tile_lock(device));
+          if (tile_ctx_count(device)++ > 0) (void)hipDeviceSynchronize();
+        }
+        c->tile_counted = true;
+        {
           const char* sw = std::getenv("NNGP_SWEEP_WARM");
           c->warm_on = shard_G == 0 && !(sw && std::string(sw) == "0");
         }
         c->engine_note = "tiles: " + std::to_string(T) + " tiles of " + std::to_string(NT) + " threads, " +
                          std::to_string(c->tresident) + " resident per CU x " + std::to_string(cus) + " CUs" +
                          (c->rglobal ? ", r in global memory" : "") + (c->txw == 2 ? ", exchange wave, wave-local batches" : c->txw ? ", exchange wave" : "") +
+                         (c->tl.split ? ", interior first" : "") +
                          (c->tcs ? ", chain-split" : "");
         if (shard_G > 0) {
           c->shard = true;
@@ -844,7 +903,6 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
   CK(dalloc(&c->linv_cur_d, C));
   CK(hipHostMalloc((void**)&c->linv_cur_h, sizeof(double*) * C, hipHostMallocDefault));
   for (int k = 0; k < C; ++k) c->linv_cur_h[k] = c->ch[k].linv_d[0];
-  CK(dalloc(&c->fail_d, kMaxChains));
   CK(dalloc(&c->sinfo_d, NS));
   CK(dalloc(&c->compact_loc_d, NS));
   CK(dalloc(&c->dr_d, NS * C));
@@ -994,12 +1052,15 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
   CK(dalloc(&c->tmp_d, (size_t)n * C));   // scratch vectors, chain-strided for batched solves
   CK(dalloc(&c->tmp2_d, (size_t)n * C));
   CK(dalloc(&c->partials_d, 4 * kRedBlocks * kRowJobsMax));
-  CK(dalloc(&c->res_d, 4 * kRowJobsMax));
+  // the factors' failure flags sit right after the reductions' results, so
+  // one copy brings both to the host (kResFailOff doubles in)
+  CK(dalloc(&c->res_d, kResBytes / sizeof(double)));
+  c->fail_d = reinterpret_cast<int*>(c->res_d + kResFailOff);
   CK(dalloc(&c->scal_d, C));
   CK(hipHostMalloc((void**)&c->scal_h, sizeof(SweepScalars) * C, hipHostMallocDefault));
   std::memset(c->scal_h, 0, sizeof(SweepScalars) * C);
-  CK(hipHostMalloc((void**)&c->res_h, 4 * kRowJobsMax * sizeof(double), hipHostMallocDefault));
-  CK(hipHostMalloc((void**)&c->fail_h, kMaxChains * sizeof(int), hipHostMallocDefault));
+  CK(hipHostMalloc((void**)&c->res_h, kResBytes, hipHostMallocDefault));
+  c->fail_h = reinterpret_cast<int*>(c->res_h + kResFailOff);
   CK(upload(c->locs_d, locs_rm.data(), locs_rm.size(), c->st));
   CK(upload(c->nn_d, nn_dev.data(), nn_dev.size(), c->st));
   {
@@ -1195,7 +1256,7 @@ static int factor_enqueue(nngp_ctx* c, int k, int which, int covfun, const doubl
   const bool sphere = covfun == NNGP_EXPONENTIAL_SPHERE || covfun == NNGP_MATERN_SPHERE;
   if (sphere && c->ds < 3) {
     // sphere on d == 2: scaled coordinates are 3-D; grow the buffer once
-    HIPCHK(c, hipStreamSynchronize(c->st));
+    { int ss_ = sync_stream(c); if (ss_) return ss_; }
     hipFree(c->sc_d);
     c->sc_d = nullptr;
     HIPCHK(c, dalloc(&c->sc_d, (size_t)c->n * 4));
@@ -1212,10 +1273,9 @@ static int factor_enqueue(nngp_ctx* c, int k, int which, int covfun, const doubl
   return NNGP_OK;
 }
 
-// after factor_enqueue of the chains in mask: one copy of the flags, one sync
-static int factor_collect(nngp_ctx* c, int which, int mask, int* status) {
-  HIPCHK(c, hipMemcpyAsync(c->fail_h, c->fail_d, sizeof(int) * c->C, hipMemcpyDeviceToHost, c->st));
-  HIPCHK(c, hipStreamSynchronize(c->st));
+// after factor_enqueue of the chains in mask and a host sync that followed
+// the copy of the flags into fail_h: per-chain outcomes
+static int factor_outcomes(nngp_ctx* c, int which, int mask, int* status) {
   int rc = NNGP_OK;
   for (int k = 0; k < c->C; ++k) {
     if (!((mask >> k) & 1)) continue;
@@ -1238,6 +1298,13 @@ static int factor_collect(nngp_ctx* c, int which, int mask, int* status) {
     }
   }
   return rc;
+}
+
+// after factor_enqueue of the chains in mask: one copy of the flags, one sync
+static int factor_collect(nngp_ctx* c, int which, int mask, int* status) {
+  HIPCHK(c, hipMemcpyAsync(c->fail_h, c->fail_d, sizeof(int) * c->C, hipMemcpyDeviceToHost, c->st));
+  { int ss_ = sync_stream(c); if (ss_) return ss_; }
+  return factor_outcomes(c, which, mask, status);
 }
 
 int nngp_factor(nngp_ctx* c, int which, int covfun, const double* cp, int ncp) {
@@ -1269,7 +1336,7 @@ int nngp_get_linv(nngp_ctx* c, int which, double* Linv) {
   if ((rc = set_device(c))) return rc;
   std::vector<double> rm((size_t)c->n * c->b);
   HIPCHK(c, hipMemcpyAsync(rm.data(), S.linv_d[which], rm.size() * sizeof(double), hipMemcpyDeviceToHost, c->st));
-  HIPCHK(c, hipStreamSynchronize(c->st));
+  { int ss_ = sync_stream(c); if (ss_) return ss_; }
   for (int i = 0; i < c->n; ++i)
     for (int j = 0; j < c->b; ++j) Linv[i + (size_t)j * c->n] = rm[(size_t)c->dpos[i] * c->b + j];
   return NNGP_OK;
@@ -1285,7 +1352,7 @@ int nngp_set_linv(nngp_ctx* c, int which, const double* Linv) {
     for (int j = 0; j < c->b; ++j) rm[(size_t)c->dpos[i] * c->b + j] = Linv[i + (size_t)j * c->n];
   S.lgen[which] = ++c->gen;
   HIPCHK(c, hipMemcpyAsync(S.linv_d[which], rm.data(), rm.size() * sizeof(double), hipMemcpyHostToDevice, c->st));
-  HIPCHK(c, hipStreamSynchronize(c->st));
+  { int ss_ = sync_stream(c); if (ss_) return ss_; }
   S.have_factor[which] = true;
   if (which == 0) return refresh_sweep_values(c, c->cur);
   return NNGP_OK;
@@ -1312,7 +1379,7 @@ int nngp_get_precision_diag(nngp_ctx* c, double* D) {
   if ((rc = flush_sweep_values(c, 1 << c->cur))) return rc;
   std::vector<double2> dr((size_t)c->n * c->C);
   HIPCHK(c, hipMemcpyAsync(dr.data(), c->dr_d, dr.size() * sizeof(double2), hipMemcpyDeviceToHost, c->st));
-  HIPCHK(c, hipStreamSynchronize(c->st));
+  { int ss_ = sync_stream(c); if (ss_) return ss_; }
   for (int x = 0; x < c->n; ++x) D[c->lay.compact_loc[x]] = dr[(size_t)x * c->C + c->cur].x;
   return NNGP_OK;
 }
@@ -1324,14 +1391,14 @@ static int upload_field(nngp_ctx* c, const double* host, double* dev) {
   std::memcpy(c->stage_h, host, sizeof(double) * c->n);
   HIPCHK(c, hipMemcpyAsync(c->perm_d, c->stage_h, c->n * sizeof(double), hipMemcpyHostToDevice, c->st));
   HIPCHK(c, launch_permute_scatter(c->st, c->n, c->dpos_d, c->perm_d, dev));
-  HIPCHK(c, hipStreamSynchronize(c->st));
+  { int ss_ = sync_stream(c); if (ss_) return ss_; }
   return NNGP_OK;
 }
 
 static int download_field(nngp_ctx* c, const double* dev, double* host) {
   HIPCHK(c, launch_permute_gather(c->st, c->n, c->dpos_d, dev, c->perm_d));
   HIPCHK(c, hipMemcpyAsync(c->stage_h, c->perm_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
-  HIPCHK(c, hipStreamSynchronize(c->st));
+  { int ss_ = sync_stream(c); if (ss_) return ss_; }
   std::memcpy(host, c->stage_h, sizeof(double) * c->n);
   return NNGP_OK;
 }
@@ -1366,7 +1433,7 @@ int nngp_records_reserve(nngp_ctx* c, int n_rows) {
   ChainState& S = c->ch[c->cur];
   if (n_rows == S.rec_rows && (S.rec_d || n_rows == 0)) return NNGP_OK;
   if (S.rec_d) {
-    HIPCHK(c, hipStreamSynchronize(c->st));
+    { int ss_ = sync_stream(c); if (ss_) return ss_; }
     hipFree(S.rec_d);
   }
   S.rec_d = nullptr;
@@ -1401,7 +1468,7 @@ int nngp_get_records(nngp_ctx* c, int row0, int n_rows, double* out) {
   if (n_rows == 0) return NNGP_OK;
   int rc;
   if ((rc = set_device(c))) return rc;
-  HIPCHK(c, hipStreamSynchronize(c->st));
+  { int ss_ = sync_stream(c); if (ss_) return ss_; }
   HIPCHK(c, hipMemcpy(out, S.rec_d + (size_t)row0 * c->n, sizeof(double) * (size_t)n_rows * c->n, hipMemcpyDeviceToHost));
   return NNGP_OK;
 }
@@ -1457,47 +1524,86 @@ int nngp_loglik(nngp_ctx* c, int which, double beta0, double log_scale, double* 
 // (NNarray read once): per job exactly the single-job arithmetic, so any
 // grouping of jobs gives the same bits.  The factors' log-determinant and
 // row-statistics caches are updated in job order.
-struct LLJob { int k, which; double beta0, log_scale; double* out; };
+struct LLJob {
+  int k, which;
+  double beta0, log_scale;
+  double* out;
+  bool cached = false;  // set at enqueue: the factor's log-determinant was cached (the pass skips the logs)
+  double ld = 0.0;
+};
 
-static int loglik_jobs(nngp_ctx* c, const LLJob* jobs, int nj) {
-  { int rs_ = replica_fresh(c); if (rs_) return rs_; }
-  int rc;
-  if ((rc = set_device(c))) return rc;
+static int loglik_jobs_enqueue(nngp_ctx* c, LLJob* jobs, int nj, bool copy = true) {
   if (nj < 1 || nj > kRowJobsMax) return fail_msg(c, NNGP_ERR_ARG, "loglik: too many jobs");
-  RowJobs J;
   for (int j = 0; j < nj; ++j) {
-    ChainState& S = c->ch[jobs[j].k];
-    const int which = jobs[j].which;
-    if (!S.have_factor[which] || !S.have_field) return fail_msg(c, NNGP_ERR_STATE, "loglik: need factor and field");
-    J.linv[J.M] = S.linv_d[which];
-    J.x[J.M] = S.field_d;
-    J.shift[J.M] = jobs[j].beta0;
-    J.out[J.M] = nullptr;
-    J.res_slot[J.M] = j;
-    J.mode[J.M] = 1;
-    for (const ChainState::LogDet& e : S.ld)
-      if (e.lg == S.lgen[which]) J.mode[J.M] = 2;
-    ++J.M;
+    const ChainState& S = c->ch[jobs[j].k];
+    if (!S.have_factor[jobs[j].which] || !S.have_field)
+      return fail_msg(c, NNGP_ERR_STATE, "loglik: need factor and field");
   }
-  const int nb = launch_row_stats_jobs(c->st, J, c->nn_d, c->n, c->b, c->partials_d);
-  HIPCHK(c, hipGetLastError());
-  HIPCHK(c, launch_reduce4_jobs(c->st, J, c->partials_d, nb, c->res_d));
-  HIPCHK(c, hipMemcpyAsync(c->res_h, c->res_d, 4 * nj * sizeof(double), hipMemcpyDeviceToHost, c->st));
-  HIPCHK(c, hipStreamSynchronize(c->st));
+  // passes of at most kPassJobs jobs: the row-statistics kernel's registers
+  // grow with the jobs (3: 127 VGPRs, 4 waves per SIMD; 6: 227, 2 waves) and
+  // two 3-job passes (2 x 225 us at n = 1e6, b = 16) beat one 6-job pass
+  // (774 us).  Each job's arithmetic is the one-job kernel's in any grouping.
+  constexpr int kPassJobs = 3;
+  for (int j0 = 0; j0 < nj; j0 += kPassJobs) {
+    RowJobs J;
+    for (int j = j0; j < nj && j < j0 + kPassJobs; ++j) {
+      ChainState& S = c->ch[jobs[j].k];
+      const int which = jobs[j].which;
+      J.linv[J.M] = S.linv_d[which];
+      J.x[J.M] = S.field_d;
+      J.shift[J.M] = jobs[j].beta0;
+      J.out[J.M] = nullptr;
+      J.res_slot[J.M] = j;
+      J.mode[J.M] = 1;
+      jobs[j].cached = false;
+      for (const ChainState::LogDet& e : S.ld)
+        if (e.lg == S.lgen[which]) {
+          J.mode[J.M] = 2;
+          jobs[j].cached = true;
+          jobs[j].ld = e.v;
+        }
+      ++J.M;
+    }
+    const int nb = launch_row_stats_jobs(c->st, J, c->nn_d, c->n, c->b, c->partials_d);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, launch_reduce4_jobs(c->st, J, c->partials_d, nb, c->res_d));
+  }
+  if (copy) HIPCHK(c, hipMemcpyAsync(c->res_h, c->res_d, 4 * nj * sizeof(double), hipMemcpyDeviceToHost, c->st));
+  return NNGP_OK;
+}
+
+// after the sync: the jobs' values and the caches (jobs of chains in `skip`
+// -- a proposal factor that failed -- neither answer nor touch the caches)
+static void loglik_jobs_finish(nngp_ctx* c, const LLJob* jobs, int nj, int skip = 0) {
   for (int j = 0; j < nj; ++j) {
     const int k = jobs[j].k, which = jobs[j].which;
+    if ((skip >> k) & 1) {
+      *jobs[j].out = std::nan("");
+      continue;
+    }
     ChainState& S = c->ch[k];
     double* r = c->res_h + 4 * j;
-    bool cached = false;
-    for (const ChainState::LogDet& e : S.ld)
-      if (e.lg == S.lgen[which]) { r[0] = e.v; cached = true; }
-    if (!cached) {
+    // the cache as the pass saw it at enqueue (an earlier job of this pass may
+    // have evicted the entry since)
+    if (jobs[j].cached) r[0] = jobs[j].ld;
+    bool present = false;
+    for (const ChainState::LogDet& e : S.ld) present |= e.lg == S.lgen[which];
+    if (!present) {  // (re-)insert: the cache ends as after one call per job
       S.ld[S.ld_next] = {S.lgen[which], r[0]};
       S.ld_next ^= 1;
     }
     *jobs[j].out = r[0] - c->n * 0.5 * jobs[j].log_scale - 0.5 * r[1] / std::exp(jobs[j].log_scale);
     rowstats_store(c, k, which, jobs[j].beta0, r);
   }
+}
+
+static int loglik_jobs(nngp_ctx* c, LLJob* jobs, int nj) {
+  { int rs_ = replica_fresh(c); if (rs_) return rs_; }
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  if ((rc = loglik_jobs_enqueue(c, jobs, nj))) return rc;
+  { int ss_ = sync_stream(c); if (ss_) return ss_; }
+  loglik_jobs_finish(c, jobs, nj);
   return NNGP_OK;
 }
 
@@ -1561,13 +1667,7 @@ static void fields_written(nngp_ctx* c, int mask) {
 }
 
 // the tile engine's bounded spins set a timeout word instead of hanging
-static int tile_timeout_check(nngp_ctx* c) {
-  if (c->engine == 1 && c->tmo_h && *c->tmo_h != 0) {
-    *c->tmo_h = 0;
-    return fail_msg(c, NNGP_ERR_HIP, "tile sweep: neighbour wait timed out (tiles not co-resident?)");
-  }
-  return NNGP_OK;
-}
+
 
 static int upload_scalars(nngp_ctx* c) {
   HIPCHK(c, hipMemcpyAsync(c->scal_d, c->scal_h, sizeof(SweepScalars) * c->C, hipMemcpyHostToDevice, c->st));
@@ -1681,6 +1781,14 @@ static void warm_set(nngp_ctx* c, int mask, const double* beta0) {
   }
 }
 
+// A sweep call returns without a host sync (stream-ordered, like the other
+// calls; its tile timeout word is checked after the next sync) unless another
+// tile context shares the device -- then the call holds the device's tile
+// lock until its launch has drained (tile_lock) -- or a probe buffer is read.
+static bool sweep_async(const nngp_ctx* c) {
+  return (c->engine != 1 || tile_ctx_count(c->device) == 1) && !c->tdbg_d && !c->dbg_d;
+}
+
 int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double lnv, uint64_t seed,
                uint64_t counter_base, const double* z) {
   if (!c || n_sweeps < 0) return NNGP_ERR_ARG;
@@ -1699,8 +1807,11 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
     if (z) return fail_msg(c, NNGP_ERR_ARG, "sweep: injected normals are not supported on shard contexts");
     return shard_call(c, n_sweeps, mask);
   }
+  // the device's tile lock around the launch (and, unless the call returns
+  // without a sync, until it has drained)
   std::unique_lock<std::mutex> tlk;
   if (c->engine == 1) tlk = std::unique_lock<std::mutex>(tile_lock(c->device));
+  const bool async = sweep_async(c) && !z;
   if (z) {
     // injected normals -> compact order, chain-interleaved
     const size_t need = (size_t)n_sweeps * c->C * c->n;
@@ -1716,7 +1827,7 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
       for (int i = 0; i < c->n; ++i)
         zc[((size_t)s * c->n + c->loc_rank[i]) * c->C + k] = z[(size_t)s * c->n + i];
     HIPCHK(c, hipMemcpyAsync(c->z_d, zc.data(), need * sizeof(double), hipMemcpyHostToDevice, c->st));
-    HIPCHK(c, hipStreamSynchronize(c->st));
+    { int ss_ = sync_stream(c); if (ss_) return ss_; }
     if ((rc = enqueue_sweep_body(c, n_sweeps, mask, c->z_d))) return rc;
   } else {
     // replay a captured graph of the whole call (launch-bound at small n)
@@ -1724,8 +1835,13 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
     if ((rc = graph_for(c, n_sweeps, mask, &ex, warm ? kColours | kEpilogue : kAll))) return rc;
     HIPCHK(c, hipGraphLaunch(ex, c->st));
   }
-  HIPCHK(c, hipStreamSynchronize(c->st));
-  if ((rc = tile_timeout_check(c))) return rc;
+  if (async) {
+    c->tile_pending = c->engine == 1;
+    if (tlk.owns_lock()) tlk.unlock();
+  } else {
+    { int ss_ = sync_stream(c); if (ss_) return ss_; }
+    if ((rc = tile_timeout_check(c))) return rc;
+  }
   warm_set(c, mask, b0v);
   return NNGP_OK;
 }
@@ -1744,14 +1860,22 @@ int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const doub
   if ((rc = flush_sweep_values(c, all))) return rc;
   if ((rc = upload_scalars(c))) return rc;
   if (sharded_call(c)) return shard_call(c, n_sweeps, all);
+  // the device's tile lock around the launch (and, unless the call returns
+  // without a sync, until it has drained)
   std::unique_lock<std::mutex> tlk;
   if (c->engine == 1) tlk = std::unique_lock<std::mutex>(tile_lock(c->device));
+  const bool async = sweep_async(c);
   hipGraphExec_t ex;
   if ((rc = graph_for(c, n_sweeps, all, &ex, warm ? kColours | kEpilogue : kAll))) return rc;
   HIPCHK(c, hipGraphLaunch(ex, c->st));
-  HIPCHK(c, hipStreamSynchronize(c->st));
-  tlk = std::unique_lock<std::mutex>();
-  if ((rc = tile_timeout_check(c))) return rc;
+  if (async) {
+    c->tile_pending = c->engine == 1;
+    if (tlk.owns_lock()) tlk.unlock();
+  } else {
+    { int ss_ = sync_stream(c); if (ss_) return ss_; }
+    tlk = std::unique_lock<std::mutex>();
+    if ((rc = tile_timeout_check(c))) return rc;
+  }
   warm_set(c, all, beta0);
   if (c->tdbg_d) {
     if (const char* path = std::getenv("NNGP_DBG_OUT")) {
@@ -1904,7 +2028,7 @@ static int replica_sync(nngp_ctx* c) {
   const int mask = c->stale_mask;
   if ((rc = tile_ipc_exchange(c, true))) return rc;
   if ((rc = enqueue_sweep_body(c, 1, mask, nullptr, 4))) return rc;  // kEpilogue
-  HIPCHK(c, hipStreamSynchronize(c->st));
+  { int ss_ = sync_stream(c); if (ss_) return ss_; }
   c->stale_mask = 0;
   return tile_timeout_check(c);
 }
@@ -1983,7 +2107,7 @@ static int tile_shard_call(nngp_ctx* c, int n_sweeps, int mask) {
     return e != hipSuccess ? fail_hip(c, e, "tile shard launch") : rc;
   }
   if ((rc = enqueue_sweep_body(c, n_sweeps, mask, nullptr, kEpilogue))) return rc;
-  HIPCHK(c, hipStreamSynchronize(c->st));
+  { int ss_ = sync_stream(c); if (ss_) return ss_; }
   if (!c->comm) c->stale_mask |= mask;
   return tile_timeout_check(c);
 }
@@ -2062,7 +2186,7 @@ static int shard_call(nngp_ctx* c, int n_sweeps, int mask) {
       }
     }
   if ((rc = enqueue_sweep_body(c, n_sweeps, mask, nullptr, kEpilogue))) return rc;
-  HIPCHK(c, hipStreamSynchronize(c->st));
+  { int ss_ = sync_stream(c); if (ss_) return ss_; }
   return NNGP_OK;
 }
 
@@ -2321,7 +2445,7 @@ int nngp_sweep_timed(nngp_ctx* c, int n_sweeps, const double* beta0, const doubl
   HIPCHK(c, hipEventRecord(e[2], c->st));
   HIPCHK(c, hipGraphLaunch(epi, c->st));
   HIPCHK(c, hipEventRecord(e[3], c->st));
-  HIPCHK(c, hipStreamSynchronize(c->st));
+  { int ss_ = sync_stream(c); if (ss_) return ss_; }
   float f = 0, g = 0;
   HIPCHK(c, hipEventElapsedTime(&f, e[0], e[3]));
   HIPCHK(c, hipEventElapsedTime(&g, e[1], e[2]));
@@ -2339,7 +2463,7 @@ int nngp_get_sweep_r(nngp_ctx* c, double* r) {
   if ((rc = set_device(c))) return rc;
   std::vector<double> h((size_t)c->n * c->C);
   HIPCHK(c, hipMemcpyAsync(h.data(), c->r_d, h.size() * sizeof(double), hipMemcpyDeviceToHost, c->st));
-  HIPCHK(c, hipStreamSynchronize(c->st));
+  { int ss_ = sync_stream(c); if (ss_) return ss_; }
   for (int i = 0; i < c->n; ++i) r[i] = h[(size_t)c->dpos[i] * c->C + c->cur];
   return NNGP_OK;
 }
@@ -2454,17 +2578,24 @@ static int obs_enqueue(nngp_ctx* c, int k, int mode, double beta0, double lnv) {
   return NNGP_OK;
 }
 
+static int obs_chains_enqueue(nngp_ctx* c, int mode, int chain_mask, const double* beta0, const double* lnv,
+                              bool copy = true) {
+  int rc;
+  for (int k = 0; k < c->C; ++k)
+    if ((chain_mask >> k) & 1)
+      if ((rc = obs_enqueue(c, k, mode, beta0[k], mode == 1 ? lnv[k] : 0.0))) return rc;
+  if (copy) HIPCHK(c, hipMemcpyAsync(c->res_h, c->res_d, 4 * c->C * sizeof(double), hipMemcpyDeviceToHost, c->st));
+  return NNGP_OK;
+}
+
 static int obs_chains(nngp_ctx* c, int mode, int chain_mask, const double* beta0, const double* lnv, double* out) {
   if (!c || !out || !beta0 || (mode == 1 && !lnv) || chain_mask <= 0 || chain_mask >= (1 << c->C))
     return NNGP_ERR_ARG;
   { int rs_ = replica_fresh(c); if (rs_) return rs_; }
   int rc;
   if ((rc = set_device(c))) return rc;
-  for (int k = 0; k < c->C; ++k)
-    if ((chain_mask >> k) & 1)
-      if ((rc = obs_enqueue(c, k, mode, beta0[k], mode == 1 ? lnv[k] : 0.0))) return rc;
-  HIPCHK(c, hipMemcpyAsync(c->res_h, c->res_d, 4 * c->C * sizeof(double), hipMemcpyDeviceToHost, c->st));
-  HIPCHK(c, hipStreamSynchronize(c->st));
+  if ((rc = obs_chains_enqueue(c, mode, chain_mask, beta0, lnv))) return rc;
+  { int ss_ = sync_stream(c); if (ss_) return ss_; }
   if ((rc = tri_timeout_check(c))) return rc;  // the proposal field of a ratio comes from the solve
   for (int k = 0; k < c->C; ++k)
     if ((chain_mask >> k) & 1) out[k] = c->res_h[4 * k];
@@ -2484,6 +2615,90 @@ int nngp_field_response_ratio(nngp_ctx* c, double beta0, double lnv, double* rat
 int nngp_field_response_ratio_chains(nngp_ctx* c, int chain_mask, const double* beta0, const double* lnv,
                                      double* ratio) {
   return obs_chains(c, 1, chain_mask, beta0, lnv, ratio);
+}
+
+// ---------------------------------------------------------------- MH steps
+// A covariance proposal's factor and what its Metropolis-Hastings step
+// computes with it, behind ONE host sync (the separate calls take two or
+// three): the factors, then the step's reductions, are enqueued for every
+// chain in the mask before the outcome of any factor is known; one copy
+// brings the failure flags and the results back.  A chain whose proposal
+// factor fails reports NNGP_ERR_CHOL and NaN results (what its step computed
+// from that factor is discarded, and the caches do not see it); every other
+// chain gets exactly the bits of the separate calls.
+
+static int step_common(nngp_ctx* c, int chain_mask, int covfun, const double* covparms, int ncp, bool need_mu,
+                       const char* what) {
+  { int rs_ = replica_fresh(c); if (rs_) return rs_; }
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  for (int k = 0; k < c->C; ++k) {
+    if (!((chain_mask >> k) & 1)) continue;
+    const ChainState& S = c->ch[k];
+    if (!S.have_factor[0] || !S.have_field || (need_mu && !S.have_mu)) {
+      char buf[128];
+      std::snprintf(buf, sizeof buf, "%s: chain %d needs its current factor, the field%s", what, k,
+                    need_mu ? " and mu" : "");
+      return fail_msg(c, NNGP_ERR_STATE, buf);
+    }
+  }
+  for (int k = 0; k < c->C; ++k)
+    if ((chain_mask >> k) & 1)
+      if ((rc = factor_enqueue(c, k, 1, covfun, covparms + (size_t)k * ncp, ncp))) return rc;
+  // provisional until the flags are back (factor_outcomes settles it)
+  for (int k = 0; k < c->C; ++k)
+    if ((chain_mask >> k) & 1) c->ch[k].have_factor[1] = true;
+  return NNGP_OK;
+}
+
+static int step_collect(nngp_ctx* c, int chain_mask, int* status, int* failed) {
+  HIPCHK(c, hipMemcpyAsync(c->res_h, c->res_d, kResBytes, hipMemcpyDeviceToHost, c->st));
+  { int ss_ = sync_stream(c); if (ss_) return ss_; }
+  int rc;
+  if ((rc = tri_timeout_check(c))) return rc;
+  rc = factor_outcomes(c, 1, chain_mask, status);
+  if (rc && rc != NNGP_ERR_CHOL) return rc;
+  *failed = 0;
+  for (int k = 0; k < c->C; ++k)
+    if (((chain_mask >> k) & 1) && status[k] != NNGP_OK) *failed |= 1 << k;
+  return NNGP_OK;
+}
+
+int nngp_ancillary_step_chains(nngp_ctx* c, int chain_mask, int covfun, const double* covparms, int ncp,
+                               const double* beta0, const double* dlog_scale, const double* lnv, int* status,
+                               double* ratio) {
+  if (!c || !covparms || !beta0 || !dlog_scale || !lnv || !status || !ratio || chain_mask <= 0 ||
+      chain_mask >= (1 << c->C))
+    return fail_msg(c, NNGP_ERR_ARG, "ancillary_step_chains: bad args");
+  int rc, failed = 0;
+  if ((rc = step_common(c, chain_mask, covfun, covparms, ncp, true, "ancillary_step_chains"))) return rc;
+  if ((rc = nngp_ancillary_propose_chains(c, chain_mask, beta0, dlog_scale))) return rc;
+  if ((rc = obs_chains_enqueue(c, 1, chain_mask, beta0, lnv, false))) return rc;
+  if ((rc = step_collect(c, chain_mask, status, &failed))) return rc;
+  for (int k = 0; k < c->C; ++k)
+    if ((chain_mask >> k) & 1) ratio[k] = ((failed >> k) & 1) ? std::nan("") : c->res_h[4 * k];
+  return NNGP_OK;
+}
+
+int nngp_sufficient_step_chains(nngp_ctx* c, int chain_mask, int covfun, const double* covparms, int ncp,
+                                const double* beta0, const double* log_scale_prop, const double* log_scale_cur,
+                                int* status, double* ll_prop, double* ll_cur) {
+  if (!c || !covparms || !beta0 || !log_scale_prop || !log_scale_cur || !status || !ll_prop || !ll_cur ||
+      chain_mask <= 0 || chain_mask >= (1 << c->C))
+    return fail_msg(c, NNGP_ERR_ARG, "sufficient_step_chains: bad args");
+  int rc, failed = 0;
+  if ((rc = step_common(c, chain_mask, covfun, covparms, ncp, false, "sufficient_step_chains"))) return rc;
+  // nngp_loglik_pair_chains' jobs: the proposals first, then the current factors
+  LLJob jobs[kRowJobsMax];
+  int nj = 0;
+  for (int k = 0; k < c->C; ++k)
+    if ((chain_mask >> k) & 1) jobs[nj++] = {k, 1, beta0[k], log_scale_prop[k], ll_prop + k};
+  for (int k = 0; k < c->C; ++k)
+    if ((chain_mask >> k) & 1) jobs[nj++] = {k, 0, beta0[k], log_scale_cur[k], ll_cur + k};
+  if ((rc = loglik_jobs_enqueue(c, jobs, nj, false))) return rc;
+  if ((rc = step_collect(c, chain_mask, status, &failed))) return rc;
+  loglik_jobs_finish(c, jobs, nj, failed);
+  return NNGP_OK;
 }
 
 int nngp_accept_field(nngp_ctx* c) {
@@ -2547,7 +2762,7 @@ int nngp_spmv(nngp_ctx* c, int which, const double* X, int ncols, double* Y) {
     launch_row_stats(c->st, S.linv_d[which], c->nn_d, c->n, c->b, c->tmp2_d, 0.0, c->tmp_d, c->partials_d);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(outv.data(), c->tmp_d, c->n * sizeof(double), hipMemcpyDeviceToHost, c->st));
-    HIPCHK(c, hipStreamSynchronize(c->st));
+    { int ss_ = sync_stream(c); if (ss_) return ss_; }
     for (int i = 0; i < c->n; ++i) Y[(size_t)col * c->n + i] = outv[c->dpos[i]];
   }
   return NNGP_OK;

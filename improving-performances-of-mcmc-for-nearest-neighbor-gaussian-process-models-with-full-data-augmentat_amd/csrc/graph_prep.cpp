@@ -547,8 +547,8 @@ bool build_tile_layout(const int* nn, int n, int b, const int* colors, const dou
   L = TileLayout();
   L.n = n; L.b = b; L.NT = NT; L.RMAX = RMAX; L.W = waves;
   if (NT < 64 || NT > 1024 || RMAX < 1 || (long long)NT * RMAX > (1 << 20)) { err = "tile layout: bad NT/RMAX"; return false; }
-  if (waves < 0 || (waves > 0 && (NT != 64 || split || waves * kWaveSlotsMax > kAccSlots))) {
-    err = "tile layout: wave-local batches need NT = 64, no split, waves x kWaveSlotsMax <= kAccSlots";
+  if (waves < 0 || (waves > 0 && (NT != 64 || waves * kWaveSlotsMax > kAccSlots))) {
+    err = "tile layout: wave-local batches need NT = 64 and waves x kWaveSlotsMax <= kAccSlots";
     return false;
   }
   if (T < 1) T = 1;

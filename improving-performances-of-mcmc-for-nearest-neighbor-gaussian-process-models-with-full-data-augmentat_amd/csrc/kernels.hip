@@ -163,10 +163,13 @@ __device__ __forceinline__ double exp_nonpos(double x, const double* tab) {
   return __builtin_ldexp(__builtin_fma(p * r, t, t), ki >> 6);
 }
 
-// sqrt(s) for normal s > 0 (squared distances): hardware rsq (~2^-24) and
-// two residual corrections; correctly rounded on every sample measured.
+// sqrt(s) for s >= 0 (squared distances): hardware rsq (~2^-24) and two
+// residual corrections; correctly rounded on every sample measured.  The
+// rsq argument is floored at 1e-300 so that coinciding points (s = 0, whose
+// correlation is 1: a PD local covariance with a nugget) give exactly 0
+// instead of 0 x inf.
 __device__ __forceinline__ double sqrt_pos(double s) {
-  const double y = __builtin_amdgcn_rsq(s);
+  const double y = __builtin_amdgcn_rsq(__builtin_fmax(s, 1e-300));
   const double h = 0.5 * y;
   double g = s * y;
   double e = __builtin_fma(-g, g, s);

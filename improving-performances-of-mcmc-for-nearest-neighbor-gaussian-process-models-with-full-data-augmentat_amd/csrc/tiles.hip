@@ -950,6 +950,106 @@ __device__ __forceinline__ void tile_phase_wl(const TileDev& D, const TileLaunch
   TLSTAMP(S, 3);
 }
 
+// Wave-local batches on an interior-first layout (IB with XW == 2;
+// TileLayout::split): per colour c, each cell wave first runs its batches of
+// c's interior slots -- no row of their columns waits for a draw of colour
+// c-1 in another tile -- while the exchange wave is still polling colour
+// c-1's granules; then (barrier A) colour c-1's ghost adds (barrier B); then
+// its batches of c's boundary slots.  The chain from a neighbour's draw to
+// this tile's next draw runs through the boundary batches only; the interior
+// work overlaps the hand-off.  The rows of an interior column take no ghost
+// add of c-1, so every row sees its updates in the colour-by-colour order.
+// `cur` holds this wave's first batch of the phase (interior, else boundary),
+// prepared; the hand-off of the last colour of the call is the epilogue's.
+// Three workgroup barriers per phase: A (the hand-off is in), B (the ghost
+// adds are done), C (the boundary batches are done).
+template <int C, int NT, int RMAX, int GMAX, int PROBE, int SH>
+__device__ __forceinline__ int tile_wlib_first(const TileState& S, int c) {
+  const int fi = S.bptr_s[c] + S.wv, fb = S.bsp_s[c] + S.wv;
+  return fi < S.bsp_s[c] ? fi : (fb < S.bptr_s[c + 1] ? fb : -1);
+}
+
+template <int C, int NT, int RMAX, int GMAX, int PROBE, int SH>
+__device__ __forceinline__ void tile_phase_wlib(const TileDev& D, const TileLaunch& a, const TileShard& sh,
+                                                TileState& S, int ph, TileBatchRegs<C, 64, RMAX>& cur,
+                                                TileGhostRegs<C, GMAX>& gr) {
+  constexpr int W = NT / 64 - 1;  // cell waves
+  const int K = S.K, t = S.t, lane = S.lane;
+  const int s = ph / K, c = ph - s * K;
+  const unsigned epoch = (unsigned)ph + 1;
+  S.ph = ph;
+  TLSTAMP(S, 0);
+  const int phn = ph + 1;
+  const int cn = phn % K, sn = phn / K;
+  const int nxt_b = phn < S.nph ? tile_wlib_first<C, NT, RMAX, GMAX, PROBE, SH>(S, cn) : -1;
+  const int bsp = S.bsp_s[c], b1 = S.bptr_s[c + 1];
+  const int ifirst = S.bptr_s[c] + S.wv, bfirst = bsp + S.wv;
+  // the hand-off of the previous colour (none at the first phase of a call)
+  const bool hp = ph > 0;
+  const int cp = hp ? (ph - 1) % K : 0;
+  const int g0 = S.gptr_s[cp], g1 = hp ? S.gptr_s[cp + 1] : g0;
+  double* acc_w = S.acc_s + S.wv * (kWaveSlotsMax * C);
+  bool nx_items = false;  // the next phase's first batch: records in flight
+  // ---- interior batches
+  for (int bi = ifirst; bi < bsp; bi += W) {
+    if (bi != ifirst) {
+      tile_load_batch<C, 64, RMAX, SH>(D, S.batch_s[bi], cur, lane);
+      tile_prep_items<C, 64, RMAX>(D, a, S.sc_s, S.seed_s, s, cur, lane);
+    }
+    tile_own_wl<C, RMAX, PROBE, SH>(D, a, sh, S, cur, epoch, acc_w);
+    const int R = cur.R;
+    if (bi + W >= bsp) {  // the last interior batch: its records are dead
+      if (bfirst < b1) {
+        tile_load_items<C, 64, RMAX, SH>(D, S.batch_s[bfirst], cur, lane);
+      } else if (nxt_b >= 0) {
+        tile_load_items<C, 64, RMAX, SH>(D, S.batch_s[nxt_b], cur, lane);
+        nx_items = true;
+      }
+      if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
+    }
+    tile_own_scatter<C, 64, RMAX, PROBE>(S, cur, R, acc_w);
+  }
+  if (ifirst >= bsp) {  // no interior batch: cur already holds the first boundary batch, if any
+    if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
+  } else if (bfirst < b1) {
+    tile_prep_items<C, 64, RMAX>(D, a, S.sc_s, S.seed_s, s, cur, lane);
+    tile_load_cells<C, 64, RMAX>(D, S.batch_s[bfirst], cur, lane);
+  }
+  TLSTAMP(S, 6);
+  __syncthreads();  // A: the exchange wave has every dw of colour c-1 in gdw_s
+  TLSTAMP(S, 4);
+  for (int gb = g0; gb < g1; gb += NT * GMAX) {
+    if (gb != g0) tile_load_ghosts<C, NT, GMAX>(D, gb, g1, gr, t);
+    tile_ghost_adds<C, GMAX>(S, gr);
+  }
+  __syncthreads();  // B
+  TLSTAMP(S, 2);
+  // ---- boundary batches
+  for (int bi = bfirst; bi < b1; bi += W) {
+    if (bi != bfirst) {
+      tile_load_batch<C, 64, RMAX, SH>(D, S.batch_s[bi], cur, lane);
+      tile_prep_items<C, 64, RMAX>(D, a, S.sc_s, S.seed_s, s, cur, lane);
+    }
+    tile_own_wl<C, RMAX, PROBE, SH>(D, a, sh, S, cur, epoch, acc_w);
+    const int R = cur.R;
+    if (bi + W >= b1 && nxt_b >= 0) {
+      tile_load_items<C, 64, RMAX, SH>(D, S.batch_s[nxt_b], cur, lane);
+      nx_items = true;
+    }
+    tile_own_scatter<C, 64, RMAX, PROBE>(S, cur, R, acc_w);
+  }
+  if (nxt_b >= 0) {
+    if (!nx_items) tile_load_items<C, 64, RMAX, SH>(D, S.batch_s[nxt_b], cur, lane);
+    tile_prep_items<C, 64, RMAX>(D, a, S.sc_s, S.seed_s, sn, cur, lane);
+    tile_load_cells<C, 64, RMAX>(D, S.batch_s[nxt_b], cur, lane);
+  }
+  // C: every wave's boundary batches of c are done before any wave's interior
+  // batches of c+1 (a row may have an own member of c in one wave's boundary
+  // batch and one of c+1 in another wave's interior batch)
+  __syncthreads();
+  TLSTAMP(S, 3);
+}
+
 // ---- exchange-wave tiles (XW; TileDev::xw).  vmcnt counts a wave's
 // vector-memory operations in issue order, loads and stores together, so in
 // a wave that streams the next batch's cells every poll of a granule -- and
@@ -966,13 +1066,23 @@ __device__ __forceinline__ void tile_phase_wl(const TileDev& D, const TileLaunch
 // data: loaded at the phase start, long in registers when the hand-off
 // ends), the own batches' barriers, then the hand-off polls -> gdw_s, and its
 // share of the ghost adds
-template <int C, int NT, int GMAX, int PROBE, int SH, int WL = 0>
+// LAG (interior-first wave-local tiles): phase ph hands off colour ph - 1
+// between its interior and boundary batches (none at ph = 0; ph = nph: the
+// launch's epilogue)
+template <int C, int NT, int GMAX, int PROBE, int SH, int WL = 0, int LAG = 0>
 __device__ __forceinline__ void tile_phase_xw(const TileDev& D, TileState& S, int ph, TileGhostRegs<C, GMAX>& gr) {
   constexpr int PB = 4;  // granule polls in flight per lane
   const int K = S.K, t = S.t, lane = S.lane;
-  const int c = ph % K;
-  const unsigned epoch = (unsigned)ph + 1;
   S.ph = ph;
+  if (LAG && ph == 0) {  // the cell waves' barriers A, B and C
+    __syncthreads();
+    __syncthreads();
+    __syncthreads();
+    return;
+  }
+  const int phx = ph - LAG;
+  const int c = phx % K;
+  const unsigned epoch = (unsigned)phx + 1;
   const int bfirst = S.bptr_s[c], bend = S.bptr_s[c + 1];
   const int g0 = S.gptr_s[c], g1 = S.gptr_s[c + 1];
   const int gs0 = S.gsp_s[c], nfi = (S.gsp_s[c + 1] - gs0) * C;
@@ -1053,6 +1163,7 @@ __device__ __forceinline__ void tile_phase_xw(const TileDev& D, TileState& S, in
     tile_ghost_adds<C, GMAX>(S, gr);
   }
   __syncthreads();
+  if (LAG && ph < S.nph) __syncthreads();  // C: the cell waves' boundary batches are done
 }
 
 // the cell waves' phase (threads t < NTC = NT - 64): own batches (their
@@ -1131,8 +1242,8 @@ __device__ __forceinline__ void tile_phase_cells(const TileDev& D, const TileLau
 // chain never waits on a tile of its own that is not resident.
 template <int C, int NT, int RMAX, int GMAX, int DB, int PROBE, int SH, int RG, int IB, int CS, int XW = 0>
 __device__ __forceinline__ void sweep_tiles_body(const TileDev& D0, TileLaunch a, const TileShard& sh) {
-  static_assert(!XW || ((!RG || XW == 2) && !IB && CS == C),
-                "exchange-wave tiles: joint chains, no split layout; r in global memory only with wave-local batches");
+  static_assert(!XW || ((!RG || XW == 2) && (!IB || XW == 2) && CS == C),
+                "exchange-wave tiles: joint chains; split layouts and r in global memory only with wave-local batches");
   constexpr int NTC = XW ? NT - 64 : NT;  // cell threads
   using BR = TileBatchRegs<C, NTC, RMAX>;
   constexpr int NW = NT / 64;
@@ -1209,7 +1320,36 @@ __device__ __forceinline__ void sweep_tiles_body(const TileDev& D0, TileLaunch a
     if (S.wv == NW - 1) {  // the exchange wave
       TileGhostRegs<C, GMAX> GX;
       __syncthreads();
-      for (int ph = 0; ph < S.nph; ++ph) tile_phase_xw<C, NT, GMAX, PROBE, SH, XW == 2>(D, S, ph, GX);
+      if constexpr (IB) {
+        for (int ph = 0; ph <= S.nph; ++ph) tile_phase_xw<C, NT, GMAX, PROBE, SH, 1, 1>(D, S, ph, GX);
+      } else {
+        for (int ph = 0; ph < S.nph; ++ph) tile_phase_xw<C, NT, GMAX, PROBE, SH, XW == 2>(D, S, ph, GX);
+      }
+    } else if constexpr (XW == 2 && IB) {  // interior-first wave-local batches
+      TileBatchRegs<C, 64, RMAX> A;
+      TileGhostRegs<C, GMAX> GA;
+      const int f0 = S.nph > 0 ? tile_wlib_first<C, NT, RMAX, GMAX, PROBE, SH>(S, 0) : -1;
+      if (f0 >= 0) {
+        tile_load_batch<C, 64, RMAX, SH>(D, S.batch_s[f0], A, S.lane);
+        tile_prep_items<C, 64, RMAX>(D, a, S.sc_s, S.seed_s, 0, A, S.lane);
+      }
+      __syncthreads();
+      for (int ph = 0; ph < S.nph; ++ph) tile_phase_wlib<C, NT, RMAX, GMAX, PROBE, SH>(D, a, sh, S, ph, A, GA);
+      // epilogue: the hand-off of the call's last colour (the exchange wave's ph = nph)
+      const int cp = S.nph > 0 ? (S.nph - 1) % K : 0;
+      const int g0 = S.gptr_s[cp], g1 = S.nph > 0 ? S.gptr_s[cp + 1] : g0;
+      if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, GA, t);
+      if (S.nph > 0) {
+        __syncthreads();
+        for (int gb = g0; gb < g1; gb += NT * GMAX) {
+          if (gb != g0) tile_load_ghosts<C, NT, GMAX>(D, gb, g1, GA, t);
+          tile_ghost_adds<C, GMAX>(S, GA);
+        }
+        __syncthreads();
+      } else {
+        __syncthreads();
+        __syncthreads();
+      }
     } else if constexpr (XW == 2) {  // wave-local batches: wave w runs batches first + w, + W, ...
       TileBatchRegs<C, 64, RMAX> A, B;
       TileGhostRegs<C, GMAX> GA;
@@ -1323,12 +1463,13 @@ static hipError_t launch_tiles_c(hipStream_t st, const TileDev& D, const TileLau
   auto k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE, SH, RG, IB, 0>;
   if constexpr (NT == 512 && !RG && !IB) {
     if (D.xw == 1) k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE, SH, RG, IB, 1>;
+  }
+  // wave-local batches: r in LDS or (no probes) in global memory, plain or
+  // interior-first layouts
+  if constexpr (NT == 512 && (!RG || !PROBE)) {
     if (D.xw == 2) k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE, SH, RG, IB, 2>;
   }
-  if constexpr (NT == 512 && RG && !IB && !PROBE) {  // r in global memory on wave-local batches
-    if (D.xw == 2) k = sweep_tiles_kernel<C, NT, RMAX, GMAX, DB, PROBE, SH, RG, IB, 2>;
-  }
-  if (D.xw && (NT != 512 || (RG && D.xw != 2) || IB)) return hipErrorInvalidValue;
+  if (D.xw && (NT != 512 || ((RG || IB) && D.xw != 2))) return hipErrorInvalidValue;
   lds = lds < kTSpreadLds ? kTSpreadLds : lds;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return e;

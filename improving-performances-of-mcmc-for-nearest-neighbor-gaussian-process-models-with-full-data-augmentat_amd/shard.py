@@ -95,7 +95,8 @@ def _sync_first(name):
 
 for _name in ("get_field", "record_field", "loglik", "loglik_chains", "ancillary_propose", "ancillary_propose_chains",
               "accept_field", "beta0_stats", "field_response_ratio", "field_response_ratio_chains",
-              "sum_squared_residuals", "sum_squared_residuals_chains"):
+              "sum_squared_residuals", "sum_squared_residuals_chains", "loglik_pair_chains", "ancillary_step_chains",
+              "sufficient_step_chains"):
     setattr(ShardContext, _name, _sync_first(_name))
 
 

@@ -99,10 +99,10 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
     """Chain i's n_iterations_update Gibbs iterations; yields its device
     requests and receives their results, so that the chains of one context
     are served by one batched call per step (one host sync for all of them):
-      ("fac", covfun, covparms | None)        -> status of the proposal factor
-      ("anc", beta_0, dlog_scale, ok)          -> None (ancillary proposal field)
-      ("ratio", beta_0, lnv) | ("ratio", None) -> dnorm ratio
-      ("llpair", beta_0, new_ls, ls) | (..., None) -> (loglik(1), loglik(0))
+      ("astep", covfun, covparms, beta_0, dlog_scale, lnv)
+          -> (status of the proposal factor, dnorm ratio of the ancillary proposal)
+      ("sstep", covfun, covparms | None, beta_0, new_ls, ls)
+          -> (status, (loglik(1), loglik(0))) | None when covparms is None
       ("sweep", n_sweeps, beta_0, log_scale, lnv, key, counter) -> None
       ("ssr", beta_0)                          -> sum of squared residuals
     Every chain yields every step of an iteration (None = nothing to do), so
@@ -161,12 +161,11 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
             innov = rng.normal(0.0, math.exp(0.5 * tk["covariance_params_ancillary"]["logvar"]), n_shape + 1)
             new_ls = params["log_scale"] + innov[0]
             new_shape = params["shape"] + innov[1:]
-            st = yield ("fac", covfun, covparms(sp_names, new_shape))
+            # the proposal's factor (:123), its field (:127) and the dnorm ratio
+            # (:129-131) behind one host sync
+            st, ratio = yield ("astep", covfun, covparms(sp_names, new_shape), params["beta_0"],
+                               new_ls - params["log_scale"], params["log_noise_variance"])
             ok = _proposal_ok(st, on_chol_error)
-            # every chain stops here each iteration (ok=False: nothing to
-            # propose) so the chains of one context stay in lockstep
-            yield ("anc", params["beta_0"], new_ls - params["log_scale"], ok)
-            ratio = yield (("ratio", params["beta_0"], params["log_noise_variance"]) if ok else ("ratio", None))
             if ok:
                 if ratio > math.log(rng.uniform()):
                     params["shape"] = new_shape
@@ -188,9 +187,13 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
         new_ls = params["log_scale"] + innov[0]
         propose = math.exp(new_ls) < var_y
         new_shape = params["shape"] + innov[1:] if propose else None
-        st = yield ("fac", covfun, covparms(sp_names, new_shape) if propose else None)
-        ok = propose and _proposal_ok(st, on_chol_error)
-        lls = yield (("llpair", params["beta_0"], new_ls, params["log_scale"]) if ok else ("llpair", None))
+        # the proposal's factor (:179) and both log-likelihoods (:184-186)
+        # behind one host sync; a chain that does not propose still yields, so
+        # the chains of one context stay in lockstep
+        res = yield ("sstep", covfun, covparms(sp_names, new_shape) if propose else None, params["beta_0"], new_ls,
+                     params["log_scale"])
+        ok = propose and _proposal_ok(res[0], on_chol_error)
+        lls = res[1] if ok else None
         if ok:
             gp_ratio = lls[0] - lls[1]
             if gp_ratio > math.log(rng.uniform()):
@@ -272,29 +275,47 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
                            "covariance_acceptance_ancillary": acc_anc}}
 
 
+def _owner_of(ctx):
+    """(ChainContext, chain) serving a chain's batched calls, or (None, None)."""
+    owner = getattr(ctx, "ctx", None)
+    if owner is not None:
+        return owner, ctx.chain
+    if getattr(ctx, "n_chains", None) == 1 and hasattr(ctx, "ancillary_step_chains"):
+        return ctx, 0
+    return None, None
+
+
+def _serve_step_separately(ctx, req):
+    """A step request through the separate calls (contexts without the
+    one-sync step entry points)."""
+    try:
+        ctx.factor(1, req[1], req[2])
+        st = 0
+    except NNGPError as e:
+        if e.status != NNGP_ERR_CHOL:
+            raise
+        return NNGP_ERR_CHOL, float("nan") if req[0] == "astep" else None
+    if req[0] == "astep":
+        ctx.ancillary_propose(req[3], req[4])
+        return st, ctx.field_response_ratio(req[3], req[5])
+    return st, (ctx.loglik(1, req[3], req[4]), ctx.loglik(0, req[3], req[5]))
+
+
 def _serve_one(ctx, req):
     """One chain's request on its own -> its result."""
     kind = req[0]
-    if kind == "fac":
+    if kind in ("astep", "sstep"):
         if req[2] is None:
             return None
-        try:
-            ctx.factor(1, req[1], req[2])
-            return 0
-        except NNGPError as e:
-            if e.status == NNGP_ERR_CHOL:
-                return NNGP_ERR_CHOL
-            raise
-    if kind == "anc":
-        if req[3]:
-            ctx.ancillary_propose(req[1], req[2])
-        return None
-    if kind == "ratio":
-        return None if req[1] is None else ctx.field_response_ratio(req[1], req[2])
-    if kind == "llpair":
-        if req[1] is None:
-            return None
-        return ctx.loglik(1, req[1], req[2]), ctx.loglik(0, req[1], req[3])
+        owner, k = _owner_of(ctx)
+        if owner is None:
+            return _serve_step_separately(ctx, req)
+        cps = np.tile(np.asarray(req[2], np.float64), (owner.n_chains, 1))
+        if kind == "astep":
+            st, r = owner.ancillary_step_chains(1 << k, req[1], cps, req[3], req[4], req[5])
+            return int(st[k]), float(r[k])
+        st, lp, lc = owner.sufficient_step_chains(1 << k, req[1], cps, req[3], req[4], req[5])
+        return int(st[k]), (float(lp[k]), float(lc[k]))
     if kind == "ssr":
         return ctx.sum_squared_residuals(req[1])
     ctx.sweep(*req[1:])
@@ -325,54 +346,41 @@ def _serve_group(owner, ids, reqs, contexts, out):
         return False
     kind = kinds.pop()
     k = owner.n_chains
-    live = [i for i in ids if reqs[i][-1] is not None] if kind in ("fac", "ratio", "llpair") else list(ids)
+    live = [i for i in ids if reqs[i][2] is not None] if kind in ("astep", "sstep") else list(ids)
     mask = 0
     for i in live:
         mask |= 1 << contexts[i].chain
     for i in ids:
         out[i] = None
-    if kind == "fac":
+    if kind in ("astep", "sstep"):
         if not live:
             return True
         covfuns = {reqs[i][1] for i in live}
         if len(covfuns) != 1:
             return False
-        ncp = len(reqs[live[0]][2])
-        cps = np.zeros((k, ncp))
-        for i in live:
-            cps[contexts[i].chain] = reqs[i][2]
-        st = owner.factor_chains(1, mask, covfuns.pop(), cps)
-        for i in live:
-            out[i] = int(st[contexts[i].chain])
-        return True
-    if kind in ("ratio", "llpair", "ssr"):
-        if not live:
-            return True
+        cps = np.zeros((k, len(reqs[live[0]][2])))
         cols = [np.zeros(k) for _ in range(3)]
         for i in live:
-            for q, v in enumerate(reqs[i][1:]):
-                cols[q][contexts[i].chain] = v
-        if kind == "ratio":
-            r = owner.field_response_ratio_chains(mask, cols[0], cols[1])
-            res = {i: float(r[contexts[i].chain]) for i in live}
-        elif kind == "ssr":
-            r = owner.sum_squared_residuals_chains(mask, cols[0])
-            res = {i: float(r[contexts[i].chain]) for i in live}
+            c = contexts[i].chain
+            cps[c] = reqs[i][2]
+            for q in range(3):
+                cols[q][c] = reqs[i][3 + q]
+        if kind == "astep":
+            st, r = owner.ancillary_step_chains(mask, covfuns.pop(), cps, *cols)
+            for i in live:
+                out[i] = (int(st[contexts[i].chain]), float(r[contexts[i].chain]))
         else:
-            l1, l0 = owner.loglik_pair_chains(mask, cols[0], cols[1], cols[2])
-            res = {i: (float(l1[contexts[i].chain]), float(l0[contexts[i].chain])) for i in live}
-        out.update(res)
-        return True
-    if kind == "anc":
-        mask, b0, dls = 0, np.zeros(k), np.zeros(k)
-        for i in ids:
-            _, beta0, dl, ok = reqs[i]
-            if ok:
+            st, lp, lc = owner.sufficient_step_chains(mask, covfuns.pop(), cps, *cols)
+            for i in live:
                 c = contexts[i].chain
-                mask |= 1 << c
-                b0[c], dls[c] = beta0, dl
-        if mask:
-            owner.ancillary_propose_chains(mask, b0, dls)
+                out[i] = (int(st[c]), (float(lp[c]), float(lc[c])))
+        return True
+    if kind == "ssr":
+        b0 = np.zeros(k)
+        for i in ids:
+            b0[contexts[i].chain] = reqs[i][1]
+        r = owner.sum_squared_residuals_chains(mask, b0)
+        out.update({i: float(r[contexts[i].chain]) for i in ids})
         return True
     if len(ids) != k or len({reqs[i][1] for i in ids}) != 1:
         return False
@@ -384,8 +392,8 @@ def _serve_group(owner, ids, reqs, contexts, out):
 
 def _drive(programs, contexts):
     """Advance chain programs in lockstep; the requests of the chains of one
-    ChainContext go through one batched call (sweep_chains /
-    ancillary_propose_chains)."""
+    ChainContext go through one batched call (sweep_chains, the one-sync MH
+    steps, sum_squared_residuals_chains)."""
     results = [None] * len(programs)
     reqs = {}
     for i, g in enumerate(programs):

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define NNGP_ABI_VERSION 10
+#define NNGP_ABI_VERSION 11
 #define NNGP_SHARD_ID_BYTES 128 /* RCCL unique id */
 #define NNGP_IPC_HANDLE_BYTES 192 /* HIP IPC handles of a tile shard's granule buffer, w replica, flags */
 
@@ -231,6 +231,24 @@ int nngp_sum_squared_residuals_chains(nngp_ctx* ctx, int chain_mask, const doubl
  * nngp_loglik_chains(0, ...) with log_scale_cur, bitwise. */
 int nngp_loglik_pair_chains(nngp_ctx* ctx, int chain_mask, const double* beta0, const double* log_scale_prop,
                             const double* log_scale_cur, double* ll_prop, double* ll_cur);
+/* One Metropolis-Hastings covariance step behind ONE host sync (the separate
+ * calls take two or three).  covparms, status as nngp_factor_chains (factor 1
+ * = the proposal of each chain in chain_mask); then, enqueued before any
+ * factor's outcome is known:
+ *   ancillary_step_chains  (update_Gaussian.R:123-131): nngp_ancillary_propose_chains
+ *     with beta0 / dlog_scale and nngp_field_response_ratio_chains with beta0 / lnv
+ *     -> ratio[k];
+ *   sufficient_step_chains (update_Gaussian.R:179-186): nngp_loglik_pair_chains
+ *     -> ll_prop[k], ll_cur[k].
+ * A chain whose proposal factor is not positive definite reports
+ * status NNGP_ERR_CHOL and NaN results; every other chain's results are
+ * bitwise those of the separate calls. */
+int nngp_ancillary_step_chains(nngp_ctx* ctx, int chain_mask, int covfun, const double* covparms, int ncovparms,
+                               const double* beta0, const double* dlog_scale, const double* log_noise_variance,
+                               int* status, double* ratio);
+int nngp_sufficient_step_chains(nngp_ctx* ctx, int chain_mask, int covfun, const double* covparms, int ncovparms,
+                                const double* beta0, const double* log_scale_prop, const double* log_scale_cur,
+                                int* status, double* ll_prop, double* ll_cur);
 /* Y = B X for X n x ncols column-major (host buffers) */
 int nngp_spmv(nngp_ctx* ctx, int which, const double* X, int ncols, double* Y);
 /* x = B^{-1} u (host buffers, length n) */

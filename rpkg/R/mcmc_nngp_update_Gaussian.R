@@ -3,11 +3,12 @@
 # Same arguments and the same returned list (one list(state, records) per
 # chain).  The scalar Metropolis-Hastings / Gibbs logic stays in R; every
 # O(n) / O(nnz) step is a .Call into libnngp.so:
-#   vecchia_Linv + sparseMatrix (:72-73,123-124,179-180)  -> nngp_factor / nngp_factor_chains
+#   vecchia_Linv + sparseMatrix (:72-73)                   -> nngp_factor
 #   precision_diag (:74,142,197)                          -> inside nngp_factor / nngp_accept_factor
-#   solve(new_B, B (field - beta_0)) (:127)                -> nngp_ancillary_propose_chains
-#   dnorm ratio (:129-131)                                 -> nngp_field_response_ratio_chains
-#   ll_compressed_sparse_chol (:8-12,184-186)              -> nngp_loglik_pair_chains (both factors, one pass)
+#   ancillary step: vecchia_Linv (:123-124), solve(new_B, B (field - beta_0)) (:127),
+#     dnorm ratio (:129-131)                               -> nngp_ancillary_step_chains (one host sync)
+#   sufficient step: vecchia_Linv (:179-180), ll_compressed_sparse_chol of both
+#     factors (:8-12,184-186)                              -> nngp_sufficient_step_chains (one host sync)
 #   crossprod(B 1), (B field, B 1) (:221-222)              -> nngp_beta0_stats
 #   chromatic sampling (:257-275)                          -> nngp_sweep_chains (Philox normals on the device)
 #   SSR (:281)                                             -> nngp_sum_squared_residuals_chains
@@ -17,9 +18,8 @@
 # holding the chains (HIP must not be initialised before a fork()), advanced in
 # lockstep: every step of an iteration is one batched call for all chains of
 # the context (one kernel pass, one host synchronisation), in the order of the
-# Python host mirror (update_gaussian.py): per iteration factor_chains,
-# ancillary_propose_chains, field_response_ratio_chains, chain by chain the
-# acceptances, factor_chains, loglik_pair_chains (proposal, current), chain by chain
+# Python host mirror (update_gaussian.py): per iteration ancillary_step_chains,
+# chain by chain the acceptances, sufficient_step_chains, chain by chain
 # the acceptances, beta_0 and mu, sweep_chains, sum_squared_residuals_chains,
 # chain by chain the field records -- the sequence the C client
 # tests/cpp/capi_sequence.c replays against the Python binding.  Each chain
@@ -134,14 +134,11 @@ mcmc_nngp_update_Gaussian <- function(locs, X, observed_field, space_time_model,
         new_ls[i] <- P[[i]]$log_scale + innov[1]
         new_shape[[i]] <- P[[i]]$shape + innov[-1]
       }
-      st <- nngp_factor_chains(ctx, 1L, all_chains, covfun, cp_rows(new_shape, seq_len(C)))
-      ok <- proposal_ok(st, seq_len(C))
-      if (any(ok)) {
-        m <- .nngp_mask(which(ok))
-        nngp_ancillary_propose_chains(ctx, m, ifelse(ok, vec("beta_0"), 0), ifelse(ok, new_ls - vec("log_scale"), 0))
-        ratio <- nngp_field_response_ratio_chains(ctx, m, ifelse(ok, vec("beta_0"), 0),
-                                                  ifelse(ok, vec("log_noise_variance"), 0))
-      }
+      # the proposals' factors, fields and dnorm ratios behind one host sync
+      stp <- nngp_ancillary_step_chains(ctx, all_chains, covfun, cp_rows(new_shape, seq_len(C)), vec("beta_0"),
+                                        new_ls - vec("log_scale"), vec("log_noise_variance"))
+      ok <- proposal_ok(stp$status, seq_len(C))
+      ratio <- stp$ratio
       for (i in seq_len(C)) {
         if (ok[i] && ratio[i] > log(draw(i, function() runif(1)))) {
           P[[i]]$shape <- new_shape[[i]]
@@ -172,15 +169,12 @@ mcmc_nngp_update_Gaussian <- function(locs, X, observed_field, space_time_model,
     prop <- which(exp(new_ls) < var_y)
     ok <- rep(FALSE, C)
     if (length(prop)) {
-      st <- nngp_factor_chains(ctx, 1L, .nngp_mask(prop), covfun, cp_rows(new_shape, prop))
-      ok <- proposal_ok(st, prop)
-    }
-    if (any(ok)) {
-      m <- .nngp_mask(which(ok))
-      b0 <- ifelse(ok, vec("beta_0"), 0)
-      ll <- nngp_loglik_pair_chains(ctx, m, b0, ifelse(ok, new_ls, 0), ifelse(ok, vec("log_scale"), 0))
-      l1 <- ll$proposal
-      l0 <- ll$current
+      # the proposals' factors and both log-likelihoods behind one host sync
+      stp <- nngp_sufficient_step_chains(ctx, .nngp_mask(prop), covfun, cp_rows(new_shape, prop), vec("beta_0"),
+                                         new_ls, vec("log_scale"))
+      ok <- proposal_ok(stp$status, prop)
+      l1 <- stp$proposal
+      l0 <- stp$current
     }
     for (i in seq_len(C)) {
       if (ok[i] && l1[i] - l0[i] > log(draw(i, function() runif(1)))) {

@@ -106,6 +106,14 @@ nngp_loglik_chains <- function(ctx, which, chain_mask, beta_0, log_scale)
 nngp_loglik_pair_chains <- function(ctx, chain_mask, beta_0, log_scale_prop, log_scale_cur)
   .Call(C_nngp_loglik_pair_chains, ctx, as.integer(chain_mask), as.double(beta_0), as.double(log_scale_prop),
         as.double(log_scale_cur))
+# one host sync for a proposal's factor and its MH step (update_Gaussian.R:123-131 / :179-186):
+# list(status, ratio) / list(status, proposal, current); a failed factor (status 3): NaN values
+nngp_ancillary_step_chains <- function(ctx, chain_mask, covfun, covparms, beta_0, dlog_scale, log_noise_variance)
+  .Call(C_nngp_ancillary_step_chains, ctx, as.integer(chain_mask), nngp_covfun_id(covfun), as.matrix(covparms) + 0,
+        as.double(beta_0), as.double(dlog_scale), as.double(log_noise_variance))
+nngp_sufficient_step_chains <- function(ctx, chain_mask, covfun, covparms, beta_0, log_scale_prop, log_scale_cur)
+  .Call(C_nngp_sufficient_step_chains, ctx, as.integer(chain_mask), nngp_covfun_id(covfun), as.matrix(covparms) + 0,
+        as.double(beta_0), as.double(log_scale_prop), as.double(log_scale_cur))
 nngp_field_response_ratio_chains <- function(ctx, chain_mask, beta_0, log_noise_variance)
   .Call(C_nngp_field_response_ratio_chains, ctx, as.integer(chain_mask), as.double(beta_0),
         as.double(log_noise_variance))

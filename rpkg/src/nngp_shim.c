@@ -469,6 +469,30 @@ SEXP C_nngp_factor_chains(SEXP p, SEXP which, SEXP mask, SEXP covfun, SEXP covpa
   return st;
 }
 
+/* covparms: n_chains x ncovparms matrix (row k = chain k) -> row-major rm */
+static int covparms_rows(nngp_ctx* c, SEXP covparms, double* rm) {
+  nngp_info inf;
+  check(nngp_ctx_info(c, &inf), c);
+  const int k = inf.n_chains, ncp = Rf_ncols(covparms);
+  if (Rf_nrows(covparms) != k) Rf_error("nngp: covparms needs one row per chain");
+  if (ncp > 16) Rf_error("nngp: at most 16 covariance parameters");
+  for (int i = 0; i < k; ++i)
+    for (int j = 0; j < ncp; ++j) rm[i * ncp + j] = REAL(covparms)[i + (size_t)j * k];
+  return ncp;
+}
+
+static SEXP named_list(int n, SEXP* v, const char** names) {
+  SEXP out = PROTECT(Rf_allocVector(VECSXP, n));
+  SEXP nm = PROTECT(Rf_allocVector(STRSXP, n));
+  for (int i = 0; i < n; ++i) {
+    SET_VECTOR_ELT(out, i, v[i]);
+    SET_STRING_ELT(nm, i, Rf_mkChar(names[i]));
+  }
+  Rf_setAttrib(out, R_NamesSymbol, nm);
+  UNPROTECT(2);
+  return out;
+}
+
 static SEXP chains_out(nngp_ctx* c) {
   nngp_info inf;
   check(nngp_ctx_info(c, &inf), c);
@@ -532,6 +556,54 @@ SEXP C_nngp_sum_squared_residuals_chains(SEXP p, SEXP mask, SEXP beta0) {
 
 /* ---------- registration ---------- */
 #define E(name, n) {#name, (DL_FUNC)&name, n}
+SEXP C_nngp_ancillary_step_chains(SEXP p, SEXP mask, SEXP covfun, SEXP covparms, SEXP beta0, SEXP dls, SEXP lnv) {
+  nngp_ctx* c = get_ctx(p);
+  const int k = ctx_chains(c);
+  double rm[4 * 16];
+  const int ncp = covparms_rows(c, covparms, rm);
+  const double *b0 = per_chain(beta0, k, "beta0"), *dl = per_chain(dls, k, "dlog_scale"),
+               *lv = per_chain(lnv, k, "log_noise_variance");
+  SEXP st = PROTECT(Rf_allocVector(INTSXP, k));
+  SEXP ratio = PROTECT(chains_out(c));
+  for (int i = 0; i < k; ++i) INTEGER(st)[i] = 0;
+  const int rc = nngp_ancillary_step_chains(c, as_int(mask), as_int(covfun), rm, ncp, b0, dl, lv, INTEGER(st),
+                                            REAL(ratio));
+  if (rc) {
+    UNPROTECT(2);
+    check(rc, c);
+  }
+  SEXP v[2] = {st, ratio};
+  const char* nm[2] = {"status", "ratio"};
+  SEXP out = named_list(2, v, nm);
+  UNPROTECT(2);
+  return out;
+}
+
+SEXP C_nngp_sufficient_step_chains(SEXP p, SEXP mask, SEXP covfun, SEXP covparms, SEXP beta0, SEXP ls_prop,
+                                   SEXP ls_cur) {
+  nngp_ctx* c = get_ctx(p);
+  const int k = ctx_chains(c);
+  double rm[4 * 16];
+  const int ncp = covparms_rows(c, covparms, rm);
+  const double *b0 = per_chain(beta0, k, "beta0"), *lp = per_chain(ls_prop, k, "log_scale_prop"),
+               *lc = per_chain(ls_cur, k, "log_scale_cur");
+  SEXP st = PROTECT(Rf_allocVector(INTSXP, k));
+  SEXP prop = PROTECT(chains_out(c));
+  SEXP cur = PROTECT(chains_out(c));
+  for (int i = 0; i < k; ++i) INTEGER(st)[i] = 0;
+  const int rc = nngp_sufficient_step_chains(c, as_int(mask), as_int(covfun), rm, ncp, b0, lp, lc, INTEGER(st),
+                                             REAL(prop), REAL(cur));
+  if (rc) {
+    UNPROTECT(3);
+    check(rc, c);
+  }
+  SEXP v[3] = {st, prop, cur};
+  const char* nm[3] = {"status", "proposal", "current"};
+  SEXP out = named_list(3, v, nm);
+  UNPROTECT(3);
+  return out;
+}
+
 static const R_CallMethodDef call_methods[] = {
     E(C_nngp_abi_version, 0),
     E(C_nngp_status_string, 1),
@@ -579,6 +651,8 @@ static const R_CallMethodDef call_methods[] = {
     E(C_nngp_factor_chains, 5),
     E(C_nngp_loglik_chains, 5),
     E(C_nngp_loglik_pair_chains, 5),
+    E(C_nngp_ancillary_step_chains, 7),
+    E(C_nngp_sufficient_step_chains, 7),
     E(C_nngp_field_response_ratio_chains, 4),
     E(C_nngp_sum_squared_residuals_chains, 3),
     {NULL, NULL, 0}};

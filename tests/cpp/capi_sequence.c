@@ -65,9 +65,8 @@ static int lockstep(nngp_ctx* ctx, int n, double* f) {
       cps[3 * k] = 1.0; cps[3 * k + 1] = exp(nsh[k]); cps[3 * k + 2] = 0.0;
       dls[k] = nls[k] - ls[k];
     }
-    CHECK(nngp_factor_chains(ctx, 1, all, NNGP_EXPONENTIAL_ISOTROPIC, cps, 3, st), ctx);
-    CHECK(nngp_ancillary_propose_chains(ctx, all, b0, dls), ctx);
-    CHECK(nngp_field_response_ratio_chains(ctx, all, b0, lnv, v), ctx);
+    /* the R drop-in's one-sync step: factor, proposal field and ratio */
+    CHECK(nngp_ancillary_step_chains(ctx, all, NNGP_EXPONENTIAL_ISOTROPIC, cps, 3, b0, dls, lnv, st, v), ctx);
     pr3("ratio", it, v);
     for (int k = 0; k < C; ++k)
       if (st[k] == 0 && v[k] > lu_anc[k]) {
@@ -82,8 +81,7 @@ static int lockstep(nngp_ctx* ctx, int n, double* f) {
       nsh[k] = shape[k] + 0.01 * (2 - k);
       cps[3 * k] = 1.0; cps[3 * k + 1] = exp(nsh[k]); cps[3 * k + 2] = 0.0;
     }
-    CHECK(nngp_factor_chains(ctx, 1, all, NNGP_EXPONENTIAL_ISOTROPIC, cps, 3, st), ctx);
-    CHECK(nngp_loglik_pair_chains(ctx, all, b0, nls, ls, l1, l0), ctx);
+    CHECK(nngp_sufficient_step_chains(ctx, all, NNGP_EXPONENTIAL_ISOTROPIC, cps, 3, b0, nls, ls, st, l1, l0), ctx);
     pr3("l1", it, l1);
     pr3("l0", it, l0);
     for (int k = 0; k < C; ++k) {

@@ -20,7 +20,7 @@ def test_header_symbols_exported(P):
     lib = C.CDLL(str(_lib.LIB_PATH))
     for s in sorted(declared):
         assert hasattr(lib, s), s
-    assert P.lib.nngp_abi_version() == 10
+    assert P.lib.nngp_abi_version() == 11
 
 
 def test_library_has_gfx950_code_object():
@@ -233,6 +233,22 @@ def test_tile_sweep_emulation_wave_local(tile_check_exe, n, m, tiles, chains, se
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
 
 
+@pytest.mark.parametrize("n,m,tiles,chains,seed,G", [
+    (3000, 10, 16, 3, 1, 1), (60000, 15, 64, 3, 5, 1), (20000, 10, 40, 4, 2, 4), (400, 5, 16, 3, 7, 2)])
+def test_tile_sweep_emulation_wave_local_interior_first(tile_check_exe, n, m, tiles, chains, seed, G):
+    """Interior-first wave-local layouts (NNGP_TILE_SPLIT=1 on wave-local
+    batches, tiles.hip tile_phase_wlib): per colour the interior run, then the
+    boundary run, each cut into 64-lane batches in rounds of 7 waves.  The
+    emulation runs the kernel's schedule -- every tile's interior batches of
+    colour c, the ghost adds of colour c-1, the boundary batches of c -- and
+    checks the field against the serial sweep (1e-11) and the layout."""
+    import subprocess
+
+    out = subprocess.run([str(tile_check_exe), str(n), str(m), str(tiles), str(chains), str(seed), "64", "8",
+                          str(G), "1", "2", "7"], capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
+
+
 def test_exchange_wave_barrier_count_matches_own_draw():
     """The exchange wave of a tile (tiles.hip tile_phase_xw) holds no cells and
     passes the own batches' workgroup barriers by count: kOwnDrawBarriers must
@@ -385,6 +401,29 @@ class _FailingCtx:
         pass
 
 
+class _FailingStepCtx(_FailingCtx):
+    """The same failure through the one-sync MH step entry points
+    (nngp_ancillary_step_chains / nngp_sufficient_step_chains): a CHOL
+    failure is a per-chain status, any other failure raises."""
+
+    n_chains = 1
+
+    def _step(self):
+        from nngp_amd._lib import NNGP_ERR_CHOL, NNGPError
+
+        if self.status != NNGP_ERR_CHOL:
+            raise NNGPError(self.status, "injected")
+        return np.array([self.status], np.int32)
+
+    def ancillary_step_chains(self, mask, covfun, cps, b0, dls, lnv):
+        assert mask == 1 and cps.shape[0] == 1
+        return self._step(), np.array([np.nan])
+
+    def sufficient_step_chains(self, mask, covfun, cps, b0, lsp, lsc):
+        assert mask == 1 and cps.shape[0] == 1
+        return self._step(), np.array([np.nan]), np.array([np.nan])
+
+
 def _drive_one(g, ctx):
     """Run a chain program against one context (update_gaussian._run_chain's
     loop): -> the request kinds it issued, in order."""
@@ -394,7 +433,7 @@ def _drive_one(g, ctx):
     try:
         req = next(g)
         while True:
-            kinds.append((req[0], req[-1] is not None if req[0] != "anc" else req[3]))
+            kinds.append((req[0], req[2] is not None if req[0] in ("astep", "sstep") else True))
             req = g.send(_serve_one(ctx, req))
     except StopIteration:
         return kinds
@@ -421,17 +460,17 @@ def test_mh_proposal_factor_failures(P):
     (here a HIP error) propagates in both modes."""
     from nngp_amd._lib import NNGP_ERR_CHOL, NNGP_ERR_HIP, NNGPError
 
-    with pytest.raises(NNGPError) as e:
-        _drive_one(_program(_FailingCtx(NNGP_ERR_CHOL), "error"), _FailingCtx(NNGP_ERR_CHOL))
-    assert e.value.status == NNGP_ERR_CHOL
-    kinds = _drive_one(_program(_FailingCtx(NNGP_ERR_CHOL), "reject"), _FailingCtx(NNGP_ERR_CHOL))
-    # both proposals rejected (no ratio, no log-likelihoods), the iteration goes on
-    assert kinds == [("fac", True), ("anc", False), ("ratio", False), ("fac", True), ("llpair", False),
-                     ("sweep", True), ("ssr", True)], kinds
-    for mode in ("error", "reject"):
+    for Ctx in (_FailingCtx, _FailingStepCtx):  # separate calls / one-sync step entry points
         with pytest.raises(NNGPError) as e:
-            _drive_one(_program(_FailingCtx(NNGP_ERR_HIP), mode), _FailingCtx(NNGP_ERR_HIP))
-        assert e.value.status == NNGP_ERR_HIP
+            _drive_one(_program(Ctx(NNGP_ERR_CHOL), "error"), Ctx(NNGP_ERR_CHOL))
+        assert e.value.status == NNGP_ERR_CHOL
+        kinds = _drive_one(_program(Ctx(NNGP_ERR_CHOL), "reject"), Ctx(NNGP_ERR_CHOL))
+        # both proposals rejected (their ratio / log-likelihoods unused), the iteration goes on
+        assert kinds == [("astep", True), ("sstep", True), ("sweep", True), ("ssr", True)], kinds
+        for mode in ("error", "reject"):
+            with pytest.raises(NNGPError) as e:
+                _drive_one(_program(Ctx(NNGP_ERR_HIP), mode), Ctx(NNGP_ERR_HIP))
+            assert e.value.status == NNGP_ERR_HIP
 
 
 def test_r_shim_wraps_every_abi_entry_point():

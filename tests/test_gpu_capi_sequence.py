@@ -63,8 +63,10 @@ def test_c_client_equals_python_binding(P):
 
 def test_c_client_r_dropin_lockstep_equals_python_binding(P):
     """The R drop-in's 3-chain lockstep iteration (rpkg/R/mcmc_nngp_update_Gaussian.R:
-    factor_chains -> ancillary_propose_chains -> field_response_ratio_chains ->
-    accept_field / accept_factor -> factor_chains -> loglik_chains x 2 ->
+    ancillary_step_chains -> accept_field / accept_factor ->
+    sufficient_step_chains -> (here, in Python: the separate calls they
+    replace, factor_chains -> ancillary_propose_chains ->
+    field_response_ratio_chains and factor_chains -> loglik_chains x 2) ->
     accept_factor -> beta0_stats / set_mu per chain -> sweep_chains ->
     sum_squared_residuals_chains -> record_field; get_records / get_field at the
     end), 2 iterations with fixed draws and fixed log-uniforms (chain 0 always

@@ -211,3 +211,68 @@ def test_loglik_pair_equals_two_loglik_calls_bitwise(P, O):
         for ll, L, ls in ((res[0][0][k], L1, lsp[k]), (res[0][1][k], L0, lsc[k])):
             llo = O.loglik(L, f - b0[k], NN, ls)
             assert abs(ll - llo) <= 1e-10 * abs(llo)
+
+
+def test_mh_step_calls_equal_separate_calls_bitwise(P):
+    """nngp_ancillary_step_chains / nngp_sufficient_step_chains (a proposal's
+    factor and its MH step behind one host sync, update_Gaussian.R:123-131 and
+    :179-186) == the separate calls they replace, bitwise, chain by chain; a
+    chain whose proposal factor is not positive definite (two coinciding
+    points, no nugget) reports NNGP_ERR_CHOL and NaN results without
+    disturbing the other chains, and a later step of that chain is exact."""
+    from nngp_amd._lib import NNGP_ERR_CHOL
+
+    n, m, C = 6000, 10, 3
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=46)
+    locs = locs.copy()
+    k0 = 500
+    locs[k0] = locs[NN[k0, 1] - 1]  # row k0 coincides with its first neighbour
+    rng = np.random.default_rng(47)
+    b0, dls, lnv = rng.normal(size=C) * 0.1, rng.normal(size=C) * 0.1, rng.normal(size=C) * 0.1 - 1.0
+    lsp, lsc = rng.normal(size=C) * 0.1, rng.normal(size=C) * 0.1
+    cur = [[1.0, 0.08 + 0.01 * k, 0.1] for k in range(C)]
+    prop = np.array([[1.1, 0.07 + 0.01 * k, 0.0 if k == 1 else 0.05] for k in range(C)])  # chain 1 fails
+    mask = (1 << C) - 1
+
+    def setup(ctx):
+        for k in range(C):
+            ctx.select(k)
+            ctx.factor(0, "exponential_isotropic", cur[k])
+            ctx.set_field(np.random.default_rng(k).normal(size=n))
+            ctx.set_mu(None, b0[k])
+
+    with P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=C) as ctx:
+        setup(ctx)
+        st_a, ratio = ctx.ancillary_step_chains(mask, "exponential_isotropic", prop, b0, dls, lnv)
+        props = []
+        for k in range(C):
+            ctx.select(k)
+            if st_a[k] == 0:
+                ctx.accept_field()
+            props.append(ctx.get_field())
+        st_s, lp, lc = ctx.sufficient_step_chains(mask, "exponential_isotropic", prop, b0, lsp, lsc)
+        st_s2, lp2, lc2 = ctx.sufficient_step_chains(2, "exponential_isotropic", prop * [1, 1, 0] + [0, 0, 0.05], b0,
+                                                     lsp, lsc)
+    with P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=C) as ctx:
+        setup(ctx)
+        st = ctx.factor_chains(1, mask, "exponential_isotropic", prop)
+        ok = (1 << 0) | (1 << 2)
+        ctx.ancillary_propose_chains(ok, b0, dls)
+        ratio_ref = ctx.field_response_ratio_chains(ok, b0, lnv)
+        props_ref = []
+        for k in range(C):
+            ctx.select(k)
+            if st[k] == 0:
+                ctx.accept_field()
+            props_ref.append(ctx.get_field())
+        st2 = ctx.factor_chains(1, mask, "exponential_isotropic", prop)
+        lp_ref, lc_ref = ctx.loglik_pair_chains(ok, b0, lsp, lsc)
+        ctx.factor_chains(1, 2, "exponential_isotropic", prop * [1, 1, 0] + [0, 0, 0.05])
+        lp2_ref, lc2_ref = ctx.loglik_pair_chains(2, b0, lsp, lsc)
+    assert list(st) == list(st_a) == list(st2) == list(st_s) == [0, NNGP_ERR_CHOL, 0], (st, st_a, st_s)
+    assert np.isnan(ratio[1]) and np.isnan(lp[1]) and np.isnan(lc[1])
+    for k in (0, 2):
+        assert ratio[k] == ratio_ref[k] and lp[k] == lp_ref[k] and lc[k] == lc_ref[k], k
+        np.testing.assert_array_equal(props[k], props_ref[k])
+    np.testing.assert_array_equal(props[1], props_ref[1])  # the failed chain kept its field
+    assert st_s2[1] == 0 and lp2[1] == lp2_ref[1] and lc2[1] == lc2_ref[1]

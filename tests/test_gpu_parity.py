@@ -56,6 +56,24 @@ def test_factor_matches_oracle(P, O, m, covfun):
         np.testing.assert_allclose(ctx.precision_diag(), O.precision_diag(ref, NN), rtol=1e-10)
 
 
+@pytest.mark.parametrize("covfun", ["exponential_isotropic", "matern15_isotropic"])
+def test_factor_with_coinciding_points_matches_oracle(P, O, covfun):
+    """Two locations at distance 0 (correlation 1) with a nugget: a positive
+    definite local covariance that GpGp factors; the device's distance
+    (sqrt_pos at s = 0) must be 0, not 0 x inf."""
+    locs, NN, col, lm, y = make_problem(P, 3000, 10, seed=71)
+    locs = locs.copy()
+    for k0 in (100, 1500, 2999):
+        locs[k0] = locs[NN[k0, 1] - 1]
+    cp = [1.0, 0.08, 0.1]
+    with _ctx(P, locs, NN, col, lm, y) as ctx:
+        ctx.factor(0, covfun, cp)
+        got = ctx.get_linv(0)
+    ref = O.vecchia_linv(covfun, cp, locs, NN)
+    assert np.all(np.isfinite(got))
+    np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-10)
+
+
 @pytest.mark.parametrize("covfun,cp,d", [
     ("exponential_scaledim", [1.3, 0.1, 0.3, 0.0], 2),
     ("exponential_spacetime", [0.7, 0.1, 0.5, 0.0], 3),
@@ -678,6 +696,91 @@ def test_tile_engine_r_in_global_memory_equals_lds_bitwise(P, engine, monkeypatc
             out.append(res)
     for k in range(C):
         np.testing.assert_array_equal(out[1][k], out[0][k], err_msg=f"chain {k}")
+
+
+@pytest.mark.parametrize("n,m,C", [(20000, 10, 1), (60000, 15, 3), (40000, 20, 4)])
+def test_tile_engine_r_in_global_wave_local_equals_lds_bitwise(P, engine, monkeypatch, n, m, C):
+    """Wave-local batches (tiles.hip tile_phase_wl) with r in global memory
+    (the route n = 1e7 takes on one GPU at 3 chains, where the colour engine
+    refuses m = 20) == wave-local LDS tiles on the same layout, bitwise, after
+    two calls (3 + 2 sweeps)."""
+    if engine != "tiles-default":
+        pytest.skip("sets the engine itself")
+    monkeypatch.setenv("NNGP_TILE_WL", "1")
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=n + C + 7)
+    rng = np.random.default_rng(C + 7)
+    fields = [rng.normal(size=n) for _ in range(C)]
+    out = []
+    for rg in (False, True):
+        if rg:
+            monkeypatch.setenv("NNGP_TILE_R", "global")
+        else:
+            monkeypatch.delenv("NNGP_TILE_R", raising=False)
+        with P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=C) as ctx:
+            info = ctx.info
+            assert info["sweep_engine"] == 1 and info["tile_r_global"] == int(rg), info
+            assert "wave-local" in info["engine_note"], info["engine_note"]
+            for k in range(C):
+                ctx.select(k)
+                ctx.factor(0, "matern15_isotropic", [1.0, 0.05 + 0.01 * k, 0.0])
+                ctx.set_field(fields[k])
+                ctx.set_mu(None, 0.1 * k)
+            ctx.sweep_chains(3, [0.1 * k for k in range(C)], [0.1] * C, [-0.4] * C, [31 + k for k in range(C)],
+                             [0] * C)
+            ctx.sweep_chains(2, [0.1 * k for k in range(C)], [0.0] * C, [-0.5] * C, [41 + k for k in range(C)],
+                             [3] * C)
+            res = []
+            for k in range(C):
+                ctx.select(k)
+                res.append(ctx.get_field())
+            out.append(res)
+    for k in range(C):
+        np.testing.assert_array_equal(out[1][k], out[0][k], err_msg=f"chain {k}")
+
+
+@pytest.mark.parametrize("n,m,C,rg", [(60000, 15, 3, False), (200000, 15, 3, False), (40000, 20, 4, False),
+                                      (60000, 15, 3, True)])
+def test_tile_engine_interior_first_wave_local_matches_wave_local(P, engine, monkeypatch, n, m, C, rg):
+    """Interior-first wave-local tiles (NNGP_TILE_SPLIT=1, tiles.hip
+    tile_phase_wlib: a colour's interior batches overlap the previous
+    colour's hand-off) == plain wave-local tiles after two calls (3 + 2
+    sweeps) to 1e-11: the same per-row update order, but the split layout
+    cuts a slot's cells over other lanes, so its sum rounds differently
+    (measured: 7e-15 absolute)."""
+    if engine != "tiles-default":
+        pytest.skip("sets the engine itself")
+    monkeypatch.setenv("NNGP_TILE_WL", "1")
+    if rg:
+        monkeypatch.setenv("NNGP_TILE_R", "global")
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=n + C + 11)
+    rng = np.random.default_rng(C + 11)
+    fields = [rng.normal(size=n) for _ in range(C)]
+    out = []
+    for split in (False, True):
+        if split:
+            monkeypatch.setenv("NNGP_TILE_SPLIT", "1")
+        else:
+            monkeypatch.delenv("NNGP_TILE_SPLIT", raising=False)
+        with P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=C) as ctx:
+            info = ctx.info
+            assert info["sweep_engine"] == 1 and "wave-local" in info["engine_note"], info["engine_note"]
+            assert ("interior first" in info["engine_note"]) == split, info["engine_note"]
+            for k in range(C):
+                ctx.select(k)
+                ctx.factor(0, "matern15_isotropic", [1.0, 0.05 + 0.01 * k, 0.0])
+                ctx.set_field(fields[k])
+                ctx.set_mu(None, 0.1 * k)
+            ctx.sweep_chains(3, [0.1 * k for k in range(C)], [0.1] * C, [-0.4] * C, [31 + k for k in range(C)],
+                             [0] * C)
+            ctx.sweep_chains(2, [0.1 * k for k in range(C)], [0.0] * C, [-0.5] * C, [41 + k for k in range(C)],
+                             [3] * C)
+            res = []
+            for k in range(C):
+                ctx.select(k)
+                res.append(ctx.get_field())
+            out.append(res)
+    for k in range(C):
+        np.testing.assert_allclose(out[1][k], out[0][k], rtol=1e-11, atol=1e-12, err_msg=f"chain {k}")
 
 
 def test_beta0_stats_reuses_loglik_pass_and_invalidates(P, O, engine):
