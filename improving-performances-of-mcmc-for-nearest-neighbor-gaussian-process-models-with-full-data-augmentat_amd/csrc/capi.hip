@@ -144,7 +144,14 @@ struct nngp_ctx {
   double* z_d = nullptr;
   size_t z_cap = 0;
   SweepScalars* scal_d = nullptr;  // C
-  SweepScalars* scal_h = nullptr;  // pinned, C
+  SweepScalars* scal_h = nullptr;  // pinned, C: the next call's scalars (sweep_prepare)
+  // staging ring of the scalar uploads: a sweep call returns before its
+  // upload has run, so the next call stages into another slot (a slot is
+  // reused once its previous copy has run: its event)
+  static constexpr int kScalRing = 8;
+  SweepScalars* scal_ring_h = nullptr;  // pinned, kScalRing x C
+  hipEvent_t scal_ev[kScalRing] = {};
+  int scal_next = 0;
   double* res_h = nullptr;         // pinned, 4 x kRowJobsMax doubles, then fail_h
   int* fail_h = nullptr;           // pinned, kMaxChains failure rows of the factors (inside res_h)
   unsigned long long* dbg_d = nullptr;  // NNGP_PROBE=9: per-chunk timestamps
@@ -537,6 +544,9 @@ void nngp_ctx_destroy(nngp_ctx* c) {
   }
   for (void* p : ptrs) if (p) hipFree(p);
   if (c->scal_h) hipHostFree(c->scal_h);
+  if (c->scal_ring_h) hipHostFree(c->scal_ring_h);
+  for (hipEvent_t& e : c->scal_ev)
+    if (e) hipEventDestroy(e);
   if (c->res_h) hipHostFree(c->res_h);
   if (c->linv_cur_h) hipHostFree(c->linv_cur_h);
   if (c->stage_h) hipHostFree(c->stage_h);
@@ -1059,6 +1069,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
   CK(dalloc(&c->scal_d, C));
   CK(hipHostMalloc((void**)&c->scal_h, sizeof(SweepScalars) * C, hipHostMallocDefault));
   std::memset(c->scal_h, 0, sizeof(SweepScalars) * C);
+  CK(hipHostMalloc((void**)&c->scal_ring_h, sizeof(SweepScalars) * C * nngp_ctx::kScalRing, hipHostMallocDefault));
   CK(hipHostMalloc((void**)&c->res_h, kResBytes, hipHostMallocDefault));
   c->fail_h = reinterpret_cast<int*>(c->res_h + kResFailOff);
   CK(upload(c->locs_d, locs_rm.data(), locs_rm.size(), c->st));
@@ -1670,7 +1681,14 @@ static void fields_written(nngp_ctx* c, int mask) {
 
 
 static int upload_scalars(nngp_ctx* c) {
-  HIPCHK(c, hipMemcpyAsync(c->scal_d, c->scal_h, sizeof(SweepScalars) * c->C, hipMemcpyHostToDevice, c->st));
+  const int r = c->scal_next;
+  c->scal_next = (r + 1) % nngp_ctx::kScalRing;
+  if (c->scal_ev[r]) HIPCHK(c, hipEventSynchronize(c->scal_ev[r]));  // that slot's last copy has run
+  else HIPCHK(c, hipEventCreateWithFlags(&c->scal_ev[r], hipEventDisableTiming));
+  SweepScalars* slot = c->scal_ring_h + (size_t)r * c->C;
+  std::memcpy(slot, c->scal_h, sizeof(SweepScalars) * c->C);
+  HIPCHK(c, hipMemcpyAsync(c->scal_d, slot, sizeof(SweepScalars) * c->C, hipMemcpyHostToDevice, c->st));
+  HIPCHK(c, hipEventRecord(c->scal_ev[r], c->st));
   return NNGP_OK;
 }
 
