@@ -65,6 +65,9 @@ struct ChainState {
   // nngp_get_precision_diag), so a chain that accepts two proposals in one
   // MCMC iteration refreshes once
   bool vals_stale = false;
+  // the residual sums (SweepDev::dr .y) are behind mu / beta_0: recomputed for
+  // every such chain in one pass before the next sweep (flush_sweep_values)
+  bool res_stale = false;
 };
 
 // res_d / res_h: 4 x kRowJobsMax reduction results, then the kMaxChains
@@ -394,8 +397,20 @@ int flush_one(nngp_ctx* c, int k) {
   return NNGP_OK;
 }
 
-// the sweep values of the chains in mask, where behind their current factor
+// the sweep values of the chains in mask, where behind their current factor,
+// and their residual sums, where behind mu / beta_0 (one pass for all chains)
 int flush_sweep_values(nngp_ctx* c, int mask) {
+  ResJobs J;
+  for (int k = 0; k < c->C; ++k) {
+    ChainState& S = c->ch[k];
+    if (!((mask >> k) & 1) || !S.res_stale) continue;
+    J.mu[J.M] = S.mu_is_const ? nullptr : S.mu_d;
+    J.beta0[J.M] = S.mu_beta0;
+    J.chain[J.M] = k;
+    ++J.M;
+    S.res_stale = false;
+  }
+  if (J.M) HIPCHK(c, launch_residual_sums_jobs(c->st, c->n, sweep_dev(c), J, c->obs_ptr_d, c->obs_idx_d, c->y_d));
   for (int k = 0; k < c->C; ++k)
     if (((mask >> k) & 1) && c->ch[k].vals_stale) {
       int rc = flush_one(c, k);
@@ -981,7 +996,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     CK(hipMemsetAsync(c->gval_d, 0, sizeof(double) * std::max<size_t>(1, ng * C), c->st));
     CK(upload(c->gptr_d, TL.gptr.data(), TL.gptr.size(), c->st));
     {
-      const std::vector<int4> ro = tile_refresh_order(TL.batch_ptr, TL.gptr, TL.T, TL.K, c->rorder_len);
+      const std::vector<int4> ro = tile_refresh_order(TL.batch_ptr, TL.gptr, TL.batch, TL.NT, TL.T, TL.K, c->rorder_len);
       CK(dalloc(&c->rorder_d, ro.size()));
       CK(upload(c->rorder_d, ro.data(), ro.size(), c->st));
     }
@@ -1504,8 +1519,7 @@ int nngp_set_mu(nngp_ctx* c, const double* mu, double beta0) {
   }
   S.mu_is_const = (mu == nullptr);
   S.mu_beta0 = beta0;
-  HIPCHK(c, launch_residual_sums(c->st, c->n, sweep_dev(c), c->cur, c->obs_ptr_d, c->obs_idx_d, c->y_d,
-                                 mu ? S.mu_d : nullptr, beta0));
+  S.res_stale = true;
   S.have_mu = true;
   return NNGP_OK;
 }
@@ -1655,11 +1669,9 @@ static int sweep_prepare(nngp_ctx* c, int k, double beta0, double log_scale, dou
     std::snprintf(buf, sizeof buf, "sweep: chain %d needs factor, field and mu", k);
     return fail_msg(c, NNGP_ERR_STATE, buf);
   }
-  if (S.mu_is_const && S.mu_beta0 != beta0) {
-    // residual sums depend on beta0 when mu = beta0
-    HIPCHK(c, launch_residual_sums(c->st, c->n, sweep_dev(c), k, c->obs_ptr_d, c->obs_idx_d, c->y_d,
-                                   nullptr, beta0));
+  if (S.mu_is_const && S.mu_beta0 != beta0) {  // residual sums depend on beta0 when mu = beta0
     S.mu_beta0 = beta0;
+    S.res_stale = true;
   }
   SweepScalars& sc = c->scal_h[k];
   sc.inv_s2 = std::exp(-log_scale);
@@ -1804,7 +1816,11 @@ static void warm_set(nngp_ctx* c, int mask, const double* beta0) {
 // tile context shares the device -- then the call holds the device's tile
 // lock until its launch has drained (tile_lock) -- or a probe buffer is read.
 static bool sweep_async(const nngp_ctx* c) {
-  return (c->engine != 1 || tile_ctx_count(c->device) == 1) && !c->tdbg_d && !c->dbg_d;
+  static const bool force_sync = [] {  // NNGP_SWEEP_SYNC=1: every sweep call ends with a host sync
+    const char* e = std::getenv("NNGP_SWEEP_SYNC");
+    return e && std::string(e) == "1";
+  }();
+  return !force_sync && (c->engine != 1 || tile_ctx_count(c->device) == 1) && !c->tdbg_d && !c->dbg_d;
 }
 
 int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double lnv, uint64_t seed,
@@ -2583,25 +2599,28 @@ int nngp_ancillary_propose_chains(nngp_ctx* c, int chain_mask, const double* bet
   return NNGP_OK;  // stream-ordered
 }
 
-// data-term reductions of chain k (mode 1: the dnorm ratio of the proposal,
-// mode 0: the sum of squared residuals) into res_d[4k..]
-static int obs_enqueue(nngp_ctx* c, int k, int mode, double beta0, double lnv) {
-  ChainState& S = c->ch[k];
-  if (!S.have_field || !S.have_mu) return fail_msg(c, NNGP_ERR_STATE, "data term: need field and mu");
-  int nb = launch_obs_reduce(c->st, mode, c->n_obs, c->y_d, S.mu_is_const ? nullptr : S.mu_d, beta0, c->lm_d,
-                             S.field_d, mode == 1 ? S.field_prop_d : nullptr, mode == 1 ? 0.5 * std::exp(-lnv) : 0.0,
-                             c->partials_d);
-  HIPCHK(c, hipGetLastError());
-  HIPCHK(c, launch_reduce4(c->st, c->partials_d, nb, c->res_d + 4 * k));
-  return NNGP_OK;
-}
-
+// data-term reductions (mode 1: the dnorm ratio of the proposal, mode 0:
+// the sum of squared residuals) of the chains in mask into res_d[4k..]
 static int obs_chains_enqueue(nngp_ctx* c, int mode, int chain_mask, const double* beta0, const double* lnv,
                               bool copy = true) {
-  int rc;
-  for (int k = 0; k < c->C; ++k)
-    if ((chain_mask >> k) & 1)
-      if ((rc = obs_enqueue(c, k, mode, beta0[k], mode == 1 ? lnv[k] : 0.0))) return rc;
+  // every chain in one pass (per chain obs_enqueue's bits), totals at res_d[4k]
+  ObsJobs J;
+  RowJobs R;
+  for (int k = 0; k < c->C; ++k) {
+    if (!((chain_mask >> k) & 1)) continue;
+    ChainState& S = c->ch[k];
+    if (!S.have_field || !S.have_mu) return fail_msg(c, NNGP_ERR_STATE, "data term: need field and mu");
+    J.mu[J.M] = S.mu_is_const ? nullptr : S.mu_d;
+    J.beta0[J.M] = beta0[k];
+    J.f[J.M] = S.field_d;
+    J.fnew[J.M] = mode == 1 ? S.field_prop_d : nullptr;
+    J.inv_2var[J.M] = mode == 1 ? 0.5 * std::exp(-lnv[k]) : 0.0;
+    ++J.M;
+    R.res_slot[R.M++] = k;
+  }
+  const int nb = launch_obs_reduce_jobs(c->st, mode, c->n_obs, c->y_d, c->lm_d, J, c->partials_d);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, launch_reduce4_jobs(c->st, R, c->partials_d, nb, c->res_d));
   if (copy) HIPCHK(c, hipMemcpyAsync(c->res_h, c->res_d, 4 * c->C * sizeof(double), hipMemcpyDeviceToHost, c->st));
   return NNGP_OK;
 }

@@ -138,6 +138,28 @@ hipError_t launch_set_ptr(hipStream_t st, const double** dst, int k, const doubl
 hipError_t launch_sell_refresh(hipStream_t st, const SweepDev& L, int nchunks, const int* ent_src,
                                const double* linv, int chain);
 
+// residual sums of up to kMaxChains chains in one pass (chain J.chain[j]:
+// mu J.mu[j], or beta0 J.beta0[j] when null)
+struct ResJobs {
+  const double* mu[kMaxChains] = {};
+  double beta0[kMaxChains] = {};
+  int chain[kMaxChains] = {};
+  int M = 0;
+};
+hipError_t launch_residual_sums_jobs(hipStream_t st, int n, const SweepDev& L, const ResJobs& J,
+                                     const int* obs_ptr, const int* obs_idx, const double* y);
+// obs reductions (as launch_obs_reduce) of up to kMaxChains chains in one
+// pass; partials of job j at partials + j * kRedBlocks * 4.  Returns #blocks.
+struct ObsJobs {
+  const double* mu[kMaxChains] = {};
+  double beta0[kMaxChains] = {};
+  const double* f[kMaxChains] = {};
+  const double* fnew[kMaxChains] = {};
+  double inv_2var[kMaxChains] = {};
+  int M = 0;
+};
+int launch_obs_reduce_jobs(hipStream_t st, int mode, int n_obs, const double* y, const int* lm, const ObsJobs& J,
+                           double* partials);
 // dr[x*C+chain].y = residuals_sum of the observations of compact slot x
 hipError_t launch_residual_sums(hipStream_t st, int n, const SweepDev& L, int chain, const int* obs_ptr,
                                 const int* obs_idx, const double* y, const double* mu, double beta0);
@@ -252,9 +274,11 @@ hipError_t launch_tile_halo_put(hipStream_t st, const TilePeerW& pw, const int* 
 // chain `chain`: cell/ghost values from Linv (device order) and precision_diag
 // work items of the refresh, dealt to kRefreshLists (= XCDs) lists by tile;
 // olen = the longest list
+struct TileBatch;  // graph_prep.h
 constexpr int kRefreshLists = 8;
-std::vector<int4> tile_refresh_order(const std::vector<int>& batch_ptr, const std::vector<int>& gptr, int T, int K,
-                                     int& olen);
+constexpr int kRefreshCells = 4096;  // cells of one work item (a run of batches): its LDS
+std::vector<int4> tile_refresh_order(const std::vector<int>& batch_ptr, const std::vector<int>& gptr,
+                                     const std::vector<TileBatch>& batch, int NT, int T, int K, int& olen);
 hipError_t launch_tile_refresh(hipStream_t st, const TileDev& D, const int4* order, int olen, int NT,
                                const int* cell_src, const int* gsrc, const double* linv, int chain);
 

@@ -899,6 +899,34 @@ __global__ void residual_sums_kernel(int n, SweepDev L, int chain,
   L.dr[(size_t)s * L.C + chain].y = R;
 }
 
+// residual sums of several chains in one pass: the location's observation
+// list and y read once, per chain exactly residual_sums_kernel's sum
+__global__ void residual_sums_jobs_kernel(int n, SweepDev L, ResJobs J, const int* __restrict__ obs_ptr,
+                                          const int* __restrict__ obs_idx, const double* __restrict__ y) {
+  int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  int loc = L.compact_loc[s];
+  double R[kMaxChains] = {0.0, 0.0, 0.0, 0.0};
+  for (int p = obs_ptr[loc]; p < obs_ptr[loc + 1]; ++p) {
+    int o = obs_idx[p];
+    const double yo = y[o];
+#pragma unroll
+    for (int j = 0; j < kMaxChains; ++j)
+      if (j < J.M) R[j] += yo - (J.mu[j] ? J.mu[j][o] : J.beta0[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < kMaxChains; ++j)
+    if (j < J.M) L.dr[(size_t)s * L.C + J.chain[j]].y = R[j];
+}
+
+hipError_t launch_residual_sums_jobs(hipStream_t st, int n, const SweepDev& L, const ResJobs& J,
+                                     const int* obs_ptr, const int* obs_idx, const double* y) {
+  if (J.M < 1 || J.M > kMaxChains) return hipErrorInvalidValue;
+  int g = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(residual_sums_jobs_kernel, dim3(g), dim3(kBlock), 0, st, n, L, J, obs_ptr, obs_idx, y);
+  return hipGetLastError();
+}
+
 hipError_t launch_residual_sums(hipStream_t st, int n, const SweepDev& L, int chain, const int* obs_ptr,
                                 const int* obs_idx, const double* y, const double* mu, double beta0) {
   int g = (n + kBlock - 1) / kBlock;
@@ -1249,6 +1277,58 @@ __global__ __launch_bounds__(256) void obs_reduce_kernel(int mode, int n_obs, co
     }
   }
   block_sum4(acc, partials + 4 * blockIdx.x);
+}
+
+// obs reductions of several chains in one pass (y and the location map read
+// once): per chain exactly obs_reduce_kernel's terms, accumulation order and
+// block partials (the same grid), partials of chain job j at j x kRedBlocks x 4
+template <int MJ>
+__global__ __launch_bounds__(256) void obs_reduce_jobs_kernel(int mode, int n_obs, const double* __restrict__ y,
+                                                              const int* __restrict__ lm, ObsJobs J,
+                                                              double* __restrict__ partials) {
+  double acc[MJ][4];
+#pragma unroll
+  for (int j = 0; j < MJ; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[j][q] = 0.0;
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < n_obs; o += gridDim.x * blockDim.x) {
+    const double yo = y[o];
+    const int loc = lm[o];
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) {
+      if (j >= J.M) continue;
+      const double m = J.mu[j] ? J.mu[j][o] : J.beta0[j];
+      if (mode == 0) {
+        double e = yo - J.f[j][loc] - m + J.beta0[j];
+        acc[j][0] += e * e;
+      } else {
+        double ea = yo - (J.fnew[j][loc] + m - J.beta0[j]);
+        double eb = yo - (J.f[j][loc] + m - J.beta0[j]);
+        acc[j][0] += (eb * eb - ea * ea) * J.inv_2var[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < MJ; ++j)
+    if (j < J.M) {
+      block_sum4(acc[j], partials + (size_t)j * kRedBlocks * 4 + 4 * blockIdx.x);
+      __syncthreads();  // block_sum4's LDS is reused by the next chain
+    }
+}
+
+int launch_obs_reduce_jobs(hipStream_t st, int mode, int n_obs, const double* y, const int* lm, const ObsJobs& J,
+                           double* partials) {
+  int g = (n_obs + kBlock - 1) / kBlock;
+  if (g > kRedBlocks) g = kRedBlocks;
+  if (g < 1) g = 1;
+  switch (J.M) {
+    case 1: hipLaunchKernelGGL(obs_reduce_jobs_kernel<1>, dim3(g), dim3(kBlock), 0, st, mode, n_obs, y, lm, J, partials); break;
+    case 2: hipLaunchKernelGGL(obs_reduce_jobs_kernel<2>, dim3(g), dim3(kBlock), 0, st, mode, n_obs, y, lm, J, partials); break;
+    case 3: hipLaunchKernelGGL(obs_reduce_jobs_kernel<3>, dim3(g), dim3(kBlock), 0, st, mode, n_obs, y, lm, J, partials); break;
+    case 4: hipLaunchKernelGGL(obs_reduce_jobs_kernel<4>, dim3(g), dim3(kBlock), 0, st, mode, n_obs, y, lm, J, partials); break;
+    default: return -1;
+  }
+  return g;
 }
 
 int launch_obs_reduce(hipStream_t st, int mode, int n_obs, const double* y, const double* mu,

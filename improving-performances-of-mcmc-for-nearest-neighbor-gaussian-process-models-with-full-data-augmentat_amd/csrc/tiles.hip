@@ -1596,8 +1596,8 @@ __global__ __launch_bounds__(256) void tile_refresh_kernel(TileDev D, const int4
                                                            int NT, const int* __restrict__ cell_src,
                                                            const int* __restrict__ gsrc,
                                                            const double* __restrict__ linv, int chain) {
-  __shared__ double sq[4096];
-  __shared__ unsigned char endf[4096];
+  __shared__ double sq[kRefreshCells];
+  __shared__ unsigned char endf[kRefreshCells];
   // U independent gathers in flight per thread
   constexpr int U = 8;
   const int t = threadIdx.x;
@@ -1618,10 +1618,11 @@ __global__ __launch_bounds__(256) void tile_refresh_kernel(TileDev D, const int4
     }
     return;
   }
-  const int4 B = D.batch[o.y];
+  // a run of o.z consecutive batches of one tile (wave-local batches are small:
+  // several per item), their cells one contiguous range of the stream
+  const int4 B0 = D.batch[o.y], BL = D.batch[o.y + o.z - 1];
   double* cv = const_cast<double*>(D.cell_val) + (size_t)chain * D.n_cells;
-  const int R = B.y & 0xFFFF;
-  const int ncell = R * NT;
+  const int ncell = BL.x + (BL.y & 0xFFFF) * NT - B0.x;
   for (int e00 = t; e00 < ncell; e00 += U * 256) {
     int src[U];
     unsigned pk[U];
@@ -1629,8 +1630,8 @@ __global__ __launch_bounds__(256) void tile_refresh_kernel(TileDev D, const int4
 #pragma unroll
     for (int q = 0; q < U; ++q) {
       const int e0 = e00 + q * 256;
-      src[q] = e0 < ncell ? __builtin_nontemporal_load(cell_src + B.x + e0) : -1;
-      pk[q] = e0 < ncell ? __builtin_nontemporal_load(D.cell_pk + B.x + e0) : 0u;
+      src[q] = e0 < ncell ? __builtin_nontemporal_load(cell_src + B0.x + e0) : -1;
+      pk[q] = e0 < ncell ? __builtin_nontemporal_load(D.cell_pk + B0.x + e0) : 0u;
     }
 #pragma unroll
     for (int q = 0; q < U; ++q) v[q] = src[q] >= 0 ? linv[src[q]] : 0.0;
@@ -1638,32 +1639,46 @@ __global__ __launch_bounds__(256) void tile_refresh_kernel(TileDev D, const int4
     for (int q = 0; q < U; ++q) {
       const int e0 = e00 + q * 256;
       if (e0 < ncell) {
-        cv[B.x + e0] = v[q];
-        const int f = (e0 % NT) * R + e0 / NT;  // e0 = j*NT + thread
-        sq[f] = v[q] * v[q];
-        endf[f] = (pk[q] & kTEnd) ? 1 : 0;
+        cv[B0.x + e0] = v[q];
+        sq[e0] = v[q] * v[q];
+        endf[e0] = (pk[q] & kTEnd) ? 1 : 0;
       }
     }
   }
   __syncthreads();
-  if (t < B.z) {
-    const int x = B.w + t;
+  // per slot: the sum of squares of its cells in stream order f (cell f of a
+  // batch at (f % R) * NT + f / R)
+  const int nslots = BL.w + BL.z - B0.w;
+  for (int u = t; u < nslots; u += 256) {
+    const int x = B0.w + u;
+    int b = o.y;
+    while (x >= D.batch[b].w + D.batch[b].z) ++b;
+    const int4 B = D.batch[b];
+    const int R = B.y & 0xFFFF, rel = B.x - B0.x;
     const int f0 = D.sinfo[x].y & 0xFFFFF;
     double s = 0.0;
     for (int f = f0;; ++f) {
-      s += sq[f];
-      if (endf[f]) break;
+      const int e = rel + (f % R) * NT + f / R;
+      s += sq[e];
+      if (endf[e]) break;
     }
     D.dr[(size_t)x * D.C + chain].x = s;
   }
 }
 
-std::vector<int4> tile_refresh_order(const std::vector<int>& batch_ptr, const std::vector<int>& gptr, int T, int K,
-                                     int& olen) {
+std::vector<int4> tile_refresh_order(const std::vector<int>& batch_ptr, const std::vector<int>& gptr,
+                                     const std::vector<TileBatch>& batch, int NT, int T, int K, int& olen) {
   std::vector<std::vector<int4>> lists(kRefreshLists);
   for (int t = 0; t < T; ++t) {
     std::vector<int4>& l = lists[(size_t)t * kRefreshLists / T];
-    for (int q = batch_ptr[(size_t)t * K]; q < batch_ptr[(size_t)(t + 1) * K]; ++q) l.push_back(make_int4(0, q, 0, 0));
+    // runs of consecutive batches of the tile with at most kRefreshCells cells
+    const int q1 = batch_ptr[(size_t)(t + 1) * K];
+    for (int q = batch_ptr[(size_t)t * K]; q < q1;) {
+      int nb = 0, cells = 0;
+      while (q + nb < q1 && (nb == 0 || cells + batch[q + nb].R * NT <= kRefreshCells)) cells += batch[q + nb++].R * NT;
+      l.push_back(make_int4(0, q, nb, 0));
+      q += nb;
+    }
     const int g1 = gptr[(size_t)(t + 1) * K];
     for (int g = gptr[(size_t)t * K]; g < g1; g += 2048) l.push_back(make_int4(1, g, std::min(g + 2048, g1), 0));
   }

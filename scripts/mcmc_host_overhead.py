@@ -80,6 +80,13 @@ class FakeCtx:
     def loglik_pair_chains(self, mask, b0, lsp, lsc):
         return self.rng.normal(size=self.n_chains), self.rng.normal(size=self.n_chains)
 
+    def ancillary_step_chains(self, mask, covfun, cps, b0, dls, lnv):
+        return np.zeros(self.n_chains, np.int32), self.rng.normal(size=self.n_chains)
+
+    def sufficient_step_chains(self, mask, covfun, cps, b0, lsp, lsc):
+        return (np.zeros(self.n_chains, np.int32), self.rng.normal(size=self.n_chains),
+                self.rng.normal(size=self.n_chains))
+
     def sum_squared_residuals_chains(self, mask, b0):
         return np.full(self.n_chains, 0.25 * self.n)
 
