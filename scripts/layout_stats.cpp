@@ -35,7 +35,24 @@ int main(int argc, char** argv) {
     int R = 0, cells = 0;
     for (int q = L.batch_ptr[t*K+c]; q < L.batch_ptr[t*K+c+1]; ++q) { R += L.batch[q].R; cells += L.batch[q].nthr; }
     Rtc[t*K+c] = R;
+    if (WAVES > 0) {  // wave-local: the critical R = sum over rounds of the round's max R
+      const int b0 = L.batch_ptr[t*K+c], b1 = L.batch_ptr[t*K+c+1];
+      int crit = 0;
+      for (int r0 = b0; r0 < b1; r0 += WAVES) {
+        int rm = 0;
+        for (int q = r0; q < std::min(b1, r0 + WAVES); ++q) rm = std::max(rm, L.batch[q].R);
+        crit += rm;
+      }
+      Rtc[t*K+c] = crit;
+      ctc[t*K+c] = (b1 - b0 + WAVES - 1) / WAVES;  // rounds
+    }
   }
+  if (WAVES > 0)
+    for (int c = 0; c < K; ++c) {
+      int r1 = 0, r2 = 0, r3 = 0;
+      for (int t = 0; t < T; ++t) { const int r = ctc[t*K+c]; r1 += r == 1; r2 += r == 2; r3 += r >= 3; }
+      if (r2 + r3) printf("c%2d tiles with 1 / 2 / 3+ wave rounds: %d / %d / %d\n", c, r1, r2, r3);
+    }
   // per colour: mean R, max R, mean over tiles of max R over neighbours
   double tot_mean = 0, tot_nbmax = 0, tot_max = 0, gh = 0, fs = 0;
   for (int c = 0; c < K; ++c) {
