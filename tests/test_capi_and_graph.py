@@ -249,6 +249,26 @@ def test_tile_sweep_emulation_wave_local_interior_first(tile_check_exe, n, m, ti
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
 
 
+def test_interior_first_wave_local_barrier_counts_match():
+    """Interior-first wave-local tiles (tiles.hip tile_phase_wlib, opt-in): the
+    cell waves pass three workgroup barriers per phase (A: the hand-off is in,
+    B: the ghost adds are done, C: the boundary batches are done) and the
+    exchange wave's lagged phase (tile_phase_xw<..., LAG = 1>) must pass the
+    same three, also at ph = 0 where it has nothing to hand off; a mismatch
+    pairs barriers wrongly (an LDS race or a spin timeout)."""
+    src = (next(ROOT.glob("*_amd")) / "csrc" / "tiles.hip").read_text()
+    wlib = src.split("void tile_phase_wlib(", 1)[1].split("\n}\n", 1)[0]
+    assert wlib.count("__syncthreads()") == 3, wlib.count("__syncthreads()")
+    xw = src.split("void tile_phase_xw(", 1)[1].split("\n}\n", 1)[0]
+    first = xw.split("if (LAG && ph == 0) {", 1)[1].split("return;", 1)[0]
+    assert first.count("__syncthreads()") == 3
+    # the lagged phase (wave-local: no own-batch barriers): after the polls,
+    # after the ghost adds, and C (not in the epilogue ph = nph)
+    rest = xw.split("return;", 1)[1].split("// hand-off: every (foreign slot, chain)", 1)[1]
+    assert "if (LAG && ph < S.nph) __syncthreads();" in rest
+    assert rest.count("__syncthreads()") == 3, rest.count("__syncthreads()")
+
+
 def test_exchange_wave_barrier_count_matches_own_draw():
     """The exchange wave of a tile (tiles.hip tile_phase_xw) holds no cells and
     passes the own batches' workgroup barriers by count: kOwnDrawBarriers must
