@@ -525,10 +525,14 @@ def main():
         # capture every call shape of the timed region before it: the first
         # call of a shape (and of its warm form) captures and instantiates a
         # hipGraph (capi.hip graph_for), which must not land inside t0..t1.
-        # Two calls per shape: the second is warm (warm mode) or cold (cold
-        # mode, beta_0 alternates) -- the form every timed call takes
+        # The second call of a shape is warm (warm mode) or cold (cold mode,
+        # beta_0 alternates) -- the form every timed call takes; eight calls
+        # per shape so the device has run the timed shape for ~20 ms before
+        # t0 whatever --warmup is (measured at the driver's --steps 20:
+        # --warmup 5 with two priming calls 12.44-12.47k against 12.66-12.72k
+        # at --warmup 20; with four 12.78k against 12.87-12.88k)
         for s in sorted({min(nc, steps)} | ({steps % nc} if steps % nc else set())):
-            for _ in range(2):
+            for _ in range(8):
                 call(s, 1 << 40)
         sync = (lambda: torch.cuda.synchronize(local_rank)) if torch.cuda.is_available() else (lambda: None)
         return timed_region(run, steps, warmup, dist, sync)
