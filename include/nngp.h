@@ -181,7 +181,10 @@ int nngp_loglik(nngp_ctx* ctx, int which, double beta0, double log_scale, double
 
 /* n_sweeps chromatic sweeps (A1).  Normals: Philox4x32-10 with key = seed,
  * counter = (location, counter_base + sweep, 0x5EED) unless z != NULL, in which
- * case z (n_sweeps x n row-major, z[s*n + i]) supplies them. */
+ * case z (n_sweeps x n row-major, z[s*n + i]) supplies them.  Stream-ordered:
+ * the call may return before the sweeps have run (the only tile context of a
+ * device; NNGP_SWEEP_SYNC=1 waits); every entry point that hands results to
+ * the host waits for them, and reports a tile timeout of an earlier sweep. */
 int nngp_sweep(nngp_ctx* ctx, int n_sweeps, double beta0, double log_scale,
                double log_noise_variance, uint64_t seed, uint64_t counter_base,
                const double* z);
