@@ -711,8 +711,11 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       // count).  Measured at the headline: 12.96k vs 12.47k chain-sweeps/s at
       // 3 chains (2,218 vs 2,275 us per 10-sweep launch), 5.76k vs 7.09k at 1
       // chain
+      // Not by default with r in global memory: at configs[4]'s per-GPU share
+      // (n = 1.25e6, m = 20, 3 chains) 2,702 vs 2,819 chain-sweeps/s, at
+      // n = 1e7 one chain 284 vs 364.
       const char* twl = std::getenv("NNGP_TILE_WL");
-      const bool wl_env = twl ? std::string(twl) == "1" : n_chains >= 3;
+      const bool wl_env = twl ? std::string(twl) == "1" : (n_chains >= 3 && !rg_forced);
       // interior-first layouts run on wave-local batches (tiles.hip
       // tile_phase_wlib) or, without the exchange wave, on workgroup batches
       const bool xw = !csplit && (!split || wl_env) && (!rg_forced || wl_env) && NT == 512 && xwm == 1;
