@@ -532,6 +532,10 @@ hipError_t launch_factor(hipStream_t st, int family, double var, double nugget, 
     if (b <= 12) return launch_factor_ds<12, 1>(st, ds, NNGP_FACTOR_ARGS);
     return launch_factor_ds<16, 1>(st, ds, NNGP_FACTOR_ARGS);
   }
+  if (b <= 21) {  // m = 20 (configs[4]): the local block in registers, part of L spilled
+    if (family == 0) return launch_factor_ds<21, 0>(st, ds, NNGP_FACTOR_ARGS);
+    return launch_factor_ds<21, 1>(st, ds, NNGP_FACTOR_ARGS);
+  }
   if (family == 0) return launch_factor_rt<0>(st, ds, NNGP_FACTOR_ARGS);
   return launch_factor_rt<1>(st, ds, NNGP_FACTOR_ARGS);
 }
