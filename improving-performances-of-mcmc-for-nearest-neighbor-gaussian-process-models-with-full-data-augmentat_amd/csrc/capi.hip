@@ -576,6 +576,28 @@ void nngp_ctx_destroy(nngp_ctx* c) {
 const char* nngp_ctx_last_error(const nngp_ctx* c) { return c ? c->err.c_str() : g_err.c_str(); }
 
 // shard_G > 0: a rank of the colour-sharded sweep (colour-launch engine)
+// the longest column of B (entries of a location in the NNarray rows)
+static int max_column_length(const int* nn, int n, int b) {
+  std::vector<int> cl(n, 0);
+  int mx = 0;
+  for (long long e = 0; e < (long long)n * b; ++e)
+    if (nn[e] >= 0) mx = std::max(mx, ++cl[nn[e]]);
+  return mx;
+}
+
+// lanes per chain of the colour engine's chunks (a column must fit one chunk
+// of LW x kRowsMax entries): 3 chains use the 4-chain shape (measured faster
+// than 21 lanes) unless a column is longer than its 256 entries (m = 20:
+// up to 275), then 21 lanes (336 entries)
+static int colour_lanes(int C, int max_col) {
+  if (const char* e = std::getenv("NNGP_COLOUR_LANES"))  // tests: 21 lanes at 3 chains
+    if (C == 3 && std::atoi(e) == 21) return 21;
+  if (C == 1) return 64;
+  if (C == 2) return 32;
+  if (C == 3 && max_col > 16 * kRowsMax) return 21;
+  return 16;
+}
+
 static int ctx_create(const double* locs, int n, int d, const int* NNarray, int b, const int* coloring,
                       const int* locs_match, const double* observed_field, int n_obs, int n_chains,
                       int device, int shard_G, int shard_rank, nngp_ctx** out) {
@@ -680,14 +702,8 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       // (LW x kRowsMax entries, 256 at 3-4 chains: configs[4]'s m = 20 graph
       // at 3 chains); tiles whose r does not fit the LDS then run with r in
       // global memory rather than fail
-      const int col_cap = (n_chains == 1 ? 64 : (n_chains == 2 ? 32 : 16)) * kRowsMax;
-      int max_col = 0;
-      {
-        std::vector<int> cl(n, 0);
-        for (long long e = 0; e < (long long)n * b; ++e)
-          if (nn[e] >= 0) max_col = std::max(max_col, ++cl[nn[e]]);
-      }
-      const bool colours_refuse = max_col > col_cap;
+      const int max_col = max_column_length(nn.data(), n, b);
+      const bool colours_refuse = max_col > colour_lanes(n_chains, max_col) * kRowsMax;
       const bool rows_beyond_lds = (long long)(n / std::max(T, 1)) * n_chains * 8 > (long long)lds_max;
       const bool rg_forced = (std::getenv("NNGP_TILE_R") && std::string(std::getenv("NNGP_TILE_R")) == "global") ||
                              (rows_beyond_lds && colours_refuse && NT == 512);
@@ -863,8 +879,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     Lw.LW = 0; Lw.nchunks = 0;
     Lw.n_entries = (long long)c->tl.cell_pk.size() + (long long)c->tl.gsrc.size();
   } else {
-    // lanes per chain: 3 chains use the 4-chain shape (measured faster than 21 lanes)
-    const int LW = n_chains == 1 ? 64 : (n_chains == 2 ? 32 : 16);
+    const int LW = colour_lanes(n_chains, max_column_length(nn.data(), n, b));
     if (!build_sweep_layout(nn.data(), n, b, coloring, locs, d, LW, c->lay, err)) {
       delete c;
       return fail_msg(nullptr, NNGP_ERR_ARG, err);

@@ -882,6 +882,7 @@ hipError_t launch_sell_refresh(hipStream_t st, const SweepDev& L, int nchunks, c
     case 64: hipLaunchKernelGGL(sell_refresh_kernel<64>, dim3(g), dim3(kBlock), 0, st, L, nchunks, ent_src, linv, chain); break;
     case 32: hipLaunchKernelGGL(sell_refresh_kernel<32>, dim3(g), dim3(kBlock), 0, st, L, nchunks, ent_src, linv, chain); break;
     case 16: hipLaunchKernelGGL(sell_refresh_kernel<16>, dim3(g), dim3(kBlock), 0, st, L, nchunks, ent_src, linv, chain); break;
+    case 21: hipLaunchKernelGGL(sell_refresh_kernel<21>, dim3(g), dim3(kBlock), 0, st, L, nchunks, ent_src, linv, chain); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -1218,6 +1219,7 @@ hipError_t launch_sweep_color(hipStream_t st, const SweepDev& L, const ColorLaun
     case 64: hipLaunchKernelGGL((sweep_color_kernel<64>), dim3(gs + gz), dim3(kBlock), 0, st, L, a); break;
     case 32: hipLaunchKernelGGL((sweep_color_kernel<32>), dim3(gs + gz), dim3(kBlock), 0, st, L, a); break;
     case 16: hipLaunchKernelGGL((sweep_color_kernel<16>), dim3(gs + gz), dim3(kBlock), 0, st, L, a); break;
+    case 21: hipLaunchKernelGGL((sweep_color_kernel<21>), dim3(gs + gz), dim3(kBlock), 0, st, L, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

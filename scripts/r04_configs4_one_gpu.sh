@@ -1,6 +1,7 @@
 #!/bin/bash
 # configs[4] (n = 1e7, m = 20, 3 chains) on ONE GPU: the bench line under a rocprofv3 kernel-trace/stats run
-# (r in global memory: 240 MB of r cannot live in 40 MB of LDS)
+# (colour engine on 21-lane chunks since the end of round 4; before that r in global memory: 240 MB of r
+# cannot live in 40 MB of LDS)
 cd $GRAFT_REPO_ROOT
 ROOTDIR=$(pwd); export TMPDIR=/tmp
 mkdir -p gpurun_out

@@ -384,6 +384,55 @@ def test_batched_chains_bitwise_equal_single_chain_contexts(P, O, n, m, C):
     np.testing.assert_allclose(got[0], ref, rtol=1e-7, atol=1e-8)
 
 
+@pytest.mark.parametrize("n,m", [(6000, 20), (60000, 15)])
+def test_colour_engine_21_lanes_three_chains(P, O, monkeypatch, n, m):
+    """The colour engine at 3 chains on 21 lanes per chain (its layout when a
+    column of B is longer than the 16-lane chunk's 256 entries: m = 20 at
+    n >= ~1e6, configs[4] on one GPU; forced here by NNGP_COLOUR_LANES=21):
+    every chain bitwise equal to the same context's chain swept alone, equal
+    to rounding to a 1-chain context, chain 0 to the oracle."""
+    monkeypatch.setenv("NNGP_ENGINE", "colors")
+    monkeypatch.setenv("NNGP_COLOUR_LANES", "21")
+    C = 3
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=n + m)
+    rng = np.random.default_rng(m)
+    cps = [[1.0 + 0.2 * k, 0.05 + 0.01 * k, 0.1 * k] for k in range(C)]
+    fields = [rng.normal(size=n) for _ in range(C)]
+    b0, ls, lnv = [0.2 * k for k in range(C)], [0.1 - 0.05 * k for k in range(C)], [-0.3 + 0.1 * k for k in range(C)]
+    seeds, bases = [99 + k for k in range(C)], [7 + 3 * k for k in range(C)]
+
+    def setup(ctx):
+        for k in range(C):
+            ctx.select(k)
+            ctx.factor(0, "matern15_isotropic", cps[k])
+            ctx.set_field(fields[k])
+            ctx.set_mu(None, b0[k])
+
+    with P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=C) as ctx:
+        assert ctx.info["sweep_engine"] == 0 and ctx.info["lanes_per_chain"] == 21, ctx.info
+        setup(ctx)
+        ctx.sweep_chains(4, b0, ls, lnv, seeds, bases)
+        got = [ctx.select(k).get_field() for k in range(C)]
+        Lo0 = ctx.select(0).get_linv(0)
+    with P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=C) as seq:
+        setup(seq)
+        for k in range(C):
+            seq.select(k).sweep(4, b0[k], ls[k], lnv[k], seeds[k], bases[k])
+        for k in range(C):
+            np.testing.assert_array_equal(got[k], seq.select(k).get_field())
+    for k in range(C):
+        with P.ChainContext(locs, NN, col, lm, y, device=0) as one:
+            one.factor(0, "matern15_isotropic", cps[k])
+            one.set_field(fields[k])
+            one.set_mu(None, b0[k])
+            one.sweep(4, b0[k], ls[k], lnv[k], seeds[k], bases[k])
+            np.testing.assert_allclose(got[k], one.get_field(), rtol=1e-11, atol=1e-12)
+    z = O.sweep_normals(seeds[0], bases[0], 4, n)
+    ref = O.sweep("local", fields[0], Lo0, NN, col, O.precision_diag(Lo0, NN), np.ones(n, np.int32), y,
+                  np.full(n, b0[0]), lm, b0[0], ls[0], lnv[0], z)
+    np.testing.assert_allclose(got[0], ref, rtol=1e-7, atol=1e-8)
+
+
 def test_single_chain_sweep_inside_batched_context(P, O):
     """nngp_sweep on one chain of a 3-chain context leaves the other chains
     untouched and equals the oracle (injected normals)."""
