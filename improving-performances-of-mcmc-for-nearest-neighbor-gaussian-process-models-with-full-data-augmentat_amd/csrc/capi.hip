@@ -134,7 +134,8 @@ struct nngp_ctx {
   int* level_ptr_d = nullptr;    // DAG level offsets (device copy)
   std::vector<int> tri_seg;      // solve plan: (lv0, lv1, kind) triples, kind 1 = one-workgroup run
   bool tri_dag = false;          // NNGP_TRI=dag: one sync-free launch for the whole DAG
-  unsigned* tri_tmo_d = nullptr; // its timeout word
+  bool tri_rescue = false;       // NNGP_TRI_RESCUE=1: its ticket order from the start (tests)
+  unsigned* tri_tmo_d = nullptr; // its control words: [0] timeout, [1] rescue, [2..3] rescue tickets
   unsigned* tri_tmo_h = nullptr; // pinned copy, read at the next host sync
   int* obs_ptr_d = nullptr;
   int* obs_idx_d = nullptr;
@@ -190,8 +191,9 @@ struct nngp_ctx {
   std::string engine_note;        // why this sweep engine (nngp_ctx_engine_note)
   int tstagger = 0;               // chain-split: start offset per chain (NNGP_TILE_STAGGER, 100 MHz ticks)
   double* rg_d = nullptr;         // sum of the tiles' local rows x C
-  unsigned* ctl_d = nullptr;      // [0] call id, [1] timeout word
-  unsigned* tmo_h = nullptr;      // pinned copy of the timeout word after each launch
+  unsigned* ctl_d = nullptr;      // [0] call id, [1] timeout word of a launch, [2] sticky timeout (tiles.hip)
+  unsigned* tmo_h = nullptr;      // pinned copy of the sticky timeout word after each launch
+  int inject_tmo = 0;             // tests (NNGP_TILE_INJECT_TIMEOUT=k): the first k sweep calls report a timeout
   unsigned long long* tdbg_d = nullptr;  // NNGP_PROBE=9: per-tile phase times, =2: per-phase timeline
   size_t tdbg_n = 0;
   int tprobe = 0;
@@ -277,9 +279,12 @@ hipError_t upload(T* dst, const T* src, size_t count, hipStream_t st) {
   return hipMemcpyAsync(dst, src, sizeof(T) * count, hipMemcpyHostToDevice, st);
 }
 
+// (after a host sync) the sticky timeout word of the launches since the last
+// check: reported once, then cleared on the device too
 static int tile_timeout_check(nngp_ctx* c) {
   if (c->engine == 1 && c->tmo_h && *c->tmo_h != 0) {
     *c->tmo_h = 0;
+    HIPCHK(c, hipMemsetAsync(c->ctl_d + 2, 0, sizeof(unsigned), c->st));
     return fail_msg(c, NNGP_ERR_HIP, "tile sweep: neighbour wait timed out (tiles not co-resident?)");
   }
   return NNGP_OK;
@@ -408,9 +413,12 @@ int flush_sweep_values(nngp_ctx* c, int mask) {
     J.beta0[J.M] = S.mu_beta0;
     J.chain[J.M] = k;
     ++J.M;
-    S.res_stale = false;
   }
-  if (J.M) HIPCHK(c, launch_residual_sums_jobs(c->st, c->n, sweep_dev(c), J, c->obs_ptr_d, c->obs_idx_d, c->y_d));
+  if (J.M) {
+    HIPCHK(c, launch_residual_sums_jobs(c->st, c->n, sweep_dev(c), J, c->obs_ptr_d, c->obs_idx_d, c->y_d));
+    // up to date only once the pass is enqueued (a failed launch leaves them stale)
+    for (int q = 0; q < J.M; ++q) c->ch[J.chain[q]].res_stale = false;
+  }
   for (int k = 0; k < c->C; ++k)
     if (((mask >> k) & 1) && c->ch[k].vals_stale) {
       int rc = flush_one(c, k);
@@ -647,6 +655,9 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     std::vector<int> f(obs_cnt.begin(), obs_cnt.end() - 1);
     for (int o = 0; o < n_obs; ++o) obs_idx[f[lm0[o]]++] = o;
   }
+  // the longest column of B, once (a scan of the n x b NNarray: 2e8 entries at
+  // configs[4]): the engine choice and the colour chunks' lanes use it
+  const int max_col = max_column_length(nn.data(), n, b);
   // sweep engine: tiles (one persistent launch per call, r resident in LDS)
   // when the tile layout fits a CU's LDS, else one launch per colour.
   // NNGP_ENGINE=colors|tiles forces one; NNGP_TILES=T sets the tile count.
@@ -702,7 +713,6 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       // (LW x kRowsMax entries, 256 at 3-4 chains: configs[4]'s m = 20 graph
       // at 3 chains); tiles whose r does not fit the LDS then run with r in
       // global memory rather than fail
-      const int max_col = max_column_length(nn.data(), n, b);
       const bool colours_refuse = max_col > colour_lanes(n_chains, max_col) * kRowsMax;
       const bool rows_beyond_lds = (long long)(n / std::max(T, 1)) * n_chains * 8 > (long long)lds_max;
       const bool rg_forced = (std::getenv("NNGP_TILE_R") && std::string(std::getenv("NNGP_TILE_R")) == "global") ||
@@ -879,7 +889,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     Lw.LW = 0; Lw.nchunks = 0;
     Lw.n_entries = (long long)c->tl.cell_pk.size() + (long long)c->tl.gsrc.size();
   } else {
-    const int LW = colour_lanes(n_chains, max_column_length(nn.data(), n, b));
+    const int LW = colour_lanes(n_chains, max_col);
     if (!build_sweep_layout(nn.data(), n, b, coloring, locs, d, LW, c->lay, err)) {
       delete c;
       return fail_msg(nullptr, NNGP_ERR_ARG, err);
@@ -992,6 +1002,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     CK(dalloc(&c->ctl_d, 4));
     CK(hipHostMalloc((void**)&c->tmo_h, sizeof(unsigned), hipHostMallocDefault));
     *c->tmo_h = 0;
+    if (const char* e = std::getenv("NNGP_TILE_INJECT_TIMEOUT")) c->inject_tmo = std::atoi(e);
     // device batch record {off, R | nthr << 16, nslots, slot0}
     std::vector<int4> tb(nb);
     for (size_t q = 0; q < nb; ++q) {
@@ -1048,7 +1059,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     if (const char* pr = std::getenv("NNGP_PROBE"))
       if ((std::atoi(pr) == 9 || std::atoi(pr) == 2) && (C == 1 || C == 3)) {
         c->tprobe = std::atoi(pr) == 9 ? 1 : 2;
-        c->tdbg_n = (size_t)TL.T * (c->tprobe == 1 ? 8 : 512 * 8);
+        c->tdbg_n = (size_t)TL.T * (c->tprobe == 1 ? 8 : 512 * 16);  // tiles.hip kTimelinePhases x kTimelineSlots
         CK(dalloc(&c->tdbg_d, c->tdbg_n));
         CK(hipMemsetAsync(c->tdbg_d, 0, sizeof(unsigned long long) * c->tdbg_n, c->st));
       }
@@ -1069,8 +1080,10 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     const char* e = std::getenv("NNGP_TRI");
     const bool per_level = e && std::string(e) == "level";
     c->tri_dag = !per_level && !(e && std::string(e) == "levels");
-    CK(dalloc(&c->tri_tmo_d, 1));
-    CK(hipMemset(c->tri_tmo_d, 0, sizeof(unsigned)));
+    const char* er = std::getenv("NNGP_TRI_RESCUE");
+    c->tri_rescue = er && std::string(er) == "1";
+    CK(dalloc(&c->tri_tmo_d, 4));
+    CK(hipMemset(c->tri_tmo_d, 0, 4 * sizeof(unsigned)));
     CK(hipHostMalloc((void**)&c->tri_tmo_h, sizeof(unsigned), hipHostMallocDefault));
     *c->tri_tmo_h = 0;
     const int L = (int)c->level_ptr.size() - 1;
@@ -1754,7 +1767,7 @@ static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, int mask, const double*
       HIPCHK(c, launch_sweep_tiles(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NTK, c->tl.max_batches,
                                     c->tl.max_gslots));
     }
-    HIPCHK(c, hipMemcpyAsync(c->tmo_h, c->ctl_d + 1, sizeof(unsigned), hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipMemcpyAsync(c->tmo_h, c->ctl_d + 2, sizeof(unsigned), hipMemcpyDeviceToHost, c->st));
   }
   if ((parts & kColours) && c->engine == 0) {
     const size_t zn = (size_t)n * c->C;
@@ -1886,6 +1899,10 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
     hipGraphExec_t ex;
     if ((rc = graph_for(c, n_sweeps, mask, &ex, warm ? kColours | kEpilogue : kAll))) return rc;
     HIPCHK(c, hipGraphLaunch(ex, c->st));
+    if (c->inject_tmo > 0 && c->engine == 1) {
+      --c->inject_tmo;
+      HIPCHK(c, launch_tile_inject_timeout(c->st, c->ctl_d));
+    }
   }
   if (async) {
     c->tile_pending = c->engine == 1;
@@ -1920,6 +1937,10 @@ int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const doub
   hipGraphExec_t ex;
   if ((rc = graph_for(c, n_sweeps, all, &ex, warm ? kColours | kEpilogue : kAll))) return rc;
   HIPCHK(c, hipGraphLaunch(ex, c->st));
+  if (c->inject_tmo > 0 && c->engine == 1) {
+    --c->inject_tmo;
+    HIPCHK(c, launch_tile_inject_timeout(c->st, c->ctl_d));
+  }
   if (async) {
     c->tile_pending = c->engine == 1;
     if (tlk.owns_lock()) tlk.unlock();
@@ -2066,7 +2087,7 @@ static int tile_ipc_exchange(nngp_ctx* c, bool full) {
   }
   HIPCHK(c, launch_tile_xsignal(c->st, pf, c->xseq, c->tG, c->trank));
   HIPCHK(c, launch_tile_xwait(c->st, c->xflag_d, c->ctl_d, c->xseq, c->tG, c->trank));
-  HIPCHK(c, hipMemcpyAsync(c->tmo_h, c->ctl_d + 1, sizeof(unsigned), hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipMemcpyAsync(c->tmo_h, c->ctl_d + 2, sizeof(unsigned), hipMemcpyDeviceToHost, c->st));
   return NNGP_OK;
 }
 
@@ -2148,7 +2169,7 @@ static int tile_shard_call(nngp_ctx* c, int n_sweeps, int mask) {
   a.z_in = nullptr;
   hipError_t e = launch_sweep_tiles(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NTK, c->tl.max_batches,
                                     c->tl.max_gslots, &sh, c->tTl);
-  if (e == hipSuccess) e = hipMemcpyAsync(c->tmo_h, c->ctl_d + 1, sizeof(unsigned), hipMemcpyDeviceToHost, c->st);
+  if (e == hipSuccess) e = hipMemcpyAsync(c->tmo_h, c->ctl_d + 2, sizeof(unsigned), hipMemcpyDeviceToHost, c->st);
   // the broadcasts go out even after a failed launch: the peers wait in them
   rc = tile_shard_exchange(c);
   if (e != hipSuccess || rc) {
@@ -2346,7 +2367,7 @@ static int tile_group_call(nngp_ctx** ctxs, int G, int n_sweeps, const double* b
     GCHK(L, launch_sweep_tiles(L->st, devs[g0], a, L->tl.max_rows, L->tl.NTK, L->tl.max_batches, L->tl.max_gslots, &sh,
                                (g1 - g0) * Tl));
     for (int h = g0; h < g1; ++h)
-      GCHK(L, hipMemcpyAsync(ctxs[h]->tmo_h, ctxs[h]->ctl_d + 1, sizeof(unsigned), hipMemcpyDeviceToHost, L->st));
+      GCHK(L, hipMemcpyAsync(ctxs[h]->tmo_h, ctxs[h]->ctl_d + 2, sizeof(unsigned), hipMemcpyDeviceToHost, L->st));
     for (int h = g0; h < g1; ++h) GCHK(L, hipEventRecord(ev[G + h], L->st));
     g0 = g1;
   }
@@ -2524,7 +2545,7 @@ int nngp_get_sweep_r(nngp_ctx* c, double* r) {
 static int tri_solve_dev(nngp_ctx* c, const TriArgs& ta, const double* u, double* x) {
   if (c->tri_dag) {
     HIPCHK(c, launch_tri_dag(c->st, ta, c->level_rows_d, c->n, c->nn_d, c->b, u, x, (long long)c->n * ta.stride,
-                             c->tri_tmo_d));
+                             c->tri_tmo_d, c->tri_rescue));
     HIPCHK(c, hipMemcpyAsync(c->tri_tmo_h, c->tri_tmo_d, sizeof(unsigned), hipMemcpyDeviceToHost, c->st));
     return NNGP_OK;
   }
@@ -2706,6 +2727,14 @@ static int step_common(nngp_ctx* c, int chain_mask, int covfun, const double* co
   return NNGP_OK;
 }
 
+// an error after step_common's provisional marking: no masked chain keeps a
+// proposal factor whose outcome was never settled (accept_factor refuses it)
+static int step_abort(nngp_ctx* c, int chain_mask, int rc) {
+  for (int k = 0; k < c->C; ++k)
+    if ((chain_mask >> k) & 1) c->ch[k].have_factor[1] = false;
+  return rc;
+}
+
 static int step_collect(nngp_ctx* c, int chain_mask, int* status, int* failed) {
   HIPCHK(c, hipMemcpyAsync(c->res_h, c->res_d, kResBytes, hipMemcpyDeviceToHost, c->st));
   { int ss_ = sync_stream(c); if (ss_) return ss_; }
@@ -2727,9 +2756,9 @@ int nngp_ancillary_step_chains(nngp_ctx* c, int chain_mask, int covfun, const do
     return fail_msg(c, NNGP_ERR_ARG, "ancillary_step_chains: bad args");
   int rc, failed = 0;
   if ((rc = step_common(c, chain_mask, covfun, covparms, ncp, true, "ancillary_step_chains"))) return rc;
-  if ((rc = nngp_ancillary_propose_chains(c, chain_mask, beta0, dlog_scale))) return rc;
-  if ((rc = obs_chains_enqueue(c, 1, chain_mask, beta0, lnv, false))) return rc;
-  if ((rc = step_collect(c, chain_mask, status, &failed))) return rc;
+  if ((rc = nngp_ancillary_propose_chains(c, chain_mask, beta0, dlog_scale))) return step_abort(c, chain_mask, rc);
+  if ((rc = obs_chains_enqueue(c, 1, chain_mask, beta0, lnv, false))) return step_abort(c, chain_mask, rc);
+  if ((rc = step_collect(c, chain_mask, status, &failed))) return step_abort(c, chain_mask, rc);
   for (int k = 0; k < c->C; ++k)
     if ((chain_mask >> k) & 1) ratio[k] = ((failed >> k) & 1) ? std::nan("") : c->res_h[4 * k];
   return NNGP_OK;
@@ -2750,8 +2779,8 @@ int nngp_sufficient_step_chains(nngp_ctx* c, int chain_mask, int covfun, const d
     if ((chain_mask >> k) & 1) jobs[nj++] = {k, 1, beta0[k], log_scale_prop[k], ll_prop + k};
   for (int k = 0; k < c->C; ++k)
     if ((chain_mask >> k) & 1) jobs[nj++] = {k, 0, beta0[k], log_scale_cur[k], ll_cur + k};
-  if ((rc = loglik_jobs_enqueue(c, jobs, nj, false))) return rc;
-  if ((rc = step_collect(c, chain_mask, status, &failed))) return rc;
+  if ((rc = loglik_jobs_enqueue(c, jobs, nj, false))) return step_abort(c, chain_mask, rc);
+  if ((rc = step_collect(c, chain_mask, status, &failed))) return step_abort(c, chain_mask, rc);
   loglik_jobs_finish(c, jobs, nj, failed);
   return NNGP_OK;
 }

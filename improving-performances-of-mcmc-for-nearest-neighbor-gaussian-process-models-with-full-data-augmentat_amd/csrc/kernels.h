@@ -261,6 +261,8 @@ hipError_t launch_sweep_tiles_cs(hipStream_t st, const TileDev& D, const TileLau
                                  int max_batches, int max_gslots, int* occ = nullptr);
 // ctl[0] += 1 (call id), ctl[1] = 0 (timeout word): before every launch of a rank
 hipError_t launch_tile_call_bump(hipStream_t st, unsigned* ctl);
+// tests: the control words a launch whose tiles timed out leaves behind
+hipError_t launch_tile_inject_timeout(hipStream_t st, unsigned* ctl);
 // tile shard, w exchange by peer copies instead of RCCL: signal the peers
 // (flag word `rank` of every other rank := call id), wait for theirs
 struct TilePeerFlags { unsigned* f[kTileRanksMax] = {}; };
@@ -304,9 +306,12 @@ hipError_t launch_tri_levels_block(hipStream_t st, const TriArgs& a, const int* 
                                    int lv1, const int* nn, int b, const double* u, double* x);
 // the whole DAG in one sync-free launch (rows = all levels back to back,
 // nrows of them); x (x_len doubles) is overwritten with a pending sentinel
-// first; *tmo is set if a wait timed out
+// first; ctl: 4 words -- [0] set if a wait timed out (sticky until the host
+// clears it), [1] the rescue word, [2..3] the rescue ticket counter (both
+// reset by the launch; kernels.hip tri_dag_kernel); rescue: every wave takes
+// the ticket order from the start (tests)
 hipError_t launch_tri_dag(hipStream_t st, const TriArgs& a, const int* rows, int nrows, const int* nn, int b,
-                          const double* u, double* x, long long x_len, unsigned* tmo);
+                          const double* u, double* x, long long x_len, unsigned* ctl, bool rescue = false);
 // y[i] = shift + scale * x[i*xstride]
 // dst[i] = src[idx[i]] (gather) / dst[idx[i]] = src[i] (scatter), i < n:
 // R order <-> device row order of a field-sized vector

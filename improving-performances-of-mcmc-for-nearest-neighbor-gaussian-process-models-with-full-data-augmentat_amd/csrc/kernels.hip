@@ -1440,92 +1440,143 @@ hipError_t launch_tri_levels_block(hipStream_t st, const TriArgs& a, const int* 
 // level order (rows[] holds the levels back to back, chains interleaved);
 // wave w takes items 4w.., 4(w+W).., ... (16 lanes per item, as tri_row16:
 // the same products, the same DPP row reduction, so x is bitwise the level
-// kernels' x).  Progress: the grid is at most the resident waves, so the
-// lowest unfinished item always sits in a running wave whose every earlier
-// item is done, and it only reads lower items.  Inside a wave the 4 items
-// are retried until all are done (an item may read one of the same wave), and
-// every wave's waits are bounded: on a timeout the word *tmo is set, the
-// unfinished entries stay NaN and the waves leave.
+// kernels' x).  Inside a wave the 4 items are retried until all are done (an
+// item may read one of the same wave), and every wave's waits are bounded: on
+// a timeout the word ctl[0] is set, the unfinished entries stay NaN and the
+// waves leave.
+// Progress does not rest on residency or dispatch order.  The static striding
+// is fast when every wave of the grid runs, but a wave that is not resident
+// (another launch holds CUs -- e.g. a persistent tile sweep of another
+// context, which in turn waits for CUs this launch holds) would leave its
+// items undone and the running waves waiting on them.  So a wave that has
+// waited on one group for kTriRescueTicks raises the rescue word ctl[1]; from
+// then on every running wave (and every wave that starts later) takes groups
+// in increasing order from ONE ticket counter (ctl[2..3], a returning device
+// atomic per group), skipping groups already done.  The claimed groups are
+// always a prefix of the item order, so the lowest unfinished item is held by
+// a running wave whose inputs (lower items) are all done: it completes, at any
+// residency.  An item computed twice (a static wave and a rescuer) stores the
+// same bits.
 constexpr unsigned long long kTriPending = 0x7FF4A5A5DEAD5A5Aull;
+constexpr unsigned long long kTriRescueTicks = 2000000;  // 20 ms of the 100 MHz clock on one group
 
 __device__ __forceinline__ double tri_load_dev(const double* p) {
   return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
+// one group of 4 items (16 lanes each) from item `base`.  Returns 0 when all
+// four are done, 1 on a timeout (ctl[0] set), 2 when the group was left
+// undone because a rescue is on (watch: the static pass).  skip: items whose
+// x is already stored count as done (rescue mode: another wave computed them)
+template <int BMAX>
+__device__ __forceinline__ int tri_dag_group(const TriArgs& a, const int* __restrict__ rows, long long nitems,
+                                             const int* __restrict__ nn, int b, const double* __restrict__ u,
+                                             double* x, unsigned* ctl, long long base, bool watch, bool skip) {
+  constexpr int J = BMAX / 16;
+  const int l = threadIdx.x & 15, sub = (threadIdx.x >> 4) & 3;
+  const int S = a.stride;
+  const long long it = base + sub;
+  const bool active = it < nitems;
+  const int i = active ? rows[it / a.nc] : 0;
+  const int kk = active ? (int)(it % a.nc) : 0;
+  const int k = a.kidx[kk];
+  const double* lr = a.linv[kk] + (size_t)i * b;
+  bool done = !active;
+  if (skip && active) {
+    const double v = tri_load_dev(x + (size_t)i * S + k);
+    done = __builtin_bit_cast(unsigned long long, v) != kTriPending;
+  }
+  if (__ballot(!done) == 0) return 0;
+  int idx[J];
+  double lv[J], xv[J];
+  bool have[J];
+#pragma unroll
+  for (int q = 0; q < J; ++q) {
+    const int j = l + 16 * q;
+    idx[q] = (active && j >= 1 && j < b) ? __builtin_nontemporal_load(nn + (size_t)i * b + j) : -1;
+    lv[q] = idx[q] >= 0 ? __builtin_nontemporal_load(lr + j) : 0.0;
+    xv[q] = 0.0;
+    have[q] = idx[q] < 0;
+  }
+  const double ui = (active && l == 15) ? u[(size_t)i * S + k] : 0.0;
+  const double d0 = (active && l == 15) ? lr[0] : 1.0;
+  const unsigned long long t0 = watch ? wall_clock64() : 0ull;
+  for (unsigned spins = 0;; ++spins) {
+    bool ready = true;
+#pragma unroll
+    for (int q = 0; q < J; ++q) {
+      if (!have[q]) {
+        const double v = tri_load_dev(x + (size_t)idx[q] * S + k);
+        if (__builtin_bit_cast(unsigned long long, v) != kTriPending) {
+          xv[q] = v;
+          have[q] = true;
+        } else {
+          ready = false;
+        }
+      }
+    }
+    const unsigned long long bal = __ballot(ready);
+    const bool grp = ((bal >> (16 * sub)) & 0xFFFFull) == 0xFFFFull;
+    double p = 0.0;
+#pragma unroll
+    for (int q = 0; q < J; ++q) p = __builtin_fma(lv[q], xv[q], p);
+    p += dpp_f64<0x111, 0xF, true>(p);  // row_shr:1
+    p += dpp_f64<0x112, 0xF, true>(p);  // row_shr:2
+    p += dpp_f64<0x114, 0xF, true>(p);  // row_shr:4
+    p += dpp_f64<0x118, 0xF, true>(p);  // row_shr:8 -> lane 15 holds the row sum
+    if (!done && grp) {
+      if (l == 15)
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(x + (size_t)i * S + k),
+                           __builtin_bit_cast(unsigned long long, (ui - p) / d0), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      done = true;
+    }
+    if (__ballot(!done) == 0) return 0;
+    // (wave-uniform: the control words are read by the first lane only)
+    if ((spins & 255u) == 255u) {
+      if (spins > (1u << 22) ||
+          __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        __hip_atomic_store(ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 1;
+      }
+      if (watch) {
+        if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+          return 2;
+        if (wall_clock64() - t0 > kTriRescueTicks) {
+          __hip_atomic_store(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          return 2;
+        }
+      }
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 template <int BMAX>
 __global__ __launch_bounds__(256) void tri_dag_kernel(TriArgs a, const int* __restrict__ rows, long long nitems,
                                                       const int* __restrict__ nn, int b,
                                                       const double* __restrict__ u, double* x,
-                                                      unsigned* __restrict__ tmo) {
-  constexpr int J = BMAX / 16;
-  const int l = threadIdx.x & 15, sub = (threadIdx.x >> 4) & 3;
+                                                      unsigned* __restrict__ ctl) {
   const long long W = (long long)gridDim.x * (blockDim.x >> 6);
   const long long w = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  const int S = a.stride;
-  bool quit = false;
-  for (long long base = 4 * w; base < nitems && !quit; base += 4 * W) {
-    const long long it = base + sub;
-    const bool active = it < nitems;
-    const int i = active ? rows[it / a.nc] : 0;
-    const int kk = active ? (int)(it % a.nc) : 0;
-    const int k = a.kidx[kk];
-    const double* lr = a.linv[kk] + (size_t)i * b;
-    int idx[J];
-    double lv[J], xv[J];
-    bool have[J];
-#pragma unroll
-    for (int q = 0; q < J; ++q) {
-      const int j = l + 16 * q;
-      idx[q] = (active && j >= 1 && j < b) ? __builtin_nontemporal_load(nn + (size_t)i * b + j) : -1;
-      lv[q] = idx[q] >= 0 ? __builtin_nontemporal_load(lr + j) : 0.0;
-      xv[q] = 0.0;
-      have[q] = idx[q] < 0;
-    }
-    const double ui = (active && l == 15) ? u[(size_t)i * S + k] : 0.0;
-    const double d0 = (active && l == 15) ? lr[0] : 1.0;
-    bool done = !active;
-    for (unsigned spins = 0;; ++spins) {
-      bool ready = true;
-#pragma unroll
-      for (int q = 0; q < J; ++q) {
-        if (!have[q]) {
-          const double v = tri_load_dev(x + (size_t)idx[q] * S + k);
-          if (__builtin_bit_cast(unsigned long long, v) != kTriPending) {
-            xv[q] = v;
-            have[q] = true;
-          } else {
-            ready = false;
-          }
-        }
-      }
-      const unsigned long long bal = __ballot(ready);
-      const bool grp = ((bal >> (16 * sub)) & 0xFFFFull) == 0xFFFFull;
-      double p = 0.0;
-#pragma unroll
-      for (int q = 0; q < J; ++q) p = __builtin_fma(lv[q], xv[q], p);
-      p += dpp_f64<0x111, 0xF, true>(p);  // row_shr:1
-      p += dpp_f64<0x112, 0xF, true>(p);  // row_shr:2
-      p += dpp_f64<0x114, 0xF, true>(p);  // row_shr:4
-      p += dpp_f64<0x118, 0xF, true>(p);  // row_shr:8 -> lane 15 holds the row sum
-      if (!done && grp) {
-        if (l == 15)
-          __hip_atomic_store(reinterpret_cast<unsigned long long*>(x + (size_t)i * S + k),
-                             __builtin_bit_cast(unsigned long long, (ui - p) / d0), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        done = true;
-      }
-      if (__ballot(!done) == 0) break;
-      // (wave-uniform: the timeout word is read by the first lane only)
-      if (spins > (1u << 22) ||
-          ((spins & 255u) == 255u &&
-           __builtin_amdgcn_readfirstlane(__hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))) {
-        __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        quit = true;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
+  bool rescue = __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  for (long long base = 4 * w; base < nitems && !rescue; base += 4 * W) {
+    const int r = tri_dag_group<BMAX>(a, rows, nitems, nn, b, u, x, ctl, base, true, false);
+    if (r == 1) return;
+    rescue = r == 2;
+  }
+  // a rescue raised while this wave was in its static pass (or after it):
+  // help, in ticket order
+  if (!rescue) rescue = __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (!rescue) return;
+  unsigned long long* head = reinterpret_cast<unsigned long long*>(ctl + 2);
+  for (;;) {
+    unsigned long long g = 0;
+    if ((threadIdx.x & 63) == 0) g = __hip_atomic_fetch_add(head, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    g = __shfl(g, 0);
+    if ((long long)g * 4 >= nitems) return;
+    if (tri_dag_group<BMAX>(a, rows, nitems, nn, b, u, x, ctl, (long long)g * 4, false, true) == 1) return;
   }
 }
 
@@ -1534,8 +1585,22 @@ __global__ void fill_u64_kernel(long long n, unsigned long long v, unsigned long
     p[e] = v;
 }
 
+// x := the pending sentinel; the rescue word (:= rescue: every wave goes
+// straight to the ticket order -- NNGP_TRI_RESCUE=1, the tests' way to check
+// that order) and the ticket counter of the tri_dag launch that follows := 0
+// (the timeout word ctl[0] stays set until the host has read it)
+__global__ void tri_dag_init_kernel(long long n, double* __restrict__ x, unsigned* __restrict__ ctl, unsigned rescue) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    ctl[1] = rescue;
+    *reinterpret_cast<unsigned long long*>(ctl + 2) = 0ull;
+  }
+  unsigned long long* p = reinterpret_cast<unsigned long long*>(x);
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x)
+    p[e] = kTriPending;
+}
+
 hipError_t launch_tri_dag(hipStream_t st, const TriArgs& a, const int* rows, int nrows, const int* nn, int b,
-                          const double* u, double* x, long long x_len, unsigned* tmo) {
+                          const double* u, double* x, long long x_len, unsigned* ctl, bool rescue) {
   const auto kern = b <= 16 ? tri_dag_kernel<16> : tri_dag_kernel<32>;
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
@@ -1548,9 +1613,8 @@ hipError_t launch_tri_dag(hipStream_t st, const TriArgs& a, const int* rows, int
   long long g = std::min<long long>((long long)cus * per_cu, (nitems + 15) / 16);
   if (g < 1) g = 1;
   const int gf = (int)std::min<long long>((x_len + 255) / 256, 4096);
-  hipLaunchKernelGGL(fill_u64_kernel, dim3(gf > 0 ? gf : 1), dim3(256), 0, st, x_len, kTriPending,
-                     reinterpret_cast<unsigned long long*>(x));
-  hipLaunchKernelGGL(kern, dim3((int)g), dim3(256), 0, st, a, rows, nitems, nn, b, u, x, tmo);
+  hipLaunchKernelGGL(tri_dag_init_kernel, dim3(gf > 0 ? gf : 1), dim3(256), 0, st, x_len, x, ctl, rescue ? 1u : 0u);
+  hipLaunchKernelGGL(kern, dim3((int)g), dim3(256), 0, st, a, rows, nitems, nn, b, u, x, ctl);
   return hipGetLastError();
 }
 

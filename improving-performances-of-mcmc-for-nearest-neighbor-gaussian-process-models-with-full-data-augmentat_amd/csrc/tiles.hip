@@ -67,9 +67,27 @@ hipError_t launch_set_ptr(hipStream_t st, const double** dst, int k, const doubl
   return hipGetLastError();
 }
 
+// ctl: [0] call id, [1] the launch's timeout word (its tiles stop waiting once
+// it is set), [2] the sticky copy the host reads: a timeout stays reported
+// until the host has seen it (capi.hip tile_timeout_check clears it), however
+// many launches follow before the next host sync
 __global__ void tile_call_bump_kernel(unsigned* ctl) {
   ctl[0] += 1u;  // call id (never 0 inside a launch)
-  ctl[1] = 0u;   // timeout word
+  ctl[1] = 0u;   // timeout word of this launch
+}
+
+__device__ __forceinline__ void tile_timeout_raise(unsigned* tmo) {
+  __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(tmo + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// tests (NNGP_TILE_INJECT_TIMEOUT=k: after each of the first k sweep calls of
+// a context): what a launch whose tiles timed out leaves in ctl
+__global__ void tile_inject_timeout_kernel(unsigned* ctl) { tile_timeout_raise(ctl + 1); }
+
+hipError_t launch_tile_inject_timeout(hipStream_t st, unsigned* ctl) {
+  hipLaunchKernelGGL(tile_inject_timeout_kernel, dim3(1), dim3(1), 0, st, ctl);
+  return hipGetLastError();
 }
 
 hipError_t launch_tile_call_bump(hipStream_t st, unsigned* ctl) {
@@ -94,7 +112,7 @@ __global__ void tile_xwait_kernel(const unsigned* __restrict__ xflag, unsigned* 
     for (unsigned spins = 0;; ++spins) {
       if (__hip_atomic_load(xflag + h, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == call) break;
       if (spins > (1u << 22)) {
-        __hip_atomic_store(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        tile_timeout_raise(ctl + 1);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -331,10 +349,11 @@ __device__ __forceinline__ void tile_ghost_adds(TileState& S, const TileGhostReg
 // NNGP_PROBE=2 timeline: thread 0 of every tile stores the 100 MHz clock at
 // points k of phase S.ph (no waits added besides the clock read's own)
 constexpr int kTimelinePhases = 512;
+constexpr int kTimelineSlots = 16;  // stamps per phase (capi.hip allocates T x phases x slots)
 #define TLSTAMP(S, k)                                                                         \
   do {                                                                                        \
     if (PROBE == 2 && (S).t == 0 && (S).ph < kTimelinePhases)                                 \
-      D.dbg[((size_t)(S).T * kTimelinePhases + (S).ph) * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+      D.dbg[((size_t)(S).T * kTimelinePhases + (S).ph) * kTimelineSlots + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
 
@@ -640,7 +659,7 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
         // has given up (timeout word), the others stop waiting within ~1k polls
         if (S.timed_out || spins > (1u << 20) ||
             ((spins & 1023u) == 1023u && __hip_atomic_load(S.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-          if (!S.timed_out) __hip_atomic_store(S.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (!S.timed_out) tile_timeout_raise(S.tmo);
           S.timed_out = true;
           break;
         }
@@ -653,7 +672,7 @@ __device__ __forceinline__ void tile_phase(const TileDev& D, const TileLaunch& a
   __syncthreads();
   TLSTAMP(S, 2);
   if (PROBE == 2 && t == 0 && S.ph < kTimelinePhases) {
-    D.dbg[((size_t)S.T * kTimelinePhases + S.ph) * 8 + 5] = *S.spin_s;
+    D.dbg[((size_t)S.T * kTimelinePhases + S.ph) * kTimelineSlots + 5] = *S.spin_s;
     *S.spin_s = 0;
   }
   for (int gb = g0; gb < g1; gb += NT * GMAX) {
@@ -747,7 +766,7 @@ __device__ __forceinline__ void tile_phase_ib(const TileDev& D, const TileLaunch
           }
           if (S.timed_out || spins > (1u << 20) ||
               ((spins & 1023u) == 1023u && __hip_atomic_load(S.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-            if (!S.timed_out) __hip_atomic_store(S.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!S.timed_out) tile_timeout_raise(S.tmo);
             S.timed_out = true;
             break;
           }
@@ -759,7 +778,7 @@ __device__ __forceinline__ void tile_phase_ib(const TileDev& D, const TileLaunch
     }
     __syncthreads();
     if (PROBE == 2 && t == 0 && S.ph < kTimelinePhases) {
-      D.dbg[((size_t)S.T * kTimelinePhases + S.ph) * 8 + 5] = *S.spin_s;
+      D.dbg[((size_t)S.T * kTimelinePhases + S.ph) * kTimelineSlots + 5] = *S.spin_s;
       *S.spin_s = 0;
     }
     for (int gb = g0; gb < g1; gb += NT * GMAX) {
@@ -807,13 +826,15 @@ __device__ __forceinline__ void wave_lds_order() { asm volatile("s_waitcnt lgkmc
 
 template <int C, int RMAX, int PROBE, int SH>
 __device__ __forceinline__ void tile_own_wl(const TileDev& D, const TileLaunch& a, const TileShard& sh, TileState& S,
-                                            TileBatchRegs<C, 64, RMAX>& b, unsigned epoch, double* acc_w) {
+                                            TileBatchRegs<C, 64, RMAX>& b, unsigned epoch, double* acc_w,
+                                            bool first = false) {
   constexpr int IMAX = TileBatchRegs<C, 64, RMAX>::IMAX;
   const int lane = S.lane;
   const double* __restrict__ r_s = S.r_s;
   double* __restrict__ acc_s = acc_w;
   const int R = b.R, nit = b.ns * C;
   tile_cells_landed(b);
+  if (first) TLSTAMP(S, 8);
   double run[C], cont[C];
   int cont_q = -1;
   bool seen_start = false;
@@ -924,7 +945,7 @@ __device__ __forceinline__ void tile_phase_wl(const TileDev& D, const TileLaunch
       tile_load_batch<C, 64, RMAX, SH>(D, S.batch_s[bi], cur, lane);
       tile_prep_items<C, 64, RMAX>(D, a, S.sc_s, S.seed_s, s, cur, lane);
     }
-    tile_own_wl<C, RMAX, PROBE, SH>(D, a, sh, S, cur, epoch, acc_w);
+    tile_own_wl<C, RMAX, PROBE, SH>(D, a, sh, S, cur, epoch, acc_w, bi == bfirst);
     const int R = cur.R;
     if (bi + W >= bend) {  // this wave's last batch of the colour: its records are dead
       if (!DB && more) tile_load_items<C, 64, RMAX, SH>(D, S.batch_s[bnext], nxt, lane);
@@ -1139,7 +1160,7 @@ __device__ __forceinline__ void tile_phase_xw(const TileDev& D, TileState& S, in
       // has given up (timeout word), the others stop waiting within ~1k polls
       if (S.timed_out || spins > (1u << 20) ||
           ((spins & 1023u) == 1023u && __hip_atomic_load(S.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-        if (!S.timed_out) __hip_atomic_store(S.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!S.timed_out) tile_timeout_raise(S.tmo);
         S.timed_out = true;
 #pragma unroll
         for (int k = 0; k < PB; ++k)
@@ -1153,8 +1174,8 @@ __device__ __forceinline__ void tile_phase_xw(const TileDev& D, TileState& S, in
     }
   }
   if (PROBE == 2 && lane == 0 && S.ph < kTimelinePhases) {
-    D.dbg[((size_t)S.T * kTimelinePhases + S.ph) * 8 + 7] = __builtin_amdgcn_s_memrealtime();
-    D.dbg[((size_t)S.T * kTimelinePhases + S.ph) * 8 + 5] = *S.spin_s;
+    D.dbg[((size_t)S.T * kTimelinePhases + S.ph) * kTimelineSlots + 7] = __builtin_amdgcn_s_memrealtime();
+    D.dbg[((size_t)S.T * kTimelinePhases + S.ph) * kTimelineSlots + 5] = *S.spin_s;
     *S.spin_s = 0;
   }
   __syncthreads();

@@ -33,7 +33,7 @@ for rep in range(4):
     ctx.sweep_chains(S, *args, [rep * S] * C)
     el = time.perf_counter() - t
 nph = S * K
-raw = np.fromfile(out, dtype=np.uint64).reshape(T, 512, 8)[:, :nph]
+raw = np.fromfile(out, dtype=np.uint64).reshape(T, 512, 16)[:, :nph]  # tiles.hip kTimelineSlots
 spins = raw[..., 5].astype(np.float64)
 d = raw[..., [0, 1, 2, 3, 4, 6]].astype(np.float64) / 100.0  # us
 miss = d[..., 1] == 0              # (tile, colour) with no own batch: no publish stamp
@@ -55,6 +55,15 @@ xwd = raw[..., 7].astype(np.float64)
 if (xwd > 0).any():  # exchange-wave tiles: the wave's polls done (stamp 7)
     xw = np.where(xwd > 0, xwd / 100.0 - raw[:, 0, 0].astype(np.float64).min() / 100.0, hand)
     print(f"  xw polls done - publish: mean {(xw - pub).mean():6.2f}  p90 {np.percentile(xw - pub, 90):6.2f}")
+# round 5 stamp (wave-local tiles): 8 = the phase's first batch's cells
+# landed in wave 0
+t8 = raw[..., 8].astype(np.float64)
+if (t8 > 0).any():
+    base = raw[:, 0, 0].astype(np.float64).min()
+    ok8 = t8 > 0
+    landed8 = np.where(ok8, t8 / 100.0 - base / 100.0, start)
+    print(f"  start->cells landed  mean {(landed8 - start)[ok8].mean():6.2f}  (wave 0, phases with a batch)")
+    print(f"  cells landed->publish mean {(pub - landed8)[ok8].mean():6.2f}")
 print(f"  poll spins (max over the tile's threads): mean {spins.mean():.2f}, p90 {np.percentile(spins, 90):.0f}, "
       f"share of phases with spins {(spins > 0).mean():.2f}")
 # critical path: per phase, the spread of publish times across tiles
