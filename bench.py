@@ -625,6 +625,11 @@ def main():
                                         "(NNGP_SWEEP_WARM=0: rebuild every call)"
                                         if os.environ.get("NNGP_SWEEP_WARM", "1") != "0" and info["sweep_engine"] == 1
                                         else "cold: w -> slots and r = B w rebuilt every call"),
+                      "value_is": ("warm-call throughput: consecutive n_chromatic-sweep calls with nothing "
+                                   "changed in between; an MCMC iteration redraws beta_0 and runs a cold "
+                                   "call (cold_calls)"
+                                   if os.environ.get("NNGP_SWEEP_WARM", "1") != "0" and info["sweep_engine"] == 1
+                                   else "cold-call throughput"),
                       "single_chain": single,
                       "cold_calls": cold_calls,
                       "parallelism": f"chains {C} per GPU x {world} GPUs (independent)"},

@@ -8,6 +8,7 @@ one chain of a context with the single-chain interface.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -321,9 +322,33 @@ class ChainView:
         self.ctx.close()
 
 
+def _lds_fallback(ctx) -> bool:
+    """The context runs the colour engine only because its tiles do not fit a
+    CU's LDS at its chain count (engine_fallback 1, note names the LDS)."""
+    inf = ctx.info
+    return inf["sweep_engine"] == 0 and inf["engine_fallback"] == 1 and "LDS" in inf["engine_note"]
+
+
+def _open_group(locs, NNarray, coloring, locs_match, observed_field, dev, group):
+    """Contexts for the chains `group` of one device: one context, or -- when
+    its tile layout exceeds the LDS at this chain count (4 chains at the
+    headline n = 1e6: r of a tile's 5.2k local rows x 4 x 8 B > 160 KB) --
+    the two halves of the group as separate contexts, recursively, which run
+    the tile engine (2 chains: ~112 KB) instead of the colour engine.
+    NNGP_SPLIT_CHAINS=0 keeps one context per group."""
+    ctx = ChainContext(locs, NNarray, coloring, locs_match, observed_field, device=dev, n_chains=len(group))
+    if len(group) < 2 or os.environ.get("NNGP_SPLIT_CHAINS", "1") == "0" or not _lds_fallback(ctx):
+        return [(ctx, group)]
+    ctx.close()
+    h = (len(group) + 1) // 2
+    return (_open_group(locs, NNarray, coloring, locs_match, observed_field, dev, group[:h]) +
+            _open_group(locs, NNarray, coloring, locs_match, observed_field, dev, group[h:]))
+
+
 def make_chain_views(locs, NNarray, coloring, locs_match, observed_field, n_chains: int, devices=None):
-    """Chains dealt round-robin over `devices`, then packed <= 4 per context:
-    returns one ChainView per chain (chain i -> views[i])."""
+    """Chains dealt round-robin over `devices`, then packed <= 4 per context
+    (split further where the tile engine needs it, _open_group): returns one
+    ChainView per chain (chain i -> views[i])."""
     devices = list(devices) if devices else [-1]
     per_dev = {}
     for i in range(n_chains):
@@ -331,11 +356,10 @@ def make_chain_views(locs, NNarray, coloring, locs_match, observed_field, n_chai
     views = [None] * n_chains
     for dev, chains in per_dev.items():
         for g in range(0, len(chains), MAX_CHAINS_PER_CONTEXT):
-            group = chains[g:g + MAX_CHAINS_PER_CONTEXT]
-            ctx = ChainContext(locs, NNarray, coloring, locs_match, observed_field, device=dev,
-                               n_chains=len(group))
-            for k, i in enumerate(group):
-                views[i] = ctx.view(k)
+            for ctx, group in _open_group(locs, NNarray, coloring, locs_match, observed_field, dev,
+                                          chains[g:g + MAX_CHAINS_PER_CONTEXT]):
+                for k, i in enumerate(group):
+                    views[i] = ctx.view(k)
     return views
 
 

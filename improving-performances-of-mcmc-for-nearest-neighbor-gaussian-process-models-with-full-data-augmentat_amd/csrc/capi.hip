@@ -190,6 +190,7 @@ struct nngp_ctx {
   int engine_fallback = 0;        // 0: none, 1: tile layout unsuitable (LDS, shape), 2: residency, 3: forced colours
   std::string engine_note;        // why this sweep engine (nngp_ctx_engine_note)
   int tstagger = 0;               // chain-split: start offset per chain (NNGP_TILE_STAGGER, 100 MHz ticks)
+  int tvariant = 0;               // NNGP_TILE_VARIANT (probe builds): experiment bits
   double* rg_d = nullptr;         // sum of the tiles' local rows x C
   unsigned* ctl_d = nullptr;      // [0] call id, [1] timeout word of a launch, [2] sticky timeout (tiles.hip)
   unsigned* tmo_h = nullptr;      // pinned copy of the sticky timeout word after each launch
@@ -1060,6 +1061,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       if ((std::atoi(pr) == 9 || std::atoi(pr) == 2) && (C == 1 || C == 3)) {
         c->tprobe = std::atoi(pr) == 9 ? 1 : 2;
         c->tdbg_n = (size_t)TL.T * (c->tprobe == 1 ? 8 : 512 * 16);  // tiles.hip kTimelinePhases x kTimelineSlots
+        if (const char* v = std::getenv("NNGP_TILE_VARIANT")) c->tvariant = std::atoi(v);
         CK(dalloc(&c->tdbg_d, c->tdbg_n));
         CK(hipMemsetAsync(c->tdbg_d, 0, sizeof(unsigned long long) * c->tdbg_n, c->st));
       }
@@ -1759,6 +1761,7 @@ static int enqueue_sweep_body(nngp_ctx* c, int n_sweeps, int mask, const double*
     a.n_sweeps = n_sweeps;
     a.chain_mask = mask;
     a.z_in = z_dev;
+    a.variant = c->tvariant;
     if (c->tcs) {
       a.stagger = c->tstagger;
       HIPCHK(c, launch_sweep_tiles_cs(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NTK, c->tl.max_batches,
@@ -1956,6 +1959,9 @@ int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const doub
       HIPCHK(c, hipMemcpy(h.data(), c->tdbg_d, h.size() * 8, hipMemcpyDeviceToHost));
       if (FILE* f = std::fopen(path, "wb")) {
         std::fwrite(h.data(), 8, h.size(), f);
+        // then the neighbour tiles of each (tile, colour) (timeline.py: skew vs transit)
+        std::fwrite(c->tl.nb_ptr.data(), sizeof(int), c->tl.nb_ptr.size(), f);
+        std::fwrite(c->tl.nb.data(), sizeof(int), c->tl.nb.size(), f);
         std::fclose(f);
       }
     }

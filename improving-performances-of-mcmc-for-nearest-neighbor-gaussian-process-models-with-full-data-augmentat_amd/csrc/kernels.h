@@ -222,6 +222,7 @@ struct TileLaunch {
   int chain_mask;
   const double* z_in;         // injected normals, per sweep: slot x C (nullptr: Philox inline)
   int stagger = 0;            // chain-split: chain k starts k x stagger ticks (100 MHz) late
+  int variant = 0;            // NNGP_TILE_VARIANT: experiment bits (probe builds only)
 };
 
 // cells per thread of an own batch (the layout's RMAX): two batches of C

@@ -242,7 +242,7 @@ __device__ __forceinline__ void tile_load_batch(const TileDev& D, const int4 B, 
 template <int C, int NT, int RMAX, int CS = C>
 __device__ __forceinline__ void tile_prep_items(const TileDev& D, const TileLaunch& a, const double* sc_s,
                                                 const unsigned long long* seed_s, int s,
-                                                TileBatchRegs<C, NT, RMAX>& b, int t) {
+                                                TileBatchRegs<C, NT, RMAX>& b, int t, int var = 0) {
 #pragma unroll
   for (int k = 0; k < TileBatchRegs<C, NT, RMAX>::IMAX; ++k) {
     const int u = t + k * NT;
@@ -250,10 +250,14 @@ __device__ __forceinline__ void tile_prep_items(const TileDev& D, const TileLaun
       const int q = u / C, ch = u - q * C;
       const double inv_s2 = sc_s[2 * ch], inv_t2 = sc_s[2 * ch + 1];
       double z = 0.0;
-      if (a.z_in) z = a.z_in[((size_t)s * D.n + b.x0 + q) * CS + ch];
+      // var (NNGP_TILE_VARIANT, probe timing experiments only, wrong results):
+      // 2 = no normals, 4 = no records
+      if (var & 2) z = 0.0;
+      else if (a.z_in) z = a.z_in[((size_t)s * D.n + b.x0 + q) * CS + ch];
       else z = normal_loc(seed_s[2 * ch], seed_s[2 * ch + 1] + s, (uint32_t)b.loc[k]);
-      const double P = b.a0[k] * inv_s2 + (double)b.nobs[k] * inv_t2;
-      const double cR = inv_t2 * b.a1[k] + inv_s2 * (b.a0[k] * b.w[k]);
+      const double a0 = (var & 4) ? 1.0 : b.a0[k], a1 = (var & 4) ? 0.5 : b.a1[k], wk = (var & 4) ? 0.0 : b.w[k];
+      const double P = a0 * inv_s2 + (double)((var & 4) ? 1 : b.nobs[k]) * inv_t2;
+      const double cR = inv_t2 * a1 + inv_s2 * (a0 * wk);
       b.a0[k] = cR;
       b.a1[k] = 1.0 / P;
       b.zs[k] = z / sqrt(P);
@@ -355,6 +359,9 @@ constexpr int kTimelineSlots = 16;  // stamps per phase (capi.hip allocates T x 
     if (PROBE == 2 && (S).t == 0 && (S).ph < kTimelinePhases)                                 \
       D.dbg[((size_t)(S).T * kTimelinePhases + (S).ph) * kTimelineSlots + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+// (wave-local tiles: slot 9 + w = wave w's last publish of the phase, so the
+// host can tell the neighbours' skew from the hand-off's transit; the dump
+// appends the neighbour lists, scripts/timeline.py)
 
 
 // one step of a segmented inclusive scan (flag f = "a segment starts here or
@@ -834,7 +841,6 @@ __device__ __forceinline__ void tile_own_wl(const TileDev& D, const TileLaunch& 
   double* __restrict__ acc_s = acc_w;
   const int R = b.R, nit = b.ns * C;
   tile_cells_landed(b);
-  if (first) TLSTAMP(S, 8);
   double run[C], cont[C];
   int cont_q = -1;
   bool seen_start = false;
@@ -915,6 +921,8 @@ __device__ __forceinline__ void tile_own_wl(const TileDev& D, const TileLaunch& 
   }
   wave_lds_order();
   TLSTAMP(S, 1);
+  if (PROBE == 2 && lane == 0 && S.ph < kTimelinePhases && S.wv < 7)
+    D.dbg[((size_t)S.T * kTimelinePhases + S.ph) * kTimelineSlots + 9 + S.wv] = __builtin_amdgcn_s_memrealtime();
 }
 
 // the cell waves' colour phase on wave-local batches.  DB (<= 2 chains, two
@@ -958,7 +966,7 @@ __device__ __forceinline__ void tile_phase_wl(const TileDev& D, const TileLaunch
     if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
   }
   TLSTAMP(S, 6);
-  if (more) tile_prep_items<C, 64, RMAX>(D, a, S.sc_s, S.seed_s, sn, nxt, lane);
+  if (more) tile_prep_items<C, 64, RMAX>(D, a, S.sc_s, S.seed_s, sn, nxt, lane, PROBE == 2 ? a.variant : 0);
   if (!DB && more) tile_load_cells<C, 64, RMAX>(D, S.batch_s[bnext], nxt, lane);
   TLSTAMP(S, 4);
   __syncthreads();  // the exchange wave has every dw of the colour in gdw_s

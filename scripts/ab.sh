@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round 4 A/B measurements cited in DESIGN.md §3 "Round 4" and §5 (one box, variants interleaved by
+# A/B measurement recipes cited in DESIGN.md §3 and §5 (one box, variants interleaved by
 # scripts/ab_env.py: chain-sweeps/s and the sweep kernel's launch time by HIP events).  Usage:
-#   bash scripts/r04_ab.sh wl|prio|c4share|1e7|split|sync
+#   bash scripts/ab.sh wl|prio|c4share|1e7|split|sync
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp

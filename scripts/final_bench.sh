@@ -1,6 +1,6 @@
 #!/bin/bash
-# round 4 final tree, part B: the driver's bench command, the default bench, rocprofv3 kernel stats of the bench
-# and the PMC FETCH/WRITE passes of the sweep kernel
+# the driver's bench command, the default bench, rocprofv3 kernel stats of the bench and the PMC
+# FETCH/WRITE passes of the sweep kernel (scripts/pmc.sh) -> gpurun_out/
 cd $GRAFT_REPO_ROOT
 ROOTDIR=$(pwd); export TMPDIR=/tmp
 mkdir -p gpurun_out

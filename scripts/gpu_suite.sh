@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4 final tree, part A: the full GPU suite and the smoke (the driver's round-end commands)
+# the full GPU suite and the smoke (the driver's round-end commands) -> gpurun_out/pytest_gpu_full.txt, smoke.log
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out; export TMPDIR=/tmp
 timeout -k 10 1050 python -u -m pytest tests -x -q -m gpu --timeout 400 --timeout-method thread > gpurun_out/pytest_gpu_full.txt 2>&1 || { tail -30 gpurun_out/pytest_gpu_full.txt; exit 1; }

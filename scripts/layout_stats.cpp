@@ -26,6 +26,15 @@ int main(int argc, char** argv) {
   for (int c = 0; c < K; ++c) printf("%d ", csz[c]); printf("\n");
   TileLayout L; std::string err;
   if (!build_tile_layout(nn.data(), n, m + 1, col.data(), lo.data(), 2, T, NT, RMAX, L, err, 1, false, WAVES)) { printf("err %s\n", err.c_str()); return 1; }
+  {
+    std::vector<int> lr(T);
+    for (int t = 0; t < T; ++t) lr[t] = L.erow_ptr[t + 1] - L.erow_ptr[t];
+    std::vector<int> srt = lr; std::sort(srt.begin(), srt.end());
+    double mean = 0; for (int v : lr) mean += v; mean /= T;
+    int own_max = 0; for (int t = 0; t < T; ++t) own_max = std::max(own_max, L.tile_row0[t + 1] - L.tile_row0[t]);
+    printf("local rows per tile: mean %.0f p50 %d p90 %d max %d (own rows max %d)\n", mean, srt[T / 2], srt[T * 9 / 10],
+           srt[T - 1], own_max);
+  }
   printf("max_rows %d max_batches %d max_gslots %d cells %zu (nnz %lld, x%.3f) batches %zu\n", L.max_rows, L.max_batches,
          L.max_gslots, L.cell_pk.size(), L.nnz, (double)L.cell_pk.size() / L.nnz, L.batch.size());
   // per (tile, colour): cells, R, ghost cells, foreign slots

@@ -33,7 +33,7 @@ for rep in range(4):
     ctx.sweep_chains(S, *args, [rep * S] * C)
     el = time.perf_counter() - t
 nph = S * K
-raw = np.fromfile(out, dtype=np.uint64).reshape(T, 512, 16)[:, :nph]  # tiles.hip kTimelineSlots
+raw = np.fromfile(out, dtype=np.uint64)[: T * 512 * 16].reshape(T, 512, 16)[:, :nph]  # tiles.hip kTimelineSlots
 spins = raw[..., 5].astype(np.float64)
 d = raw[..., [0, 1, 2, 3, 4, 6]].astype(np.float64) / 100.0  # us
 miss = d[..., 1] == 0              # (tile, colour) with no own batch: no publish stamp
@@ -55,15 +55,37 @@ xwd = raw[..., 7].astype(np.float64)
 if (xwd > 0).any():  # exchange-wave tiles: the wave's polls done (stamp 7)
     xw = np.where(xwd > 0, xwd / 100.0 - raw[:, 0, 0].astype(np.float64).min() / 100.0, hand)
     print(f"  xw polls done - publish: mean {(xw - pub).mean():6.2f}  p90 {np.percentile(xw - pub, 90):6.2f}")
-# round 5 stamp (wave-local tiles): 8 = the phase's first batch's cells
-# landed in wave 0
-t8 = raw[..., 8].astype(np.float64)
-if (t8 > 0).any():
+# slots 9..15 (wave-local tiles): each cell wave's last publish of the phase;
+# with the neighbour lists appended to the dump: the latest publish of the
+# tiles this tile reads granules from -> skew (own publish -> it) and transit
+# (it -> the exchange wave has every granule)
+allraw = np.fromfile(out, dtype=np.uint64)
+tail_i = np.frombuffer(allraw[T * 512 * 16:].tobytes(), dtype=np.int32)
+if tail_i.size > T * K + 1 and (xwd > 0).any() and (raw[..., 9] > 0).any():
+    nb_ptr = tail_i[: T * K + 1]
+    nb = tail_i[T * K + 1:]
     base = raw[:, 0, 0].astype(np.float64).min()
-    ok8 = t8 > 0
-    landed8 = np.where(ok8, t8 / 100.0 - base / 100.0, start)
-    print(f"  start->cells landed  mean {(landed8 - start)[ok8].mean():6.2f}  (wave 0, phases with a batch)")
-    print(f"  cells landed->publish mean {(pub - landed8)[ok8].mean():6.2f}")
+    wp = raw[..., 9:16].astype(np.float64)
+    lastpub = np.where(wp > 0, wp / 100.0 - base / 100.0, -np.inf).max(axis=2)  # (T, nph)
+    lastpub = np.where(np.isfinite(lastpub), lastpub, pub)
+    xwt = np.where(xwd > 0, xwd / 100.0 - base / 100.0, hand)
+    prod = np.full((T, nph), -np.inf)
+    for t_ in range(T):
+        for ph in range(nph):
+            c = ph % K
+            lo, hi = nb_ptr[t_ * K + c], nb_ptr[t_ * K + c + 1]
+            if hi > lo:
+                prod[t_, ph] = lastpub[nb[lo:hi], ph].max()
+    ok = np.isfinite(prod) & (xwd > 0)
+    print(f"  own first publish -> own last publish  mean {(lastpub - pub)[ok].mean():6.2f}")
+    sk = (prod - lastpub)[ok]
+    tr = (xwt - prod)[ok]
+    print(f"  own last publish -> producers' last publish (skew) mean {sk.mean():6.2f}  p10 {np.percentile(sk, 10):6.2f} "
+          f"p90 {np.percentile(sk, 90):6.2f}")
+    print(f"  producers' last publish -> all granules in (transit) mean {tr.mean():6.2f}  p10 {np.percentile(tr, 10):6.2f} "
+          f"p90 {np.percentile(tr, 90):6.2f}")
+    print(f"  phase start -> producers' last publish mean {(prod - start)[ok].mean():6.2f};"
+          f" neighbours per (tile, colour) mean {np.diff(nb_ptr).mean():.1f}")
 print(f"  poll spins (max over the tile's threads): mean {spins.mean():.2f}, p90 {np.percentile(spins, 90):.0f}, "
       f"share of phases with spins {(spins > 0).mean():.2f}")
 # critical path: per phase, the spread of publish times across tiles

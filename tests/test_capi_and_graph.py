@@ -516,3 +516,47 @@ def test_r_shim_wraps_every_abi_entry_point():
     rfun = (root / "rpkg" / "R" / "nngp.R").read_text() + (root / "rpkg" / "R" / "mcmc_nngp_update_Gaussian.R").read_text()
     for c in defined:
         assert c in rfun, f"{c} has no R wrapper"
+
+
+def test_chain_groups_split_where_tiles_exceed_the_lds(P, monkeypatch):
+    """context.make_chain_views: a chain group whose context fell back to the
+    colour engine for the LDS (engine_fallback 1) is reopened as two halves,
+    recursively; other fallbacks and NNGP_SPLIT_CHAINS=0 keep one context
+    (host logic, fake contexts: no GPU)."""
+    opened, closed = [], []
+
+    class Fake:
+        def __init__(self, *a, device=0, n_chains=1):
+            self.n_chains = n_chains
+            opened.append(n_chains)
+            fits = n_chains <= fits_at
+            note = "tiles" if fits else ("colours (tile engine not used: tile layout needs 170000 B of LDS per tile"
+                                         if lds else "colours (tile engine not used: residency)")
+            self.info = {"sweep_engine": 1 if fits else 0, "engine_fallback": 0 if fits else (1 if lds else 2),
+                         "engine_note": note}
+
+        def view(self, k):
+            return (self, k)
+
+        def close(self):
+            closed.append(self.n_chains)
+
+    monkeypatch.setattr(P.context, "ChainContext", Fake)
+    monkeypatch.delenv("NNGP_SPLIT_CHAINS", raising=False)
+    fits_at, lds = 2, True
+    v = P.context.make_chain_views(None, None, None, None, None, 4, devices=[0])
+    assert opened == [4, 2, 2] and closed == [4]
+    assert [k for _, k in v] == [0, 1, 0, 1] and v[0][0] is v[1][0] and v[2][0] is not v[0][0]
+    opened.clear(); closed.clear()
+    fits_at = 1
+    v = P.context.make_chain_views(None, None, None, None, None, 3, devices=[0])
+    assert opened == [3, 2, 1, 1, 1] and closed == [3, 2] and [k for _, k in v] == [0, 0, 0]
+    opened.clear(); closed.clear()
+    fits_at, lds = 2, False  # another reason (residency): no split
+    v = P.context.make_chain_views(None, None, None, None, None, 4, devices=[0])
+    assert opened == [4] and closed == []
+    opened.clear(); closed.clear()
+    lds = True
+    monkeypatch.setenv("NNGP_SPLIT_CHAINS", "0")
+    P.context.make_chain_views(None, None, None, None, None, 4, devices=[0])
+    assert opened == [4] and closed == []

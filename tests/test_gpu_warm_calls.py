@@ -235,3 +235,48 @@ def test_two_contexts_swept_concurrently_one_device(P, O, monkeypatch):
         ref = O.sweep("local", fields[q], Ls[q], NN, col, O.precision_diag(Ls[q], NN), np.ones(n, np.int32), y,
                       np.full(n, b0s[q]), lm, b0s[q], lss[q], lnvs[q], z)
         np.testing.assert_allclose(conc[q][0], ref, rtol=1e-8, atol=1e-9)
+
+
+def test_four_chains_split_into_tile_contexts(P, O, monkeypatch):
+    """Four chains at the headline size: one 4-chain context's tiles exceed a
+    CU's LDS (colour engine), so make_chain_views opens two 2-chain tile
+    contexts instead (context.py _open_group); each chain's sweep equals the
+    oracle's (update_Gaussian.R:257-275) and a 4-chain colour context."""
+    ctxmod = P.context
+    n, m = 1_000_000, 15
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=21)
+    monkeypatch.delenv("NNGP_ENGINE", raising=False)
+    monkeypatch.delenv("NNGP_SPLIT_CHAINS", raising=False)
+    views = ctxmod.make_chain_views(locs, NN, col, lm, y, 4, devices=[0])
+    owners = [v.ctx for v in views]
+    assert owners[0] is owners[1] and owners[2] is owners[3] and owners[0] is not owners[2]
+    for o in (owners[0], owners[2]):
+        assert o.n_chains == 2 and o.info["sweep_engine"] == 1, o.info
+    rng = np.random.default_rng(5)
+    cps = [[1.0, 0.05 * (1 + 0.1 * k), 0.0] for k in range(4)]
+    fields = [rng.normal(size=n) for _ in range(4)]
+    b0s, lss, lnvs = [0.3, -0.2, 0.1, 0.0], [0.1, -0.3, 0.0, 0.2], [-0.5, -0.2, -0.7, -0.4]
+    keys = [101 + k for k in range(4)]
+    for k, v in enumerate(views):
+        v.factor(0, COV, cps[k])
+        v.set_field(fields[k])
+        v.set_mu(None, b0s[k])
+    for o, ks in ((owners[0], [0, 1]), (owners[2], [2, 3])):
+        o.sweep_chains(2, [b0s[k] for k in ks], [lss[k] for k in ks], [lnvs[k] for k in ks], [keys[k] for k in ks],
+                       [0, 0])
+    got = [v.get_field() for v in views]
+    for o in {id(o): o for o in owners}.values():
+        o.close()
+    # the same chains in one 4-chain (colour-engine) context
+    monkeypatch.setenv("NNGP_SPLIT_CHAINS", "0")
+    one = ctxmod.make_chain_views(locs, NN, col, lm, y, 4, devices=[0])
+    assert one[0].ctx is one[3].ctx and one[0].ctx.info["sweep_engine"] == 0
+    for k, v in enumerate(one):
+        v.factor(0, COV, cps[k])
+        v.set_field(fields[k])
+        v.set_mu(None, b0s[k])
+    one[0].ctx.sweep_chains(2, b0s, lss, lnvs, keys, [0, 0, 0, 0])
+    ref = [v.get_field() for v in one]
+    one[0].ctx.close()
+    for k in range(4):
+        assert _rel(got[k], ref[k]) <= 1e-8, (k, _rel(got[k], ref[k]))
