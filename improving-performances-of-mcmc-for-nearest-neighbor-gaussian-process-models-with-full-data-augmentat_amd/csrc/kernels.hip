@@ -400,6 +400,175 @@ __global__ __launch_bounds__(64) void factor_kernel(double var, double nugget, d
   }
 }
 
+// Lane pairs (north star's "a lane group per location"): two lanes per row,
+// lane j = 0, 1 of a pair owns the local block's points r = 2k + j (their
+// coordinates, 8 of 16 at BM = 16) and the columns p = 2k + j of the
+// Cholesky factor L -- half of the register footprint of one lane per row,
+// so two waves fit a SIMD instead of one (the one-lane kernel is issue-bound
+// at one wave per SIMD, ~60 % issue efficiency).  Same left-looking Cholesky
+// on the correlation scale as factor_row: each lane computes the covariance
+// entries (t, q) of its columns q, the dot products
+// sum_{p < q} L[t][p] L[q][p] are split by the parity of p and the two halves
+// added with one DPP swap (IEEE addition commutes: both lanes hold the same
+// bits); the owner of column q keeps L[t][q].  The back substitution
+// x = L^-T e_last needs no reduction (column r of L lives in one lane); each
+// x[r] is swapped to the partner.  The dot products' summation order differs
+// from factor_row's (even and odd p separately), so rows differ from the
+// one-lane kernel in the last bits, within the factor tolerance.
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true); }
+// a cross-lane value stays where it is computed (with every lane of the
+// wave active): the compiler would otherwise sink the DPP move into the
+// lane-dependent select that uses it, where the partner lane is masked off
+// and the move reads 0
+__device__ __forceinline__ void pin_full_exec(double& v) { asm volatile("" : "+v"(v)); }
+
+template <int BM, int FAM, int DS>
+__global__ __launch_bounds__(64) void factor_pair_kernel(double var, double nugget, double nu, double norm,
+                                                        const double* __restrict__ sc,
+                                                        const int* __restrict__ nn, int n, int b,
+                                                        double* __restrict__ linv, int* __restrict__ fail) {
+  static_assert(BM % 2 == 0, "lane pairs: even block size");
+  constexpr int H = BM / 2;            // points / columns per lane
+  constexpr int TH = H * (H + 1);      // owned entries of the packed lower triangle: sum_t ceil((t+1)/2)
+  constexpr int SWAP = 0xB1;           // quad_perm [1,0,3,2]: the pair partner
+  __shared__ double tab[64];
+  tab[threadIdx.x] = kExp2Tab[threadIdx.x];
+  __syncthreads();
+  const double rsv = rsqrt_pos(var);
+  const int j = threadIdx.x & 1;
+  const int stride = gridDim.x * 32;
+  for (int base = blockIdx.x * 32; base < n; base += stride) {
+    const int i = base + (threadIdx.x >> 1);
+    const int row = i < n ? i : n - 1;
+    // this lane's points r = 2k + j: NNarray column BM-1-r (self at r = BM-1)
+    int nc[H];
+#pragma clang loop unroll(full)
+    for (int k = 0; k < H; ++k) {
+      const int c = BM - 1 - (2 * k + j);
+      nc[k] = c < b ? __builtin_nontemporal_load(nn + (size_t)row * b + c) : -1;
+    }
+    // valid count bs: 1 + the last valid column over both lanes
+    int last = 0;
+#pragma clang loop unroll(full)
+    for (int k = 0; k < H; ++k) {
+      const int c = BM - 1 - (2 * k + j);
+      if (c >= 1 && nc[k] >= 0 && c > last) last = c;
+    }
+    int lo = dpp_i32<SWAP>(last);
+    asm volatile("" : "+v"(lo));
+    const int bs = (last > lo ? last : lo) + 1;
+    double Xo[H][DS];
+#pragma clang loop unroll(full)
+    for (int k = 0; k < H; ++k) {
+      const int r = 2 * k + j, c = BM - 1 - r;
+      const bool valid = c < bs;
+      const int idx = valid ? nc[k] : row;
+#pragma clang loop unroll(full)
+      for (int d = 0; d < DS; ++d) {
+        const double v = sc[(size_t)idx * DS + d];
+        Xo[k][d] = valid ? v : (d == 0 ? 1e30 * (r + 1) : 0.0);
+      }
+    }
+    // L[t][2k + j] at off(t) + k, off(t) = sum_{s<t} ceil((s+1)/2); slots a
+    // lane does not own in a row (and inv of columns not reached yet) are
+    // read only into discarded selects -- zeroed so they are defined
+    double L[TH];
+    double inv[H];
+#pragma clang loop unroll(full)
+    for (int e = 0; e < TH; ++e) L[e] = 0.0;
+#pragma clang loop unroll(full)
+    for (int e = 0; e < H; ++e) inv[e] = 0.0;
+    bool bad = false;
+#pragma clang loop unroll(full)
+    for (int t = 0; t < BM; ++t) {
+      const int ot = (t / 2) * (t / 2 + 1) + ((t & 1) ? t / 2 + 1 : 0);  // off(t)
+      const bool dt = (BM - 1 - t) >= bs;
+      // point t's coordinates in both lanes
+      double xt[DS];
+#pragma clang loop unroll(full)
+      for (int d = 0; d < DS; ++d) {
+        const double mine = Xo[t / 2][d];
+        double other = dpp_f64<SWAP, 0xF, true>(mine);
+        pin_full_exec(other);
+        xt[d] = (j == (t & 1)) ? mine : other;
+      }
+      // covariance entries (t, q), q = 2k + j < t
+      double K[H];
+#pragma clang loop unroll(full)
+      for (int k = 0; k < (t + 1) / 2; ++k) {
+        double s2 = 0.0;
+#pragma clang loop unroll(full)
+        for (int d = 0; d < DS; ++d) {
+          const double u = xt[d] - Xo[k][d];
+          s2 = __builtin_fma(u, u, s2);
+        }
+        const double dist = sqrt_pos(s2);
+        const double e = exp_nonpos(-dist, tab);
+        K[k] = FAM == 1 ? __builtin_fma(dist, e, e) : e;
+      }
+#pragma clang loop unroll(full)
+      for (int q = 0; q <= t; ++q) {
+        const int oq = (q / 2) * (q / 2 + 1) + ((q & 1) ? q / 2 + 1 : 0);
+        // this lane's half of sum_{p<q} L[t][p] L[q][p]: p = 2k + j < q
+        double sp = 0.0;
+#pragma clang loop unroll(full)
+        for (int k = 0; k < (q + 1) / 2; ++k) {
+          const double term = L[ot + k] * L[oq + k];
+          // q odd: lane 1's last slot is column q itself (not yet a term)
+          sp = (2 * k + 1 >= q && (q & 1) && j == 1) ? sp : sp + term;
+        }
+        double sw = dpp_f64<SWAP, 0xF, true>(sp);
+        pin_full_exec(sw);
+        const double s = sp + sw;
+        const bool own = (q & 1) == j;
+        if (q < t) {
+          const double v = (K[q / 2] - s) * inv[q / 2];
+          // q even: lane 1's slot q/2 is column q+1 of row t, written at q+1
+          if (!(q & 1) || own) L[ot + q / 2] = v;
+        } else {
+          double dd = (dt ? 1.0 : 1.0 + nugget) - s;
+          if (!(dd > 0.0)) { bad = true; dd = 1.0; }
+          const double ri = rsqrt_pos(dd);
+          if (!(q & 1) || own) {
+            L[ot + q / 2] = dd * ri;
+            inv[q / 2] = ri;
+          }
+        }
+      }
+    }
+    // x = L^-T e_last; x[r] lives in both lanes after its owner computes it
+    double x[BM];
+    {
+      const double own = inv[H - 1];  // column BM-1 is odd: lane 1's
+      double other = dpp_f64<SWAP, 0xF, true>(own);
+      pin_full_exec(other);
+      x[BM - 1] = j == 1 ? own : other;
+    }
+#pragma clang loop unroll(full)
+    for (int r = BM - 2; r >= 0; --r) {
+      double sacc = 0.0;
+#pragma clang loop unroll(full)
+      for (int q = r + 1; q < BM; ++q) {
+        const int oq = (q / 2) * (q / 2 + 1) + ((q & 1) ? q / 2 + 1 : 0);
+        sacc -= L[oq + r / 2] * x[q];  // L[q][r]: column r's owner holds it
+      }
+      const double mine = sacc * inv[r / 2];
+      double other = dpp_f64<SWAP, 0xF, true>(mine);
+      pin_full_exec(other);
+      x[r] = ((r & 1) == j) ? mine : other;
+    }
+    if (i < n) {
+      if (bad) atomicMin(fail, i + 1);
+#pragma clang loop unroll(full)
+      for (int k = 0; k < H; ++k) {
+        const int c = 2 * k + j;  // output column
+        if (c < b) linv[(size_t)i * b + c] = (c < bs) ? x[BM - 1 - c] * rsv : 0.0;
+      }
+    }
+  }
+}
+
 // Runtime-b variant (b <= 32, and the general Matern family whose Bessel
 // evaluation defeats full unrolling): same algorithm, private arrays indexed
 // at run time (held in scratch; correct for every b, slower than the
@@ -480,6 +649,16 @@ static int resident_grid(const void* kern, int groups) {
 template <int BM, int FAM, int DS>
 static hipError_t launch_factor_one(hipStream_t st, double var, double nugget, double nu, double norm,
                                     const double* sc, const int* nn, int n, int b, double* linv, int* fail) {
+  // NNGP_FACTOR_PAIR=1: the lane-pair kernel (opt-in: measured slower)
+  if constexpr (BM == 16) {
+    const char* pe = std::getenv("NNGP_FACTOR_PAIR");
+    if (pe && pe[0] == '1') {
+      const auto kp = factor_pair_kernel<BM, FAM, DS>;
+      const int g = resident_grid(reinterpret_cast<const void*>(kp), (n + 31) / 32);
+      hipLaunchKernelGGL(kp, dim3(g), dim3(64), 0, st, NNGP_FACTOR_ARGS);
+      return hipGetLastError();
+    }
+  }
   const auto kern = factor_kernel<BM, FAM, DS, 0>;
   const int g = resident_grid(reinterpret_cast<const void*>(kern), (n + 63) / 64);
   hipLaunchKernelGGL(kern, dim3(g), dim3(64), 0, st, NNGP_FACTOR_ARGS);
@@ -622,14 +801,12 @@ __global__ __launch_bounds__(256) void row_stats_kernel(const double* __restrict
     a = group_sum<G>(a);
     u2 = group_sum<G>(u2);
     a2 = group_sum<G>(a2);
-    if (g == 0) {
-      acc[0] += log(linv[(size_t)k * b]);
+    if (g == 0) {  // (acc[0] stays 0: no caller reads this kernel's log term)
       acc[1] += u * u;
       acc[2] += a * a;
       acc[3] += a * u;
       if (out) out[(size_t)k * out_stride] = u;
       if (two) {
-        acc[0] += log(linv[(size_t)k2 * b]);
         acc[1] += u2 * u2;
         acc[2] += a2 * a2;
         acc[3] += a2 * u2;
@@ -661,14 +838,27 @@ int launch_row_stats(hipStream_t st, const double* linv, const int* nn, int n, i
 // NNarray entries load once; per job the same loads, butterfly and
 // accumulation order as row_stats_kernel (so the same partials, bitwise).
 // Two rows per trip as there, i.e. 2 x M independent gathers in flight.
+// Mode 1's log determinant sum_k log L[k][0]: a running product of the row
+// diagonals kept as mantissa x 2^exponent (frexp after every factor: no
+// overflow or underflow), one log per thread at the end -- a log per row in
+// the one lane of its group cost ~45 % of the pass (303 vs 159 us for three
+// jobs at n = 1e6, b = 16).  The product's rounding (~n ulp relative) is far
+// below the log-likelihood tolerance.
+constexpr double kLn2Hi = 0.6931471803691238;       // 28 significant bits: pe * kLn2Hi is exact
+constexpr double kLn2Lo = 1.9082149292705877e-10;   // ln 2 - kLn2Hi
 template <int G, int MJ>
 __global__ __launch_bounds__(256) void row_stats_jobs_kernel(RowJobs J, const int* __restrict__ nn, int n, int b,
                                                              double* __restrict__ partials) {
   double acc[MJ][4];
+  double pm[MJ];  // mode 1: product of the diagonals seen = pm x 2^pe
+  int pe[MJ];
 #pragma unroll
-  for (int j = 0; j < MJ; ++j)
+  for (int j = 0; j < MJ; ++j) {
+    pm[j] = 1.0;
+    pe[j] = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[j][q] = 0.0;
+  }
   const int g = threadIdx.x & (G - 1);
   const int rows_per_grid = gridDim.x * (blockDim.x / G);
   for (int k = blockIdx.x * (blockDim.x / G) + threadIdx.x / G; k < n; k += 2 * rows_per_grid) {
@@ -680,6 +870,7 @@ __global__ __launch_bounds__(256) void row_stats_jobs_kernel(RowJobs J, const in
       if (two) idx2 = __builtin_nontemporal_load(nn + (size_t)k2 * b + g);
     }
     double u[MJ], a[MJ], u2[MJ], a2[MJ];
+    double dg[MJ], dg2[MJ];  // lane g = 0: the row's diagonal L[k][0] (its own entry, NNarray column 0)
 #pragma unroll
     for (int j = 0; j < MJ; ++j) {
       double l = 0.0, xv = 0.0, l2 = 0.0, xv2 = 0.0;
@@ -694,6 +885,7 @@ __global__ __launch_bounds__(256) void row_stats_jobs_kernel(RowJobs J, const in
         }
       }
       u[j] = l * xv; a[j] = l; u2[j] = l2 * xv2; a2[j] = l2;
+      dg[j] = l; dg2[j] = l2;
     }
 #pragma unroll
     for (int j = 0; j < MJ; ++j) {
@@ -709,12 +901,19 @@ __global__ __launch_bounds__(256) void row_stats_jobs_kernel(RowJobs J, const in
         if (J.out[j]) J.out[j][(size_t)k * J.out_stride] = u[j];
         if (two && J.out[j]) J.out[j][(size_t)k2 * J.out_stride] = u2[j];
         if (J.mode[j] == 0) continue;
-        if (J.mode[j] == 1) acc[j][0] += log(J.linv[j][(size_t)k * b]);
+        if (J.mode[j] == 1) {
+          int e;
+          pm[j] = __builtin_frexp(pm[j] * dg[j], &e);
+          pe[j] += e;
+          if (two) {
+            pm[j] = __builtin_frexp(pm[j] * dg2[j], &e);
+            pe[j] += e;
+          }
+        }
         acc[j][1] += u[j] * u[j];
         acc[j][2] += a[j] * a[j];
         acc[j][3] += a[j] * u[j];
         if (two) {
-          if (J.mode[j] == 1) acc[j][0] += log(J.linv[j][(size_t)k2 * b]);
           acc[j][1] += u2[j] * u2[j];
           acc[j][2] += a2[j] * a2[j];
           acc[j][3] += a2[j] * u2[j];
@@ -722,6 +921,9 @@ __global__ __launch_bounds__(256) void row_stats_jobs_kernel(RowJobs J, const in
       }
     }
   }
+#pragma unroll
+  for (int j = 0; j < MJ; ++j)
+    if (j < J.M && J.mode[j] == 1 && g == 0) acc[j][0] = log(pm[j]) + ((double)pe[j] * kLn2Hi + (double)pe[j] * kLn2Lo);
 #pragma unroll
   for (int j = 0; j < MJ; ++j)
     if (j < J.M && J.mode[j] != 0) {

@@ -1627,6 +1627,7 @@ __global__ __launch_bounds__(256) void tile_refresh_kernel(TileDev D, const int4
                                                            const double* __restrict__ linv, int chain) {
   __shared__ double sq[kRefreshCells];
   __shared__ unsigned char endf[kRefreshCells];
+  __shared__ int4 bsh[kRefreshCells / 64];
   // U independent gathers in flight per thread
   constexpr int U = 8;
   const int t = threadIdx.x;
@@ -1674,22 +1675,32 @@ __global__ __launch_bounds__(256) void tile_refresh_kernel(TileDev D, const int4
       }
     }
   }
+  // the item's batch descriptors in LDS (a run of <= kRefreshCells / 64
+  // wave-local batches): each slot finds its batch by a binary search there
+  // instead of a chain of dependent global loads
+  for (int i = t; i < o.z; i += 256) bsh[i] = D.batch[o.y + i];
   __syncthreads();
   // per slot: the sum of squares of its cells in stream order f (cell f of a
-  // batch at (f % R) * NT + f / R)
+  // batch at (f % R) * NT + f / R, stepped incrementally)
   const int nslots = BL.w + BL.z - B0.w;
   for (int u = t; u < nslots; u += 256) {
     const int x = B0.w + u;
-    int b = o.y;
-    while (x >= D.batch[b].w + D.batch[b].z) ++b;
-    const int4 B = D.batch[b];
+    int lo = 0, hi = o.z - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (bsh[mid].w <= x) lo = mid;
+      else hi = mid - 1;
+    }
+    const int4 B = bsh[lo];
     const int R = B.y & 0xFFFF, rel = B.x - B0.x;
     const int f0 = D.sinfo[x].y & 0xFFFFF;
+    int fj = f0 % R, ft = f0 / R;
     double s = 0.0;
-    for (int f = f0;; ++f) {
-      const int e = rel + (f % R) * NT + f / R;
+    for (;;) {
+      const int e = rel + fj * NT + ft;
       s += sq[e];
       if (endf[e]) break;
+      if (++fj == R) { fj = 0; ++ft; }
     }
     D.dr[(size_t)x * D.C + chain].x = s;
   }

@@ -57,6 +57,24 @@ def test_factor_matches_oracle(P, O, m, covfun):
 
 
 @pytest.mark.parametrize("covfun", ["exponential_isotropic", "matern15_isotropic"])
+@pytest.mark.parametrize("m", [12, 15])
+def test_factor_lane_pairs_match_oracle(P, O, covfun, m, monkeypatch):
+    """The opt-in lane-pair factor kernel (NNGP_FACTOR_PAIR=1, two lanes per
+    Vecchia row, kernels.hip factor_pair_kernel; BM = 16 blocks: m = 15, and
+    m = 12 padded in front) against the oracle's GpGp::vecchia_Linv
+    restatement, at the one-lane kernel's tolerance."""
+    monkeypatch.setenv("NNGP_FACTOR_PAIR", "1")
+    locs, NN, col, lm, y = make_problem(P, 900, m, seed=40 + m)
+    cp = COVS[covfun]
+    with _ctx(P, locs, NN, col, lm, y) as ctx:
+        ctx.factor(0, covfun, cp)
+        got = ctx.get_linv(0)
+    ref = O.vecchia_linv(covfun, cp, locs, NN)
+    np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-10)
+    assert np.all(got[NN == O.NA] == 0.0)
+
+
+@pytest.mark.parametrize("covfun", ["exponential_isotropic", "matern15_isotropic"])
 def test_factor_with_coinciding_points_matches_oracle(P, O, covfun):
     """Two locations at distance 0 (correlation 1) with a nugget: a positive
     definite local covariance that GpGp factors; the device's distance
