@@ -442,6 +442,29 @@ std::mutex& tile_lock(int device) {
   return locks[device & 63];
 }
 
+// With several tile contexts on a device, their persistent launches are
+// chained on the GPU instead of drained on the host: under the device's tile
+// lock a launch first waits (on its stream) for the event recorded after the
+// device's previous tile launch, then records its own -- no two persistent
+// launches overlap, and a sweep call returns without a host sync.
+static hipEvent_t& tile_chain_event(int device) {
+  static hipEvent_t evs[64] = {};
+  return evs[device & 63];
+}
+
+static int tile_chain_wait(nngp_ctx* c) {
+  hipEvent_t& ev = tile_chain_event(c->device);
+  if (ev) HIPCHK(c, hipStreamWaitEvent(c->st, ev, 0));
+  return NNGP_OK;
+}
+
+static int tile_chain_record(nngp_ctx* c) {
+  hipEvent_t& ev = tile_chain_event(c->device);
+  if (!ev) HIPCHK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  HIPCHK(c, hipEventRecord(ev, c->st));
+  return NNGP_OK;
+}
+
 // reduce partials to res_d and copy 4 doubles to the host (synchronises)
 int fetch4(nngp_ctx* c, int nblocks, double out[4]) {
   HIPCHK(c, launch_reduce4(c->st, c->partials_d, nblocks, c->res_d));
@@ -1846,15 +1869,15 @@ static void warm_set(nngp_ctx* c, int mask, const double* beta0) {
 }
 
 // A sweep call returns without a host sync (stream-ordered, like the other
-// calls; its tile timeout word is checked after the next sync) unless another
-// tile context shares the device -- then the call holds the device's tile
-// lock until its launch has drained (tile_lock) -- or a probe buffer is read.
+// calls; its tile timeout word is checked after the next sync) unless a probe
+// buffer is read.  Tile launches of several contexts on one device are
+// chained by an event under the device's tile lock (tile_chain_event).
 static bool sweep_async(const nngp_ctx* c) {
   static const bool force_sync = [] {  // NNGP_SWEEP_SYNC=1: every sweep call ends with a host sync
     const char* e = std::getenv("NNGP_SWEEP_SYNC");
     return e && std::string(e) == "1";
   }();
-  return !force_sync && (c->engine != 1 || tile_ctx_count(c->device) == 1) && !c->tdbg_d && !c->dbg_d;
+  return !force_sync && !c->tdbg_d && !c->dbg_d;
 }
 
 int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double lnv, uint64_t seed,
@@ -1896,16 +1919,20 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
         zc[((size_t)s * c->n + c->loc_rank[i]) * c->C + k] = z[(size_t)s * c->n + i];
     HIPCHK(c, hipMemcpyAsync(c->z_d, zc.data(), need * sizeof(double), hipMemcpyHostToDevice, c->st));
     { int ss_ = sync_stream(c); if (ss_) return ss_; }
+    if (c->engine == 1 && (rc = tile_chain_wait(c))) return rc;
     if ((rc = enqueue_sweep_body(c, n_sweeps, mask, c->z_d))) return rc;
+    if (c->engine == 1 && (rc = tile_chain_record(c))) return rc;
   } else {
     // replay a captured graph of the whole call (launch-bound at small n)
     hipGraphExec_t ex;
     if ((rc = graph_for(c, n_sweeps, mask, &ex, warm ? kColours | kEpilogue : kAll))) return rc;
+    if (c->engine == 1 && (rc = tile_chain_wait(c))) return rc;
     HIPCHK(c, hipGraphLaunch(ex, c->st));
     if (c->inject_tmo > 0 && c->engine == 1) {
       --c->inject_tmo;
       HIPCHK(c, launch_tile_inject_timeout(c->st, c->ctl_d));
     }
+    if (c->engine == 1 && (rc = tile_chain_record(c))) return rc;
   }
   if (async) {
     c->tile_pending = c->engine == 1;
@@ -1939,11 +1966,13 @@ int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const doub
   const bool async = sweep_async(c);
   hipGraphExec_t ex;
   if ((rc = graph_for(c, n_sweeps, all, &ex, warm ? kColours | kEpilogue : kAll))) return rc;
+  if (c->engine == 1 && (rc = tile_chain_wait(c))) return rc;
   HIPCHK(c, hipGraphLaunch(ex, c->st));
   if (c->inject_tmo > 0 && c->engine == 1) {
     --c->inject_tmo;
     HIPCHK(c, launch_tile_inject_timeout(c->st, c->ctl_d));
   }
+  if (c->engine == 1 && (rc = tile_chain_record(c))) return rc;
   if (async) {
     c->tile_pending = c->engine == 1;
     if (tlk.owns_lock()) tlk.unlock();
@@ -2173,8 +2202,11 @@ static int tile_shard_call(nngp_ctx* c, int n_sweeps, int mask) {
   a.n_sweeps = n_sweeps;
   a.chain_mask = mask;
   a.z_in = nullptr;
-  hipError_t e = launch_sweep_tiles(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NTK, c->tl.max_batches,
-                                    c->tl.max_gslots, &sh, c->tTl);
+  int wrc = tile_chain_wait(c);
+  hipError_t e = wrc ? hipErrorUnknown
+                     : launch_sweep_tiles(c->st, tile_dev(c), a, c->tl.max_rows, c->tl.NTK, c->tl.max_batches,
+                                          c->tl.max_gslots, &sh, c->tTl);
+  if (e == hipSuccess && tile_chain_record(c)) e = hipErrorUnknown;
   if (e == hipSuccess) e = hipMemcpyAsync(c->tmo_h, c->ctl_d + 2, sizeof(unsigned), hipMemcpyDeviceToHost, c->st);
   // the broadcasts go out even after a failed launch: the peers wait in them
   rc = tile_shard_exchange(c);
@@ -2370,8 +2402,10 @@ static int tile_group_call(nngp_ctx** ctxs, int G, int n_sweeps, const double* b
     a.n_sweeps = n_sweeps;
     a.chain_mask = mask;
     a.z_in = nullptr;
+    if ((rc = tile_chain_wait(L))) { cleanup(); return rc; }
     GCHK(L, launch_sweep_tiles(L->st, devs[g0], a, L->tl.max_rows, L->tl.NTK, L->tl.max_batches, L->tl.max_gslots, &sh,
                                (g1 - g0) * Tl));
+    if ((rc = tile_chain_record(L))) { cleanup(); return rc; }
     for (int h = g0; h < g1; ++h)
       GCHK(L, hipMemcpyAsync(ctxs[h]->tmo_h, ctxs[h]->ctl_d + 2, sizeof(unsigned), hipMemcpyDeviceToHost, L->st));
     for (int h = g0; h < g1; ++h) GCHK(L, hipEventRecord(ev[G + h], L->st));
@@ -2512,6 +2546,7 @@ int nngp_sweep_timed(nngp_ctx* c, int n_sweeps, const double* beta0, const doubl
   if ((rc = graph_for(c, n_sweeps, mask, &pro, kPrologue))) return rc;
   if ((rc = graph_for(c, n_sweeps, mask, &col, kColours))) return rc;
   if ((rc = graph_for(c, n_sweeps, mask, &epi, kEpilogue))) return rc;
+  if (c->engine == 1 && (rc = tile_chain_wait(c))) return rc;
   hipEvent_t e[4];
   for (auto& x : e) HIPCHK(c, hipEventCreate(&x));
   // the colour launches alone are bracketed by e[1], e[2]: their mean
@@ -2524,6 +2559,7 @@ int nngp_sweep_timed(nngp_ctx* c, int n_sweeps, const double* beta0, const doubl
   HIPCHK(c, hipEventRecord(e[2], c->st));
   HIPCHK(c, hipGraphLaunch(epi, c->st));
   HIPCHK(c, hipEventRecord(e[3], c->st));
+  if (c->engine == 1 && (rc = tile_chain_record(c))) return rc;
   { int ss_ = sync_stream(c); if (ss_) return ss_; }
   float f = 0, g = 0;
   HIPCHK(c, hipEventElapsedTime(&f, e[0], e[3]));
