@@ -352,19 +352,26 @@ def shard_main(P, args, world, rank, local_rank, dist, scaling):
     log(f"shard setup n={n} m={args.m} {covfun} chains={C} world={world} scaling={scaling}", rank)
     agree = (lambda f: _agreed(dist, f)) if world > 1 else (lambda f: f())
     wl = agree(lambda: make_workload(P, n, args.m, covfun, cp, seed=1000, device=local_rank, chains=C))
-    ctx = agree(lambda: ShardContext(wl["locs"], wl["NN"], wl["col"], wl["lm"], wl["y"], n_ranks=world, rank=rank,
-                                     device=local_rank, n_chains=C))
+    # the chains in groups whose tiles keep r in LDS (context.split_groups:
+    # configs[4] at 3 chains -> a 2-chain and a 1-chain shard; one group
+    # otherwise); every rank makes the same decision (same layout)
+    groups = agree(lambda: P.context.split_groups(
+        lambda k: ShardContext(wl["locs"], wl["NN"], wl["col"], wl["lm"], wl["y"], n_ranks=world, rank=rank,
+                               device=local_rank, n_chains=k), list(range(C))))
+    ctx = groups[0][0]
     try:
-        init_shard_comm(ctx, dist, rccl=False)
+        for g, _ in groups:
+            init_shard_comm(g, dist, rccl=False)
         rng = np.random.default_rng(7)
 
         def prep():
-            for k in range(C):
-                ctx.select(k)
-                ctx.factor(0, covfun, cp)
-                ctx.set_field(wl["beta0"] + wl["w"] + 0.1 * rng.normal(size=len(wl["y"])))
-                ctx.set_mu(None, wl["beta0"])
-            ctx.select(0)
+            for g, ids in groups:
+                for k in range(len(ids)):
+                    g.select(k)
+                    g.factor(0, covfun, cp)
+                    g.set_field(wl["beta0"] + wl["w"] + 0.1 * rng.normal(size=len(wl["y"])))
+                    g.set_mu(None, wl["beta0"])
+                g.select(0)
 
         agree(prep)
         info = ctx.info
@@ -375,7 +382,9 @@ def shard_main(P, args, world, rank, local_rank, dist, scaling):
             done = 0
             while done < nsw:
                 s = min(nc, nsw - done)
-                ctx.sweep_chains(s, [b0] * C, [ls] * C, [lnv] * C, seeds, [base + done] * C)
+                for g, ids in groups:
+                    k = len(ids)
+                    g.sweep_chains(s, [b0] * k, [ls] * k, [lnv] * k, [seeds[i] for i in ids], [base + done] * k)
                 done += s
             return base + done
 
@@ -384,7 +393,8 @@ def shard_main(P, args, world, rank, local_rank, dist, scaling):
             f"tiles={info['n_tiles']} owned={info['shard_owned']} exchange_slots={info['shard_exchange_slots']}", rank)
         elapsed, _ = timed_region(run, args.steps, args.warmup, dist, sync)
     finally:
-        ctx.close()
+        for g, _ in groups:
+            g.close()
     nnz = info["nnz"]
     tiles = info["sweep_engine"] == 1
     bytes_sweep = C * (8 * nnz + 40 * n) + 4 * nnz
@@ -406,6 +416,8 @@ def shard_main(P, args, world, rank, local_rank, dist, scaling):
                                    f"(value = chain-sweeps/s x n/1e6)"),
                       "n": n, "m": args.m, "n_colors": info["n_colors"], "nnz": nnz, "chains": C,
                       "chain_sweeps_per_s": args.steps * C / elapsed,
+                      "chain_groups": [len(ids) for _, ids in groups],
+                      "engine_note_rank0": info["engine_note"],
                       "n_chromatic_per_call": nc, "sweep_engine": "tile shard" if tiles else "colour shard",
                       "n_tiles": info["n_tiles"], "owned_rank0": info["shard_owned"],
                       "needed_rows_rank0": info["shard_needed_rows"],

@@ -65,7 +65,8 @@ class Info(C.Structure):
                 ("shard_exchange_slots", C.c_longlong), ("tile_ghost_pass", C.c_int),
                 ("tile_ghost_cells_max", C.c_int), ("tile_r_global", C.c_int),
                 ("tile_chain_split", C.c_int), ("tile_resident_per_cu", C.c_int),
-                ("engine_fallback", C.c_int), ("tile_exchange_wave", C.c_int), ("device_cus", C.c_int)]
+                ("engine_fallback", C.c_int), ("tile_exchange_wave", C.c_int), ("device_cus", C.c_int),
+                ("tile_rows_needed", C.c_int), ("device_lds", C.c_int)]
 
 
 _dp = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")

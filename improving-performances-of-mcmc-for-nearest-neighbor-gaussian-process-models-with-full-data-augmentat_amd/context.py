@@ -322,27 +322,46 @@ class ChainView:
         self.ctx.close()
 
 
-def _lds_fallback(ctx) -> bool:
-    """The context runs the colour engine only because its tiles do not fit a
-    CU's LDS at its chain count (engine_fallback 1, note names the LDS)."""
+# LDS of a 512-thread tile besides r (slot totals, batch table, hand-off
+# values, ...): about 17 KB at configs[4]'s per-GPU share, graph_prep.cpp
+# tile_lds_bytes
+_TILE_LDS_OTHER = 24 * 1024
+
+
+def _lds_limited(ctx) -> bool:
+    """The context's tiles do not keep r in LDS at its chain count, but would
+    at half of it: it runs the colour engine for the LDS (engine_fallback 1,
+    the note names the LDS) or tiles with r in global memory (a tile shard
+    whose LDS tiles do not fit) -- not when r in global memory was asked for
+    (NNGP_TILE_R=global) or half the chains' rows still exceed the LDS."""
     inf = ctx.info
-    return inf["sweep_engine"] == 0 and inf["engine_fallback"] == 1 and "LDS" in inf["engine_note"]
+    limited = ((inf["sweep_engine"] == 0 and inf["engine_fallback"] == 1 and "LDS" in inf["engine_note"]) or
+               (inf["sweep_engine"] == 1 and "r in global memory" in inf["engine_note"] and
+                os.environ.get("NNGP_TILE_R", "") != "global"))
+    half = (ctx.n_chains + 1) // 2
+    return limited and 0 < inf["tile_rows_needed"] * half * 8 + _TILE_LDS_OTHER <= inf["device_lds"]
 
 
-def _open_group(locs, NNarray, coloring, locs_match, observed_field, dev, group):
-    """Contexts for the chains `group` of one device: one context, or -- when
-    its tile layout exceeds the LDS at this chain count (4 chains at the
-    headline n = 1e6: r of a tile's 5.2k local rows x 4 x 8 B > 160 KB) --
-    the two halves of the group as separate contexts, recursively, which run
-    the tile engine (2 chains: ~112 KB) instead of the colour engine.
-    NNGP_SPLIT_CHAINS=0 keeps one context per group."""
-    ctx = ChainContext(locs, NNarray, coloring, locs_match, observed_field, device=dev, n_chains=len(group))
-    if len(group) < 2 or os.environ.get("NNGP_SPLIT_CHAINS", "1") == "0" or not _lds_fallback(ctx):
+def split_groups(open_ctx, group):
+    """Contexts for the chains `group`: open_ctx(chains) -> context; one
+    context, or -- when its tiles keep r in LDS only at fewer chains (4
+    chains at the headline n = 1e6: a tile's 5.2k local rows x 4 x 8 B > 160
+    KB; configs[4]'s per-GPU share at 3 chains) -- the two halves of the group
+    as separate contexts, recursively, on the LDS tile engine (the launches of
+    the contexts of one device are chained on the GPU, capi.hip
+    tile_chain_event).  NNGP_SPLIT_CHAINS=0 keeps one context per group.
+    -> [(context, chain ids)]."""
+    ctx = open_ctx(len(group))
+    if len(group) < 2 or os.environ.get("NNGP_SPLIT_CHAINS", "1") == "0" or not _lds_limited(ctx):
         return [(ctx, group)]
     ctx.close()
     h = (len(group) + 1) // 2
-    return (_open_group(locs, NNarray, coloring, locs_match, observed_field, dev, group[:h]) +
-            _open_group(locs, NNarray, coloring, locs_match, observed_field, dev, group[h:]))
+    return split_groups(open_ctx, group[:h]) + split_groups(open_ctx, group[h:])
+
+
+def _open_group(locs, NNarray, coloring, locs_match, observed_field, dev, group):
+    return split_groups(lambda k: ChainContext(locs, NNarray, coloring, locs_match, observed_field, device=dev,
+                                               n_chains=k), group)
 
 
 def make_chain_views(locs, NNarray, coloring, locs_match, observed_field, n_chains: int, devices=None):

@@ -191,6 +191,8 @@ struct nngp_ctx {
   std::string engine_note;        // why this sweep engine (nngp_ctx_engine_note)
   int tstagger = 0;               // chain-split: start offset per chain (NNGP_TILE_STAGGER, 100 MHz ticks)
   int tvariant = 0;               // NNGP_TILE_VARIANT (probe builds): experiment bits
+  int tile_rows_needed = 0;       // largest local rows of a tile of the layout built here (nngp_info)
+  int lds_max = 0;                // LDS bytes per CU of the device
   double* rg_d = nullptr;         // sum of the tiles' local rows x C
   unsigned* ctl_d = nullptr;      // [0] call id, [1] timeout word of a launch, [2] sticky timeout (tiles.hip)
   unsigned* tmo_h = nullptr;      // pinned copy of the sticky timeout word after each launch
@@ -700,6 +702,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       int cus = 0, lds_max = 0;
       cus = c->cus;
       if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeSharedMemPerBlockOptin, device) != hipSuccess) lds_max = 0;
+      c->lds_max = lds_max;
       int T = std::max(1, std::min(G * cus, (n + kTileTarget - 1) / kTileTarget));
       // NNGP_TILES may ask for more tiles than CUs: the residency check below
       // then falls back to the colour engine (the tiles spin on each other, so
@@ -867,6 +870,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       }
       if (ok) {
         c->engine = 1;
+        c->tile_rows_needed = c->tl.max_rows;
         {
           // a sweep of another tile context of this device may still be in
           // flight (it returned without a sync while it was the only one):
@@ -891,6 +895,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
           c->tTl = T / G;
         }
       } else {
+        c->tile_rows_needed = c->tl.max_rows;
         c->tl = TileLayout();
         c->txw = 0;
         c->tcs = false;
@@ -1291,6 +1296,8 @@ int nngp_ctx_info(const nngp_ctx* c, nngp_info* info) {
   info->engine_fallback = c->engine_fallback;
   info->tile_exchange_wave = c->txw ? 1 : 0;
   info->device_cus = c->cus;
+  info->tile_rows_needed = c->tile_rows_needed;
+  info->device_lds = c->lds_max;
   if (c->engine == 1)
     for (size_t i = 0; i + 1 < c->tl.gptr.size(); ++i)
       info->tile_ghost_cells_max = std::max(info->tile_ghost_cells_max, c->tl.gptr[i + 1] - c->tl.gptr[i]);

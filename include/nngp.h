@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define NNGP_ABI_VERSION 11
+#define NNGP_ABI_VERSION 12  /* 12: nngp_info gained tile_rows_needed, device_lds */
 #define NNGP_SHARD_ID_BYTES 128 /* RCCL unique id */
 #define NNGP_IPC_HANDLE_BYTES 192 /* HIP IPC handles of a tile shard's granule buffer, w replica, flags */
 
@@ -116,6 +116,9 @@ typedef struct {
                                 3 = NNGP_ENGINE=colors / more ranks than the tile shard takes */
   int tile_exchange_wave;    /* tile engine: 1 = the last wave of each tile polls the hand-offs (NT - 64 cell threads) */
   int device_cus;            /* compute units of the context's device */
+  int tile_rows_needed;      /* largest local-row count of a tile in the tile layout built for this context
+                                (also when the tile engine was not used or keeps r in global memory; 0: none built) */
+  int device_lds;            /* LDS bytes per CU of the context's device */
 } nngp_info;
 
 /* ---------- library ---------- */

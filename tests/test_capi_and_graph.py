@@ -20,7 +20,7 @@ def test_header_symbols_exported(P):
     lib = C.CDLL(str(_lib.LIB_PATH))
     for s in sorted(declared):
         assert hasattr(lib, s), s
-    assert P.lib.nngp_abi_version() == 11
+    assert P.lib.nngp_abi_version() == 12
 
 
 def test_library_has_gfx950_code_object():
@@ -520,9 +520,10 @@ def test_r_shim_wraps_every_abi_entry_point():
 
 def test_chain_groups_split_where_tiles_exceed_the_lds(P, monkeypatch):
     """context.make_chain_views: a chain group whose context fell back to the
-    colour engine for the LDS (engine_fallback 1) is reopened as two halves,
-    recursively; other fallbacks and NNGP_SPLIT_CHAINS=0 keep one context
-    (host logic, fake contexts: no GPU)."""
+    colour engine for the LDS (engine_fallback 1) or keeps r in global memory
+    is reopened as two halves, recursively, when half the chains' rows fit the
+    LDS; other fallbacks, NNGP_SPLIT_CHAINS=0 and NNGP_TILE_R=global keep one
+    context (host logic, fake contexts: no GPU)."""
     opened, closed = [], []
 
     class Fake:
@@ -532,8 +533,11 @@ def test_chain_groups_split_where_tiles_exceed_the_lds(P, monkeypatch):
             fits = n_chains <= fits_at
             note = "tiles" if fits else ("colours (tile engine not used: tile layout needs 170000 B of LDS per tile"
                                          if lds else "colours (tile engine not used: residency)")
-            self.info = {"sweep_engine": 1 if fits else 0, "engine_fallback": 0 if fits else (1 if lds else 2),
-                         "engine_note": note}
+            if not fits and rg:
+                note = "tiles: 256 tiles of 512 threads, r in global memory"
+            self.info = {"sweep_engine": 1 if fits or rg else 0,
+                         "engine_fallback": 0 if fits or rg else (1 if lds else 2),
+                         "engine_note": note, "tile_rows_needed": rows, "device_lds": 160 * 1024}
 
         def view(self, k):
             return (self, k)
@@ -543,7 +547,8 @@ def test_chain_groups_split_where_tiles_exceed_the_lds(P, monkeypatch):
 
     monkeypatch.setattr(P.context, "ChainContext", Fake)
     monkeypatch.delenv("NNGP_SPLIT_CHAINS", raising=False)
-    fits_at, lds = 2, True
+    monkeypatch.delenv("NNGP_TILE_R", raising=False)
+    fits_at, lds, rg, rows = 2, True, False, 5000
     v = P.context.make_chain_views(None, None, None, None, None, 4, devices=[0])
     assert opened == [4, 2, 2] and closed == [4]
     assert [k for _, k in v] == [0, 1, 0, 1] and v[0][0] is v[1][0] and v[2][0] is not v[0][0]
@@ -560,3 +565,16 @@ def test_chain_groups_split_where_tiles_exceed_the_lds(P, monkeypatch):
     monkeypatch.setenv("NNGP_SPLIT_CHAINS", "0")
     P.context.make_chain_views(None, None, None, None, None, 4, devices=[0])
     assert opened == [4] and closed == []
+    monkeypatch.delenv("NNGP_SPLIT_CHAINS")
+    opened.clear(); closed.clear()
+    rows = 20000  # half the chains' rows still beyond the LDS (n = 1e7 on one GPU): no split
+    P.context.make_chain_views(None, None, None, None, None, 4, devices=[0])
+    assert opened == [4] and closed == []
+    opened.clear(); closed.clear()
+    rows, rg = 6907, True  # a tile shard with r in global memory (configs[4] at 3 chains): 2 + 1
+    v = P.context.make_chain_views(None, None, None, None, None, 3, devices=[0])
+    assert opened == [3, 2, 1] and closed == [3]
+    opened.clear(); closed.clear()
+    monkeypatch.setenv("NNGP_TILE_R", "global")  # asked for: kept
+    P.context.make_chain_views(None, None, None, None, None, 3, devices=[0])
+    assert opened == [3] and closed == []
