@@ -439,7 +439,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--n", "--n-locs", dest="n", type=int, default=1_000_000,
                     help="locations per GPU-share (--n-locs: the same, safe under torch.distributed.run)")
-    ap.add_argument("--m", type=int, default=15)
+    ap.add_argument("--m", "--neighbours", dest="m", type=int, default=15)
     ap.add_argument("--covfun", default="matern15_isotropic")
     ap.add_argument("--range", type=float, default=0.05)
     ap.add_argument("--n-chromatic", type=int, default=10)
