@@ -310,6 +310,7 @@ struct TileState {
   double* gdw_s;  // foreign slots x C: their dw of the current colour
   int* wflag;
   unsigned* spin_s;
+  int* pub_s;     // wave-local tiles: the last phase whose first own batch has drawn (wave 0; hand-off poll gate)
   __amdgpu_buffer_rsrc_t gran;
   unsigned call;
   int gsl;                          // this phase's first foreign slot index of the thread (loaded a phase ahead)
@@ -954,6 +955,8 @@ __device__ __forceinline__ void tile_phase_wl(const TileDev& D, const TileLaunch
       tile_prep_items<C, 64, RMAX>(D, a, S.sc_s, S.seed_s, s, cur, lane);
     }
     tile_own_wl<C, RMAX, PROBE, SH>(D, a, sh, S, cur, epoch, acc_w, bi == bfirst);
+    if (bi == bfirst && S.wv == 0 && lane == 0)  // the exchange wave's poll gate (tile_phase_xw)
+      __hip_atomic_store(S.pub_s, ph, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const int R = cur.R;
     if (bi + W >= bend) {  // this wave's last batch of the colour: its records are dead
       if (!DB && more) tile_load_items<C, 64, RMAX, SH>(D, S.batch_s[bnext], nxt, lane);
@@ -1134,6 +1137,13 @@ __device__ __forceinline__ void tile_phase_xw(const TileDev& D, TileState& S, in
   // cells and the colour's ghost cells by this wave at the phase start, one
   // 4-B load per 64-B segment: 3,160-3,400 vs 2,275 us per 10-sweep launch at
   // the headline -- the polls wait behind the prefetch.)
+  // Wave-local tiles: the first poll round waits until this tile's wave 0 has
+  // drawn its first batch of the colour -- the neighbours draw theirs at about
+  // the same time, so earlier rounds would only find old granules (each poll
+  // is an L2-bypassing request: they were most of the traffic above the
+  // layout's bytes).  Wave 0 has a batch whenever the colour has one here.
+  if (WL && !LAG && S.bptr_s[c] < S.bptr_s[c + 1])
+    while (__hip_atomic_load(S.pub_s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < ph) __builtin_amdgcn_s_sleep(1);
   // hand-off: every (foreign slot, chain) of colour c until its granule
   // carries this epoch -> gdw_s (polls in flight per lane; a retry waits for
   // this wave's own polls only).  (Measured and dropped: a train of 3 poll
@@ -1320,6 +1330,8 @@ __device__ __forceinline__ void sweep_tiles_body(const TileDev& D0, TileLaunch a
   S.wflag = S.bsp_s + K + 1;                     // NW: the wave holds a slot start
   S.spin_s = reinterpret_cast<unsigned*>(S.wflag + NW);  // NNGP_PROBE=2: max poll spins of the phase
   if (PROBE == 2 && t == 0) *S.spin_s = 0;
+  S.pub_s = reinterpret_cast<int*>(S.spin_s + 1);        // (tile_lds_bytes' 64-byte tail)
+  if (t == 0) *S.pub_s = -1;
   TSTAMP(S, -1);
   for (int lr = t; lr < nrows; lr += NT) {
     const size_t g = (size_t)D.erow[row0 + lr] * CS;
