@@ -107,6 +107,8 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
       ("ssr", beta_0)                          -> sum of squared residuals
     Every chain yields every step of an iteration (None = nothing to do), so
     the chains stay in lockstep.  Returns {"state", "records", "acceptance"}."""
+    # (runif(1) is rng.random(): the same draw as rng.uniform() bit for bit,
+    # without its argument handling -- 0.36 vs 1.5 us a call)
     rng = np.random.default_rng(int(iter_start) + i + 1)
     key = _philox_key(iter_start, i + 1, seed)
     covfun = space_time_model["covfun"]["stationary_covfun"]
@@ -167,7 +169,7 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
                                new_ls - params["log_scale"], params["log_noise_variance"])
             ok = _proposal_ok(st, on_chol_error)
             if ok:
-                if ratio > math.log(rng.uniform()):
+                if ratio > math.log(rng.random()):
                     params["shape"] = new_shape
                     params["log_scale"] = new_ls
                     ctx.accept_field()
@@ -196,7 +198,7 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
         lls = res[1] if ok else None
         if ok:
             gp_ratio = lls[0] - lls[1]
-            if gp_ratio > math.log(rng.uniform()):
+            if gp_ratio > math.log(rng.random()):
                 params["shape"] = new_shape
                 params["log_scale"] = new_ls
                 ctx.accept_factor()
@@ -248,7 +250,7 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
             innov = rng.normal(0.0, 0.01)
             if math.exp(params["log_noise_variance"] + innov) < var_y:
                 lnv = params["log_noise_variance"]
-                if -0.5 * n_obs * innov - 0.5 * ssr * (math.exp(-lnv - innov) - math.exp(-lnv)) > math.log(rng.uniform()):
+                if -0.5 * n_obs * innov - 0.5 * ssr * (math.exp(-lnv - innov) - math.exp(-lnv)) > math.log(rng.random()):
                     params["log_noise_variance"] = lnv + innov
 
         # ---- records (:305-311)
