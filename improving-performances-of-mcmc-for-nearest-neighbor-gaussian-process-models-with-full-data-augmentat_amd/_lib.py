@@ -38,7 +38,7 @@ ABI_SYMBOLS = (
     "nngp_accept_field", "nngp_beta0_stats", "nngp_sum_squared_residuals", "nngp_spmv",
     "nngp_tri_solve", "nngp_sweep_timed", "nngp_device_normals", "nngp_get_sweep_r",
     "nngp_ctx_create_shard", "nngp_shard_unique_id", "nngp_shard_comm_init", "nngp_sweep_chains_group",
-    "nngp_records_reserve", "nngp_record_field", "nngp_get_records",
+    "nngp_records_reserve", "nngp_record_field", "nngp_get_records", "nngp_records_stream",
     "nngp_shard_ipc_handle", "nngp_shard_ipc_open", "nngp_shard_sync",
     "nngp_factor_chains", "nngp_loglik_chains", "nngp_field_response_ratio_chains",
     "nngp_sum_squared_residuals_chains", "nngp_loglik_pair_chains",
@@ -139,6 +139,7 @@ def _load():
     L.nngp_records_reserve.argtypes = [_vp, C.c_int]
     L.nngp_record_field.argtypes = [_vp, C.c_int]
     L.nngp_get_records.argtypes = [_vp, C.c_int, C.c_int, _dp]
+    L.nngp_records_stream.argtypes = [_vp, _vp, C.c_int]
     return L
 
 

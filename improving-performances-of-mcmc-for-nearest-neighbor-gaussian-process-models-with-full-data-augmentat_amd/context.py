@@ -44,6 +44,7 @@ class ChainContext:
             check(lib.nngp_ctx_create_shard(*args, int(_shard[0]), int(_shard[1]), C.byref(h)))
         self._h = h
         self._sel = 0
+        self._rec_host = {}  # chain -> host array its records stream into (records_stream)
 
     def select(self, chain: int) -> "ChainContext":
         if chain != self._sel:
@@ -117,9 +118,23 @@ class ChainContext:
     def records_reserve(self, n_rows: int) -> None:
         """Device buffer of n_rows recorded fields for the selected chain."""
         self._chk(lib.nngp_records_reserve(self._h, int(n_rows)))
+        self._rec_host.pop(self._sel, None)
 
     def record_field(self, row: int) -> None:
         self._chk(lib.nngp_record_field(self._h, int(row)))
+
+    def records_stream(self, host: np.ndarray | None) -> None:
+        """Stream the selected chain's recorded rows into `host` (C-contiguous
+        float64, reserved rows x n) while the chain runs; get_records(0, rows,
+        out=host) then only waits for them.  None ends the binding.  The
+        context keeps a reference to `host` while it is bound."""
+        if host is None:
+            self._chk(lib.nngp_records_stream(self._h, None, 0))
+            self._rec_host.pop(self._sel, None)
+            return
+        assert host.dtype == np.float64 and host.flags.c_contiguous and host.ndim == 2 and host.shape[1] == self.n
+        self._chk(lib.nngp_records_stream(self._h, host.ctypes.data, int(host.shape[0])))
+        self._rec_host[self._sel] = host
 
     def get_records(self, row0: int, n_rows: int, out: np.ndarray | None = None) -> np.ndarray:
         """Rows [row0, row0 + n_rows) of the records; into `out` (C-contiguous

@@ -20,6 +20,7 @@
 #include "../../include/nngp.h"
 #include "graph_prep.h"
 #include "kernels.h"
+#include "rec_stream.h"
 
 using namespace nngp;
 
@@ -39,6 +40,7 @@ struct ChainState {
   double* mu_d = nullptr;
   double* rec_d = nullptr;  // on-device field records: rec_rows x n, location order
   int rec_rows = 0;
+  double* rec_host = nullptr;  // caller's host array the rows are streamed into (nngp_records_stream)
   bool have_factor[2] = {false, false};
   bool have_field = false, have_mu = false, mu_is_const = true;
   double mu_beta0 = 0.0;
@@ -88,6 +90,7 @@ struct nngp_ctx {
     if (tile_counted) tile_ctx_count(device)--;
   }
   bool tile_counted = false;  // counted in tile_ctx_count(device)
+  RecordStreamer* recs = nullptr;  // record rows -> host arrays (nngp_records_stream), lazily started
   // a sweep returned without a host sync: its tile timeout word is checked
   // after the next one (sync_stream)
   bool tile_pending = false;
@@ -563,6 +566,10 @@ void nngp_ctx_destroy(nngp_ctx* c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->st) hipStreamSynchronize(c->st);
+  if (c->recs) {
+    c->recs->stop();
+    delete c->recs;
+  }
   for (auto& kv : c->graphs) hipGraphExecDestroy(kv.second);
   for (auto g : c->graph_objs) hipGraphDestroy(g);
   std::vector<void*> ptrs = {c->locs_d, c->sc_d, c->nn_d, c->linv_cur_d, c->sinfo_d, c->compact_loc_d,
@@ -1520,6 +1527,10 @@ int nngp_records_reserve(nngp_ctx* c, int n_rows) {
   int rc;
   if ((rc = set_device(c))) return rc;
   ChainState& S = c->ch[c->cur];
+  if (S.rec_host) {  // a reserve ends the binding of a host array
+    S.rec_host = nullptr;
+    HIPCHK(c, c->recs->drain());
+  }
   if (n_rows == S.rec_rows && (S.rec_d || n_rows == 0)) return NNGP_OK;
   if (S.rec_d) {
     { int ss_ = sync_stream(c); if (ss_) return ss_; }
@@ -1547,6 +1558,35 @@ int nngp_record_field(nngp_ctx* c, int row) {
   if ((rc = set_device(c))) return rc;
   // device row order -> location order, stays on the device (no host sync)
   HIPCHK(c, launch_permute_gather(c->st, c->n, c->dpos_d, S.field_d, S.rec_d + (size_t)row * c->n));
+  if (S.rec_host) {  // and on to the bound host array behind the stream (rec_stream.h)
+    hipEvent_t ev = nullptr;
+    HIPCHK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    hipError_t e = hipEventRecord(ev, c->st);
+    if (e != hipSuccess) hipEventDestroy(ev);
+    HIPCHK(c, e);
+    c->recs->push({ev, S.rec_d + (size_t)row * c->n, S.rec_host + (size_t)row * c->n, (size_t)c->n});
+  }
+  return NNGP_OK;
+}
+
+int nngp_records_stream(nngp_ctx* c, double* host, int n_rows) {
+  if (!c) return NNGP_ERR_ARG;
+  ChainState& S = c->ch[c->cur];
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  if (S.rec_host) {
+    S.rec_host = nullptr;
+    HIPCHK(c, c->recs->drain());
+  }
+  if (!host) return NNGP_OK;
+  if (!S.rec_d || n_rows != S.rec_rows)
+    return fail_msg(c, NNGP_ERR_ARG, "records_stream: the host array must have the reserved rows (records_reserve first)");
+  if (!c->recs) c->recs = new (std::nothrow) RecordStreamer();
+  if (!c->recs || !c->recs->start(c->device)) {
+    hipGetLastError();
+    return fail_msg(c, NNGP_ERR_NOMEM, "records_stream: staging buffers or worker could not be set up");
+  }
+  S.rec_host = host;
   return NNGP_OK;
 }
 
@@ -1558,6 +1598,11 @@ int nngp_get_records(nngp_ctx* c, int row0, int n_rows, double* out) {
   int rc;
   if ((rc = set_device(c))) return rc;
   { int ss_ = sync_stream(c); if (ss_) return ss_; }
+  if (S.rec_host && out == S.rec_host + (size_t)row0 * c->n) {
+    // the bound array: its rows were streamed as they were recorded
+    HIPCHK(c, c->recs->drain());
+    return NNGP_OK;
+  }
   HIPCHK(c, hipMemcpy(out, S.rec_d + (size_t)row0 * c->n, sizeof(double) * (size_t)n_rows * c->n, hipMemcpyDeviceToHost));
   return NNGP_OK;
 }

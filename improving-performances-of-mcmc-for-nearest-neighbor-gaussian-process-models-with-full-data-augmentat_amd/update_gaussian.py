@@ -37,6 +37,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 import threading
 
 import numpy as np
@@ -131,8 +132,11 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
         rec["beta"] = np.zeros((n_iterations_update, X["X"].shape[1]))
     acc_suf = np.zeros(n_iterations_update)
     acc_anc = np.zeros(n_iterations_update)
-    # recorded fields stay on the device until the end of the call
-    # (records$field, :56,311); host copies per iteration if HBM is short
+    # recorded fields (records$field, :56,311) are kept on the device and
+    # streamed into rec["field"] by the library while the chain runs
+    # (records_stream; NNGP_RECORDS_STREAM=0: copied at the end of the call,
+    # the host pages touched meanwhile); host copies per iteration if HBM is
+    # short
     n_rec = rec["field"].shape[0]
     dev_rec = n_rec > 0
     if dev_rec:
@@ -142,7 +146,14 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
             dev_rec = False
     if not dev_rec:
         rec["field"][:] = 0.0
-    touch = _prefault(rec["field"]) if dev_rec else None
+    streamed = False
+    if dev_rec and os.environ.get("NNGP_RECORDS_STREAM", "1") != "0":
+        try:
+            ctx.records_stream(rec["field"])
+            streamed = True
+        except (AttributeError, NNGPError):
+            pass
+    touch = _prefault(rec["field"]) if dev_rec and not streamed else None
 
     # Vecchia factor of the current state (:67-74)
     ctx.factor(0, covfun, covparms(sp_names, params["shape"]))
@@ -268,7 +279,8 @@ def _chain_program(i, state, ctx, X, observed_field, space_time_model, va, n_ite
                 rec["field"][int(it * field_thinning) - 1] = ctx.get_field()
 
     if dev_rec:
-        touch.join()
+        if touch is not None:
+            touch.join()
         ctx.get_records(0, n_rec, out=rec["field"])
         ctx.records_reserve(0)
     params["field"] = ctx.get_field()

@@ -37,6 +37,7 @@
  *   nngp_beta0_stats ......... beta_0 Gibbs block, update_Gaussian.R:221-222
  *   nngp_sum_squared_residuals update_Gaussian.R:281
  *   nngp_record_field ........ records$field[i, ] = field, update_Gaussian.R:305-311
+ *   nngp_records_stream ...... records$field in host memory while the chain runs (same lines)
  *   nngp_spmv / nngp_tri_solve sparse_chol %*% X (update_Gaussian.R:79,147) /
  *                              Matrix::solve (initialize.R:208, predict.R:46)
  */
@@ -50,7 +51,7 @@
 extern "C" {
 #endif
 
-#define NNGP_ABI_VERSION 12  /* 12: nngp_info gained tile_rows_needed, device_lds */
+#define NNGP_ABI_VERSION 13  /* 13: nngp_records_stream; 12: nngp_info gained tile_rows_needed, device_lds */
 #define NNGP_SHARD_ID_BYTES 128 /* RCCL unique id */
 #define NNGP_IPC_HANDLE_BYTES 192 /* HIP IPC handles of a tile shard's granule buffer, w replica, flags */
 
@@ -178,6 +179,14 @@ int nngp_set_mu(nngp_ctx* ctx, const double* mu, double beta0);
 int nngp_records_reserve(nngp_ctx* ctx, int n_rows);
 int nngp_record_field(nngp_ctx* ctx, int row);
 int nngp_get_records(nngp_ctx* ctx, int row0, int n_rows, double* out);
+/* Streams the selected chain's recorded rows into a caller-owned host array
+ * (n_rows x n row-major, n_rows = the reserved rows) as they are recorded: a
+ * worker thread copies each row behind the stream while the chain runs, and
+ * nngp_get_records(ctx, row0, k, host + row0 * n) only waits for them.  The
+ * array must stay valid until that get_records, the next records_reserve,
+ * nngp_records_stream(ctx, NULL, 0) or nngp_ctx_destroy, which all end the
+ * binding (after the rows in flight have landed). */
+int nngp_records_stream(nngp_ctx* ctx, double* host, int n_rows);
 
 /* Vecchia log-likelihood (A6) of z = field - beta0 under factor `which` */
 int nngp_loglik(nngp_ctx* ctx, int which, double beta0, double log_scale, double* ll);

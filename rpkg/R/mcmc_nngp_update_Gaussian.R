@@ -109,9 +109,14 @@ mcmc_nngp_update_Gaussian <- function(locs, X, observed_field, space_time_model,
   })
   acc_anc <- acc_suf <- matrix(0, n_iterations_update, C)
   IW <- vector("list", C)
+  RB <- vector("list", C)  # host vectors the field records stream into while the chains run
   for (i in seq_len(C)) {  # :67-90
     nngp_set_chain(ctx, i - 1L)
-    if (n_saved > 0) nngp_records_reserve(ctx, n_saved)
+    if (n_saved > 0) {
+      nngp_records_reserve(ctx, n_saved)
+      RB[[i]] <- numeric(n_saved * length(P[[i]]$field))
+      nngp_records_stream(ctx, RB[[i]])
+    }
     nngp_factor(ctx, 0L, covfun, nngp_covparms(sp, P[[i]]$shape))
     nngp_set_field(ctx, P[[i]]$field)
     if (has_locs) IW[[i]] <- .nngp_interweave(ctx, X, vecchia_approx)
@@ -262,7 +267,7 @@ mcmc_nngp_update_Gaussian <- function(locs, X, observed_field, space_time_model,
   lapply(seq_len(C), function(i) {
     nngp_set_chain(ctx, i - 1L)
     rec <- REC[[i]]
-    rec$field <- if (n_saved > 0) nngp_get_records(ctx, 0L, n_saved) else matrix(0, 0, length(P[[i]]$field))
+    rec$field <- if (n_saved > 0) nngp_get_records(ctx, 0L, n_saved, RB[[i]]) else matrix(0, 0, length(P[[i]]$field))
     if (n_saved > 0) nngp_records_reserve(ctx, 0L)
     params <- P[[i]]
     params$field <- nngp_get_field(ctx)

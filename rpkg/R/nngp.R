@@ -61,7 +61,9 @@ nngp_set_mu <- function(ctx, mu, beta_0)
   invisible(.Call(C_nngp_set_mu, ctx, if (is.null(mu)) NULL else as.double(mu), as.double(beta_0)))
 nngp_records_reserve <- function(ctx, n_rows) invisible(.Call(C_nngp_records_reserve, ctx, as.integer(n_rows)))
 nngp_record_field <- function(ctx, row) invisible(.Call(C_nngp_record_field, ctx, as.integer(row)))
-nngp_get_records <- function(ctx, row0, n_rows) .Call(C_nngp_get_records, ctx, as.integer(row0), as.integer(n_rows))
+nngp_get_records <- function(ctx, row0, n_rows, buf = NULL) .Call(C_nngp_get_records, ctx, as.integer(row0), as.integer(n_rows), buf)
+# rows x n numeric vector the selected chain's records stream into while it runs (NULL: release)
+nngp_records_stream <- function(ctx, buf) invisible(.Call(C_nngp_records_stream, ctx, buf))
 
 nngp_loglik <- function(ctx, which, beta_0, log_scale)
   .Call(C_nngp_loglik, ctx, as.integer(which), as.double(beta_0), as.double(log_scale))

@@ -250,12 +250,36 @@ SEXP C_nngp_record_field(SEXP p, SEXP row) {
   return R_NilValue;
 }
 
-/* rows [row0, row0 + n_rows) as an n_rows x n matrix (records$field layout) */
-SEXP C_nngp_get_records(SEXP p, SEXP row0, SEXP n_rows) {
+/* binds (or, for NULL, releases) a numeric vector of rows x n as the
+ * selected chain's streamed records (row-major); the caller keeps the vector
+ * referenced until the binding ends (R objects do not move) */
+SEXP C_nngp_records_stream(SEXP p, SEXP buf) {
+  nngp_ctx* c = get_ctx(p);
+  if (buf == R_NilValue) {
+    check(nngp_records_stream(c, NULL, 0), c);
+    return R_NilValue;
+  }
+  if (TYPEOF(buf) != REALSXP || XLENGTH(buf) % ctx_n(c) != 0) Rf_error("nngp: records buffer must be a numeric vector of rows x n");
+  check(nngp_records_stream(c, REAL(buf), (int)(XLENGTH(buf) / ctx_n(c))), c);
+  return R_NilValue;
+}
+
+/* rows [row0, row0 + n_rows) as an n_rows x n matrix (records$field layout);
+ * buf: the vector bound by C_nngp_records_stream (the rows are already
+ * there: the call only waits for them), or NULL */
+SEXP C_nngp_get_records(SEXP p, SEXP row0, SEXP n_rows, SEXP buf) {
   nngp_ctx* c = get_ctx(p);
   const int n = ctx_n(c), r = as_int(n_rows);
-  SEXP tmp = PROTECT(Rf_allocVector(REALSXP, (R_xlen_t)r * n));  /* row-major from the library */
-  check(nngp_get_records(c, as_int(row0), r, REAL(tmp)), c);
+  SEXP tmp;
+  if (buf == R_NilValue) {
+    tmp = PROTECT(Rf_allocVector(REALSXP, (R_xlen_t)r * n));  /* row-major from the library */
+    check(nngp_get_records(c, as_int(row0), r, REAL(tmp)), c);
+  } else {
+    if (TYPEOF(buf) != REALSXP || XLENGTH(buf) < (R_xlen_t)(as_int(row0) + r) * n) Rf_error("nngp: records buffer too short");
+    tmp = PROTECT(Rf_allocVector(REALSXP, (R_xlen_t)r * n));
+    check(nngp_get_records(c, as_int(row0), r, REAL(buf) + (R_xlen_t)as_int(row0) * n), c);
+    memcpy(REAL(tmp), REAL(buf) + (R_xlen_t)as_int(row0) * n, sizeof(double) * (size_t)r * n);
+  }
   SEXP out = PROTECT(Rf_allocMatrix(REALSXP, r, n));
   for (int i = 0; i < r; ++i)
     for (int j = 0; j < n; ++j) REAL(out)[i + (R_xlen_t)j * r] = REAL(tmp)[(R_xlen_t)i * n + j];
@@ -628,7 +652,8 @@ static const R_CallMethodDef call_methods[] = {
     E(C_nngp_set_mu, 3),
     E(C_nngp_records_reserve, 2),
     E(C_nngp_record_field, 2),
-    E(C_nngp_get_records, 3),
+    E(C_nngp_get_records, 4),
+    E(C_nngp_records_stream, 2),
     E(C_nngp_loglik, 4),
     E(C_nngp_sweep, 8),
     E(C_nngp_sweep_chains, 7),

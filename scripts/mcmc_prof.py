@@ -1,5 +1,6 @@
 """cProfile of the bench's MCMC-iterations measurement (host-side time of
-the lockstep chain driver; diagnostic)."""
+the lockstep chain driver; diagnostic).  `--no-cprofile`: the same
+iterations without the profiler (for rocprofv3 --hip-trace timelines)."""
 import cProfile
 import pstats
 import sys
@@ -19,6 +20,10 @@ ctx = bench.open_context(P, wl, "matern15_isotropic", cp, 0, 3, seed=3)
 wl["field0"] = ctx.get_field()
 sync = lambda: torch.cuda.synchronize(0)  # noqa: E731
 bench.mcmc_iterations(P, wl, "matern15_isotropic", cp, ctx, 2, 1, sync)
+if "--no-cprofile" in sys.argv:
+    print(bench.mcmc_iterations(P, wl, "matern15_isotropic", cp, ctx, 10, 1, sync), flush=True)
+    ctx.close()
+    sys.exit(0)
 pr = cProfile.Profile()
 pr.enable()
 r = bench.mcmc_iterations(P, wl, "matern15_isotropic", cp, ctx, 10, 1, sync)

@@ -46,11 +46,15 @@ static int lockstep(nngp_ctx* ctx, int n, double* f) {
   double ls[3] = {0.0, 0.2, -0.1}, shape[3] = {-2.3, -2.0, -2.6}, b0[3] = {0.1, -0.2, 0.0};
   double lnv[3] = {-1.0, -0.7, -1.2};
   const double lu_anc[3] = {-1e300, 1e300, -0.7}, lu_suf[3] = {1e300, -1e300, -0.3};
+  /* chains 1 and 2 stream their records into host arrays as the R drop-in
+     does; chain 0 keeps them on the device until get_records */
+  double* rb[3] = {NULL, malloc(sizeof(double) * (size_t)NIT * n), malloc(sizeof(double) * (size_t)NIT * n)};
   for (int k = 0; k < C; ++k) {
     const double cp[3] = {1.0, exp(shape[k]), 0.0};
     for (int i = 0; i < n; ++i) f[i] = 0.05 * k + sin(3.0 * i / n + k);
     CHECK(nngp_set_chain(ctx, k), ctx);
     CHECK(nngp_records_reserve(ctx, NIT), ctx);
+    if (rb[k]) CHECK(nngp_records_stream(ctx, rb[k], NIT), ctx);
     CHECK(nngp_factor(ctx, 0, NNGP_EXPONENTIAL_ISOTROPIC, cp, 3), ctx);
     CHECK(nngp_set_field(ctx, f), ctx);
     CHECK(nngp_set_mu(ctx, NULL, b0[k]), ctx);
@@ -115,16 +119,21 @@ static int lockstep(nngp_ctx* ctx, int n, double* f) {
   double* rec = malloc(sizeof(double) * (size_t)NIT * n);
   for (int k = 0; k < C; ++k) {
     CHECK(nngp_set_chain(ctx, k), ctx);
-    CHECK(nngp_get_records(ctx, 0, NIT, rec), ctx);
+    const double* rk = rb[k] ? rb[k] : rec;
+    CHECK(nngp_get_records(ctx, 0, NIT, rb[k] ? rb[k] : rec), ctx);
     for (int r = 0; r < NIT; ++r) {
       printf("record %d %d", k, r);
-      for (int i = 0; i < n; ++i) printf(" %a", rec[(size_t)r * n + i]);
+      for (int i = 0; i < n; ++i) printf(" %a", rk[(size_t)r * n + i]);
       printf("\n");
     }
     CHECK(nngp_get_field(ctx, f), ctx);
     printf("field %d", k);
     for (int i = 0; i < n; ++i) printf(" %a", f[i]);
     printf("\n");
+    if (rb[k]) {
+      CHECK(nngp_records_stream(ctx, NULL, 0), ctx);
+      free(rb[k]);
+    }
   }
   free(rec);
   return 0;

@@ -164,6 +164,61 @@ def test_device_records_of_the_field(P):
             ctx.get_records(0, 1)
 
 
+def test_records_streamed_into_host_arrays(P):
+    """nngp_records_stream: the rows recorded for two chains land in their
+    bound host arrays (bitwise the device records); a row of 1.5e6 doubles
+    spans several staging chunks; get_records on the bound array only waits;
+    a reserve ends the binding."""
+    n = 1_500_000
+    rng = np.random.default_rng(3)
+    locs = rng.uniform(size=(n, 2))
+    NN = P.find_ordered_nn(locs, 3)
+    col = P.naive_greedy_coloring(NN)
+    with P.ChainContext(locs, NN, col, np.arange(1, n + 1, dtype=np.int32), rng.normal(size=n), device=0,
+                        n_chains=2) as ctx:
+        hosts, fields = {}, {k: [rng.normal(size=n) for _ in range(3)] for k in (0, 1)}
+        for k in (0, 1):
+            ctx.select(k).records_reserve(3)
+            hosts[k] = np.full((3, n), np.nan)
+            ctx.records_stream(hosts[k])
+        for r in range(3):
+            for k in (0, 1):
+                ctx.select(k).set_field(fields[k][r])
+                ctx.record_field(r)
+        for k in (0, 1):
+            out = ctx.select(k).get_records(0, 3, out=hosts[k])
+            assert out is hosts[k]
+            np.testing.assert_array_equal(hosts[k], np.stack(fields[k]))
+            np.testing.assert_array_equal(ctx.get_records(0, 3), np.stack(fields[k]))  # device path
+        with pytest.raises(P.NNGPError):
+            ctx.select(0).records_stream(np.zeros((2, n)))  # not the reserved rows
+        ctx.select(0).records_reserve(3)  # ends the binding: later rows stay on the device
+        ctx.set_field(fields[1][0])
+        ctx.record_field(0)
+        ctx.get_records(1, 1)
+        np.testing.assert_array_equal(hosts[0][0], fields[0][0])
+
+
+def test_update_records_streamed_equal_end_of_call_copy(P, toy, monkeypatch):
+    """The MCMC update's field records streamed while the chains run equal the
+    end-of-call copy (NNGP_RECORDS_STREAM=0) bit for bit."""
+    from nngp_amd.update_gaussian import mcmc_nngp_update_Gaussian
+
+    outs = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("NNGP_RECORDS_STREAM", mode)
+        L = P.mcmc_nngp_initialize(toy["locs"], toy["observed_field"], X_locs=toy["X"],
+                                   stationary_covfun="exponential_isotropic", m=5, n_chains=2, seed=3)
+        outs.append(mcmc_nngp_update_Gaussian(L["locs"], L["X"], L["observed_field"], L["space_time_model"],
+                                              L["vecchia_approx"], L["states"], 8, field_thinning=0.5,
+                                              n_chromatic=2, contexts=L["_contexts"], seed=1))
+        for c in L["_contexts"]:
+            c.close()
+    for name in outs[0]:
+        np.testing.assert_array_equal(outs[0][name]["records"]["field"], outs[1][name]["records"]["field"])
+        np.testing.assert_array_equal(outs[0][name]["state"]["params"]["field"], outs[1][name]["state"]["params"]["field"])
+
+
 def test_update_records_field_thinning(P, toy):
     """records$field rows with field_thinning = 0.5: iterations 2, 4, ...; the
     last row is the final state's field."""
