@@ -107,6 +107,8 @@ struct nngp_ctx {
   // device buffers
   double* locs_d = nullptr;  // n x d row-major
   double* sc_d = nullptr;    // n x ds scaled coordinates
+  double* scm_d = nullptr;   // per-chain scaled coordinates of a multi-chain factor launch
+  size_t scm_cap = 0;        // its capacity in doubles
   int* nn_d = nullptr;       // n x b row-major, 0-based, -1 = NA
   const double** linv_cur_d = nullptr;  // C pointers: current factor of each chain
   const double** linv_cur_h = nullptr;  // pinned mirror
@@ -572,7 +574,7 @@ void nngp_ctx_destroy(nngp_ctx* c) {
   }
   for (auto& kv : c->graphs) hipGraphExecDestroy(kv.second);
   for (auto g : c->graph_objs) hipGraphDestroy(g);
-  std::vector<void*> ptrs = {c->locs_d, c->sc_d, c->nn_d, c->linv_cur_d, c->sinfo_d, c->compact_loc_d,
+  std::vector<void*> ptrs = {c->locs_d, c->sc_d, c->scm_d, c->nn_d, c->linv_cur_d, c->sinfo_d, c->compact_loc_d,
                              c->dr_d, c->slot_dpos_d, c->ent_pk_d, c->ent_src_d, c->ent_val_d, c->w_slot_d,
                              c->r_d, c->level_rows_d, c->obs_ptr_d, c->obs_idx_d, c->lm_d, c->y_d, c->tmp_d,
                              c->tmp2_d, c->partials_d, c->res_d, c->z_d, c->scal_d, c->dbg_d,
@@ -1369,6 +1371,67 @@ static int factor_enqueue(nngp_ctx* c, int k, int which, int covfun, const doubl
   return NNGP_OK;
 }
 
+// the factors of the chains in mask into slot `which` (covparms: C x ncp,
+// row k for chain k): one scaled-coordinate launch and one factor launch for
+// all of them (launch_factor_jobs; rows bitwise those of factor_enqueue per
+// chain); NNGP_FACTOR_JOBS=0, the sphere covariances and chains of different
+// Matern smoothness go chain by chain
+static int factor_enqueue_chains(nngp_ctx* c, int mask, int which, int covfun, const double* covparms, int ncp) {
+  const char* fj = std::getenv("NNGP_FACTOR_JOBS");  // per call (A/B in one process)
+  const bool off = fj && fj[0] == '0';
+  const bool sphere = covfun == NNGP_EXPONENTIAL_SPHERE || covfun == NNGP_MATERN_SPHERE;
+  int cnt = 0;
+  for (int k = 0; k < c->C; ++k) cnt += (mask >> k) & 1;
+  FactorJobs J;
+  int fam0 = -1;
+  double nu0 = 0.0;
+  bool same = true;
+  for (int k = 0; k < c->C && cnt >= 2 && !off && !sphere; ++k) {
+    if (!((mask >> k) & 1)) continue;
+    const double* cp = covparms + (size_t)k * ncp;
+    double var, nug, nu;
+    std::string err;
+    const int fam = covfun_family(covfun, c->d, cp, ncp, &var, &nug, &nu, err);
+    if (fam < 0) return fail_msg(c, NNGP_ERR_ARG, err);
+    if (J.n_jobs == 0) {
+      fam0 = fam;
+      nu0 = nu;
+    } else if (fam != fam0 || !(nu == nu0)) {
+      same = false;
+    }
+    const int j = J.n_jobs++;
+    for (int q = 0; q < 8; ++q) J.sa[j].c[q] = q < ncp ? cp[q] : 0.0;
+    J.sa[j].covfun = covfun;
+    J.var[j] = var;
+    J.nugget[j] = nug;
+    J.linv[j] = c->ch[k].linv_d[which];
+    J.fail[j] = c->fail_d + k;
+  }
+  if (cnt < 2 || off || sphere || !same) {
+    for (int k = 0; k < c->C; ++k)
+      if ((mask >> k) & 1) {
+        int rc = factor_enqueue(c, k, which, covfun, covparms + (size_t)k * ncp, ncp);
+        if (rc) return rc;
+      }
+    return NNGP_OK;
+  }
+  const int use_ds = c->d <= 2 ? 2 : (c->d == 3 ? 3 : 4);
+  const size_t need = (size_t)c->n * use_ds * J.n_jobs;
+  if (need > c->scm_cap) {
+    { int ss_ = sync_stream(c); if (ss_) return ss_; }
+    if (c->scm_d) hipFree(c->scm_d);
+    c->scm_d = nullptr;
+    c->scm_cap = 0;
+    HIPCHK(c, dalloc(&c->scm_d, need));
+    c->scm_cap = need;
+  }
+  for (int j = 0; j < J.n_jobs; ++j) J.sc[j] = c->scm_d + (size_t)j * c->n * use_ds;
+  for (int k = 0; k < c->C; ++k)
+    if ((mask >> k) & 1) c->ch[k].lgen[which] = ++c->gen;
+  HIPCHK(c, launch_factor_jobs(c->st, fam0, nu0, J, c->locs_d, c->n, c->d, use_ds, c->nn_d, c->b));
+  return NNGP_OK;
+}
+
 // after factor_enqueue of the chains in mask and a host sync that followed
 // the copy of the flags into fail_h: per-chain outcomes
 static int factor_outcomes(nngp_ctx* c, int which, int mask, int* status) {
@@ -1417,9 +1480,7 @@ int nngp_factor_chains(nngp_ctx* c, int which, int chain_mask, int covfun, const
     return fail_msg(c, NNGP_ERR_ARG, "factor_chains: bad args");
   int rc;
   if ((rc = set_device(c))) return rc;
-  for (int k = 0; k < c->C; ++k)
-    if ((chain_mask >> k) & 1)
-      if ((rc = factor_enqueue(c, k, which, covfun, covparms + (size_t)k * ncp, ncp))) return rc;
+  if ((rc = factor_enqueue_chains(c, chain_mask, which, covfun, covparms, ncp))) return rc;
   rc = factor_collect(c, which, chain_mask, status);
   return rc == NNGP_ERR_CHOL ? NNGP_OK : rc;  // per-chain outcomes in status
 }
@@ -2812,9 +2873,7 @@ static int step_common(nngp_ctx* c, int chain_mask, int covfun, const double* co
       return fail_msg(c, NNGP_ERR_STATE, buf);
     }
   }
-  for (int k = 0; k < c->C; ++k)
-    if ((chain_mask >> k) & 1)
-      if ((rc = factor_enqueue(c, k, 1, covfun, covparms + (size_t)k * ncp, ncp))) return rc;
+  if ((rc = factor_enqueue_chains(c, chain_mask, 1, covfun, covparms, ncp))) return rc;
   // provisional until the flags are back (factor_outcomes settles it)
   for (int k = 0; k < c->C; ++k)
     if ((chain_mask >> k) & 1) c->ch[k].have_factor[1] = true;

@@ -90,6 +90,26 @@ hipError_t launch_factor(hipStream_t st, int family, double var, double nugget, 
                          const double* sc, int ds, const int* nn, int n, int b, double* linv,
                          int* fail);
 
+// the factors of up to kMaxChains chains (one covariance family) in ONE
+// launch of each of the two kernels: scaled coordinates of every job (and its
+// failure flag reset to INT_MAX), then the factor rows of all jobs as one
+// grid-stride range (one tail instead of one per chain).  Rows bitwise those
+// of launch_scale_coords + launch_factor per job.
+struct ScaleArgs {
+  double c[8];  // covariance parameters
+  int covfun;
+};
+struct FactorJobs {
+  int n_jobs = 0;
+  ScaleArgs sa[kMaxChains];
+  double var[kMaxChains], nugget[kMaxChains];
+  double* sc[kMaxChains];                   // per-job scaled coordinates (n x ds)
+  double* linv[kMaxChains];
+  int* fail[kMaxChains];
+};
+hipError_t launch_factor_jobs(hipStream_t st, int family, double nu, const FactorJobs& J,
+                              const double* locs_rm, int n, int d, int ds, const int* nn, int b);
+
 // per-row statistics of B x (x shifted): partial sums of
 // {log L[k][0], u_k^2, a_k^2, a_k*u_k} with u = B (x - shift), a = B 1.
 // If out != nullptr, out[k] = u_k.  All arrays in device row order.

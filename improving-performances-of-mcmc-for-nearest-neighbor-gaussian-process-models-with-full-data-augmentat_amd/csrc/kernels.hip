@@ -15,6 +15,7 @@
 //   tri_level_kernel / _levels_block     (next) Matrix::solve by DAG level
 #include "kernels.h"
 #include "device_common.h"
+#include <climits>
 #include <cstdlib>
 
 #include <cmath>
@@ -199,15 +200,8 @@ __device__ __forceinline__ double corr(double dist, double nu, double norm) {
 }
 
 // ------------------------------------------------------------------ A4
-struct ScaleArgs {
-  double c[8];
-  int covfun;
-};
-
-__global__ void scale_coords_kernel(ScaleArgs a, const double* __restrict__ locs, int n, int d,
-                                    double* __restrict__ sc, int ds) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+__device__ __forceinline__ void scale_point(const ScaleArgs& a, const double* __restrict__ locs, int i, int d,
+                                            double* __restrict__ sc, int ds) {
   double x[4] = {0, 0, 0, 0}, o[4] = {0, 0, 0, 0};
   for (int k = 0; k < d && k < 4; ++k) x[k] = locs[(size_t)i * d + k];
   switch (a.covfun) {
@@ -233,6 +227,31 @@ __global__ void scale_coords_kernel(ScaleArgs a, const double* __restrict__ locs
       for (int k = 0; k < d; ++k) o[k] = x[k] / a.c[1];
   }
   for (int k = 0; k < ds; ++k) sc[(size_t)i * ds + k] = o[k];
+}
+
+__global__ void scale_coords_kernel(ScaleArgs a, const double* __restrict__ locs, int n, int d,
+                                    double* __restrict__ sc, int ds) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  scale_point(a, locs, i, d, sc, ds);
+}
+
+// every job's scaled coordinates (blockIdx.y = job) and its failure flag reset
+__global__ void scale_coords_jobs_kernel(FactorJobs J, const double* __restrict__ locs, int n, int d, int ds) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  switch (blockIdx.y) {  // constant indices into the kernel argument
+#define NNGP_SCALE_JOB(k)                                  \
+    case k:                                                \
+      if (i == 0) *J.fail[k] = INT_MAX;                    \
+      scale_point(J.sa[k], locs, i, d, J.sc[k], ds);       \
+      break;
+    NNGP_SCALE_JOB(0)
+    NNGP_SCALE_JOB(1)
+    NNGP_SCALE_JOB(2)
+    NNGP_SCALE_JOB(3)
+#undef NNGP_SCALE_JOB
+  }
 }
 
 hipError_t launch_scale_coords(hipStream_t st, int covfun, const double* cp, int ncp,
@@ -354,49 +373,61 @@ __device__ __forceinline__ int gather_coords(double (&X)[BM][DS], const int (&nc
   return bs;
 }
 
+// the job's entry of a per-job kernel-argument array (wave-uniform j; a
+// select chain keeps the argument in scalar registers instead of a private copy)
+template <class T>
+__device__ __forceinline__ T job_pick(const T (&v)[kMaxChains], int j) {
+  return j == 0 ? v[0] : j == 1 ? v[1] : j == 2 ? v[2] : v[3];
+}
+
 // Grid-stride over groups of 64 rows with a two-deep software pipeline: the
 // next group's coordinate gathers and the group after's neighbour indices
 // are in flight while this group's covariance/Cholesky runs (one wave per
 // SIMD fits the register footprint, so no other wave hides that latency).
+// The groups of all jobs (chains) form one range: group g is rows
+// (g mod G) * 64 + lane of job g / G, G = ceil(n / 64).
 template <int BM, int FAM, int DS, int V>
-__global__ __launch_bounds__(64) void factor_kernel(double var, double nugget, double nu, double norm,
-                                                   const double* __restrict__ sc,
-                                                   const int* __restrict__ nn, int n, int b,
-                                                   double* __restrict__ linv, int* __restrict__ fail) {
+__global__ __launch_bounds__(64) void factor_kernel(FactorJobs J, double nu, double norm,
+                                                   const int* __restrict__ nn, int n, int b) {
   __shared__ double tab[64];
   tab[threadIdx.x] = kExp2Tab[threadIdx.x];
   __syncthreads();
-  const double rsv = rsqrt_pos(var);
-  const int stride = gridDim.x * 64;
-  int i = blockIdx.x * 64 + threadIdx.x;
+  const int G = (n + 63) / 64, total = G * J.n_jobs;
+  const int stride = gridDim.x;
+  auto row_of = [&](int g, int& jb) {  // past the last group: row n (no work), last job
+    if (g >= total) {
+      jb = J.n_jobs - 1;
+      return n;
+    }
+    jb = g / G;
+    return (g - jb * G) * 64 + (int)threadIdx.x;
+  };
   int nc[BM], nx[BM];
   double X[BM][DS];
-  if (V & 2) {  // indices one group ahead only (no coordinates in flight)
-    load_nn_row<BM>(nx, nn, i, n, b);
-    for (int base = blockIdx.x * 64; base < n; base += stride, i += stride) {
-#pragma unroll
-      for (int r = 0; r < BM; ++r) nc[r] = nx[r];
-      const int bs = gather_coords<BM, DS>(X, nc, sc, i, n);
-      load_nn_row<BM>(nx, nn, i + stride, n, b);
-      if (i < n)
-        factor_row<BM, FAM, DS, V>([&](int r, int k) { return X[r][k]; }, bs, i, rsv, nugget, b, tab, linv, fail);
-    }
-    return;
-  }
+  int g = blockIdx.x, jc, jn;
+  int i = row_of(g, jc);
   load_nn_row<BM>(nc, nn, i, n, b);
-  int bs = gather_coords<BM, DS>(X, nc, sc, i, n);
-  load_nn_row<BM>(nx, nn, i + stride, n, b);
-  for (int base = blockIdx.x * 64; base < n; base += stride, i += stride) {
+  int bs = gather_coords<BM, DS>(X, nc, job_pick(J.sc, jc), i, n);
+  int i1 = row_of(g + stride, jn);
+  load_nn_row<BM>(nx, nn, i1, n, b);
+  for (; g < total; g += stride) {
+    int j2;
+    const int i2 = row_of(g + 2 * stride, j2);
     double Xn[BM][DS];
-    const int bsn = gather_coords<BM, DS>(Xn, nx, sc, i + stride, n);
-    load_nn_row<BM>(nx, nn, i + 2 * stride, n, b);
+    const int bsn = gather_coords<BM, DS>(Xn, nx, job_pick(J.sc, jn), i1, n);
+    load_nn_row<BM>(nx, nn, i2, n, b);
     if (i < n)
-      factor_row<BM, FAM, DS, V>([&](int r, int k) { return X[r][k]; }, bs, i, rsv, nugget, b, tab, linv, fail);
+      factor_row<BM, FAM, DS, V>([&](int r, int k) { return X[r][k]; }, bs, i, rsqrt_pos(job_pick(J.var, jc)),
+                                 job_pick(J.nugget, jc), b, tab, job_pick(J.linv, jc), job_pick(J.fail, jc));
 #pragma unroll
     for (int r = 0; r < BM; ++r)
 #pragma unroll
       for (int k = 0; k < DS; ++k) X[r][k] = Xn[r][k];
     bs = bsn;
+    i = i1;
+    jc = jn;
+    i1 = i2;
+    jn = j2;
   }
 }
 
@@ -659,10 +690,36 @@ static hipError_t launch_factor_one(hipStream_t st, double var, double nugget, d
       return hipGetLastError();
     }
   }
+  FactorJobs J;
+  J.n_jobs = 1;
+  J.var[0] = var;
+  J.nugget[0] = nugget;
+  J.sc[0] = const_cast<double*>(sc);
+  J.linv[0] = linv;
+  J.fail[0] = fail;
   const auto kern = factor_kernel<BM, FAM, DS, 0>;
   const int g = resident_grid(reinterpret_cast<const void*>(kern), (n + 63) / 64);
-  hipLaunchKernelGGL(kern, dim3(g), dim3(64), 0, st, NNGP_FACTOR_ARGS);
+  hipLaunchKernelGGL(kern, dim3(g), dim3(64), 0, st, J, nu, norm, nn, n, b);
   return hipGetLastError();
+}
+
+// all jobs in one factor_kernel launch (the register-resident block sizes)
+template <int BM, int FAM>
+static hipError_t launch_factor_jobs_bm(hipStream_t st, int ds, double nu, const FactorJobs& J, const int* nn,
+                                        int n, int b) {
+  const long long groups = (long long)((n + 63) / 64) * J.n_jobs;
+  if (groups > INT_MAX / 2) return hipErrorInvalidValue;  // group index arithmetic stays in int
+  auto go = [&](auto kern) {
+    const int g = resident_grid(reinterpret_cast<const void*>(kern), (int)groups);
+    hipLaunchKernelGGL(kern, dim3(g), dim3(64), 0, st, J, nu, 0.0, nn, n, b);
+    return hipGetLastError();
+  };
+  switch (ds) {
+    case 2: return go(factor_kernel<BM, FAM, 2, 0>);
+    case 3: return go(factor_kernel<BM, FAM, 3, 0>);
+    case 4: return go(factor_kernel<BM, FAM, 4, 0>);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 template <int BM, int FAM>
@@ -719,6 +776,34 @@ hipError_t launch_factor(hipStream_t st, int family, double var, double nugget, 
   return launch_factor_rt<1>(st, ds, NNGP_FACTOR_ARGS);
 }
 #undef NNGP_FACTOR_ARGS
+
+hipError_t launch_factor_jobs(hipStream_t st, int family, double nu, const FactorJobs& J,
+                              const double* locs_rm, int n, int d, int ds, const int* nn, int b) {
+  if (J.n_jobs < 1 || J.n_jobs > kMaxChains || b < 1 || b > kBMaxRt) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(scale_coords_jobs_kernel, dim3((n + kBlock - 1) / kBlock, J.n_jobs), dim3(kBlock), 0, st, J,
+                     locs_rm, n, d, ds);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  // one launch for the register-resident kernels; the others (general
+  // Matern, b > 21, the lane-pair opt-in) run job after job as launch_factor
+  const char* pe = std::getenv("NNGP_FACTOR_PAIR");
+  const bool pair = b > 12 && b <= 16 && family != 2 && pe && pe[0] == '1';
+  if (family != 2 && !pair) {
+    if (b <= 8) return family == 0 ? launch_factor_jobs_bm<8, 0>(st, ds, nu, J, nn, n, b)
+                                   : launch_factor_jobs_bm<8, 1>(st, ds, nu, J, nn, n, b);
+    if (b <= 12) return family == 0 ? launch_factor_jobs_bm<12, 0>(st, ds, nu, J, nn, n, b)
+                                    : launch_factor_jobs_bm<12, 1>(st, ds, nu, J, nn, n, b);
+    if (b <= 16) return family == 0 ? launch_factor_jobs_bm<16, 0>(st, ds, nu, J, nn, n, b)
+                                    : launch_factor_jobs_bm<16, 1>(st, ds, nu, J, nn, n, b);
+    if (b <= 21) return family == 0 ? launch_factor_jobs_bm<21, 0>(st, ds, nu, J, nn, n, b)
+                                    : launch_factor_jobs_bm<21, 1>(st, ds, nu, J, nn, n, b);
+  }
+  for (int j = 0; j < J.n_jobs; ++j)
+    if ((e = launch_factor(st, family, J.var[j], J.nugget[j], nu, J.sc[j], ds, nn, n, b, J.linv[j], J.fail[j])) !=
+        hipSuccess)
+      return e;
+  return hipSuccess;
+}
 
 // ------------------------------------------------------------------ reductions
 __device__ __forceinline__ double wave_sum(double v) {

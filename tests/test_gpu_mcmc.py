@@ -331,3 +331,36 @@ def test_mh_step_calls_equal_separate_calls_bitwise(P):
         np.testing.assert_array_equal(props[k], props_ref[k])
     np.testing.assert_array_equal(props[1], props_ref[1])  # the failed chain kept its field
     assert st_s2[1] == 0 and lp2[1] == lp2_ref[1] and lc2[1] == lc2_ref[1]
+
+
+@pytest.mark.parametrize("m,covfun", [(5, "exponential_isotropic"), (10, "matern15_isotropic"),
+                                      (15, "matern15_isotropic"), (20, "exponential_isotropic"),
+                                      (15, "matern_isotropic")])
+def test_factor_jobs_launch_equals_chain_by_chain(P, m, covfun, monkeypatch):
+    """factor_chains of several chains in one scaled-coordinate and one factor
+    launch (launch_factor_jobs) gives every chain's Linv and failure flag
+    bitwise as the chain-by-chain launches (NNGP_FACTOR_JOBS=0), including a
+    chain whose proposal is not positive definite and a chain not in the mask."""
+    from nngp_amd._lib import NNGP_ERR_CHOL
+
+    n, C = 3000, 4
+    locs, NN, col, lm, y = make_problem(P, n, m, seed=21)
+    if covfun == "matern_isotropic":
+        cps = [[1.0, 0.05, 1.2, 0.0], [1.3, 0.04, 1.2, 0.1], [0.8, 0.07, 1.2, 0.0], [1.0, 0.05, 1.2, 0.0]]
+    else:
+        cps = [[1.0, 0.05, 0.0], [1.3, 0.04, 0.1], [0.8, 0.07, 0.0], [1.0, 0.05, 0.0]]
+    bad = list(cps[2])
+    bad[-1] = -2.0  # nugget -2: diagonal 1 + nugget < 0, not positive definite
+    outs = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("NNGP_FACTOR_JOBS", mode)
+        with P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=C) as ctx:
+            st = ctx.factor_chains(1, 0b1011, covfun, np.array(cps))
+            linv = [ctx.select(k).get_linv(1) for k in (0, 1, 3)]
+            st2 = ctx.factor_chains(1, 0b0110, covfun, np.array([cps[0], cps[1], bad, cps[3]]))
+            linv.append(ctx.select(1).get_linv(1))
+            outs.append((list(st), list(st2), linv))
+    assert outs[0][0] == outs[1][0] == [0, 0, 0, 0]
+    assert outs[0][1] == outs[1][1] and outs[0][1][2] == NNGP_ERR_CHOL and outs[0][1][1] == 0
+    for a, b in zip(outs[0][2], outs[1][2]):
+        np.testing.assert_array_equal(a, b)
