@@ -199,7 +199,8 @@ def mcmc_iterations(P, wl, covfun, cp, ctx, iters, warmup, sync):
     del kept
     return {"metric": "MCMC iterations/s (update_Gaussian.R:101-313, n_chromatic=10, all chains of the GPU)",
             "value": iters / el, "unit": "iterations/s", "chains": C, "iterations": iters,
-            "ms_per_iteration": el * 1e3 / iters, "field_thinning": 1.0}
+            "ms_per_iteration": el * 1e3 / iters, "field_thinning": 1.0,
+            "iterations_per_update_call": iters}
 
 
 def pmc_traffic(chains, n, m, kernel):
@@ -448,8 +449,9 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--mcmc-iters", type=int, default=40,
-                    help="timed MCMC iterations for the secondary metric (0: skip)")
+    ap.add_argument("--mcmc-iters", type=int, default=200,
+                    help="timed MCMC iterations for the secondary metric, one update call (default: the "
+                         "reference's n_iterations_update = 200, Scripts/mcmc_nngp_run.R:3; 0: skip)")
     ap.add_argument("--multi", choices=["shard-weak", "shard-strong", "replicas"], default="shard-weak",
                     help="N > 1: the sharded sweep of ONE field over the N GPUs with n = N x --n (shard-weak, "
                          "default) or n = --n (shard-strong), or independent chains per GPU (replicas)")
