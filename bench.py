@@ -340,7 +340,7 @@ def shard_main(P, args, world, rank, local_rank, dist, scaling):
     1e6-location fields per second (a sweep of the 8e6-location field counts 8)."""
     import torch
 
-    from nngp_amd.shard import ShardContext, _agreed, init_shard_comm
+    from nngp_amd.shard import ShardContext, _agreed, _same_everywhere, init_shard_comm
 
     covfun, cp, C, nc = args.covfun, [1.0, args.range, 0.0], args.chains, args.n_chromatic
     n = args.n * world if scaling == "weak" else args.n
@@ -361,6 +361,8 @@ def shard_main(P, args, world, rank, local_rank, dist, scaling):
                                device=local_rank, n_chains=k), list(range(C))))
     ctx = groups[0][0]
     try:
+        if world > 1:  # the groups must match across ranks (their shards pair up rank by rank)
+            _same_everywhere(dist, [list(ids) for _, ids in groups], "the chain groups")
         for g, _ in groups:
             init_shard_comm(g, dist, rccl=False)
         rng = np.random.default_rng(7)

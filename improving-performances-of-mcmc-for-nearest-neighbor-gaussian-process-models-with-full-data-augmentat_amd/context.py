@@ -142,7 +142,11 @@ class ChainContext:
         if out is None:
             out = np.empty((int(n_rows), self.n))
         assert out.dtype == np.float64 and out.flags.c_contiguous and out.shape == (int(n_rows), self.n)
+        host = self._rec_host.get(self._sel)
+        bound = host is not None and out.ctypes.data == host.ctypes.data + int(row0) * self.n * 8
         self._chk(lib.nngp_get_records(self._h, int(row0), int(n_rows), out.reshape(-1)))
+        if bound:  # get_records on the bound array ends the binding (nngp.h)
+            self._rec_host.pop(self._sel, None)
         return out
 
     def set_mu(self, mu, beta0: float) -> None:

@@ -41,6 +41,7 @@ struct ChainState {
   double* rec_d = nullptr;  // on-device field records: rec_rows x n, location order
   int rec_rows = 0;
   double* rec_host = nullptr;  // caller's host array the rows are streamed into (nngp_records_stream)
+  std::vector<uint8_t> rec_pushed;  // rows handed to the streamer since the binding (the others: copied at get_records)
   bool have_factor[2] = {false, false};
   bool have_field = false, have_mu = false, mu_is_const = true;
   double mu_beta0 = 0.0;
@@ -1626,6 +1627,7 @@ int nngp_record_field(nngp_ctx* c, int row) {
     if (e != hipSuccess) hipEventDestroy(ev);
     HIPCHK(c, e);
     c->recs->push({ev, S.rec_d + (size_t)row * c->n, S.rec_host + (size_t)row * c->n, (size_t)c->n});
+    S.rec_pushed[row] = 1;
   }
   return NNGP_OK;
 }
@@ -1635,18 +1637,21 @@ int nngp_records_stream(nngp_ctx* c, double* host, int n_rows) {
   ChainState& S = c->ch[c->cur];
   int rc;
   if ((rc = set_device(c))) return rc;
+  // a call that fails leaves an existing binding as it was
+  if (host && (!S.rec_d || n_rows != S.rec_rows))
+    return fail_msg(c, NNGP_ERR_ARG, "records_stream: the host array must have the reserved rows (records_reserve first)");
+  if (host && !c->recs) c->recs = new (std::nothrow) RecordStreamer();
+  if (host && (!c->recs || !c->recs->start(c->device))) {
+    hipGetLastError();
+    return fail_msg(c, NNGP_ERR_NOMEM, "records_stream: staging buffers or worker could not be set up");
+  }
   if (S.rec_host) {
     S.rec_host = nullptr;
     HIPCHK(c, c->recs->drain());
   }
   if (!host) return NNGP_OK;
-  if (!S.rec_d || n_rows != S.rec_rows)
-    return fail_msg(c, NNGP_ERR_ARG, "records_stream: the host array must have the reserved rows (records_reserve first)");
-  if (!c->recs) c->recs = new (std::nothrow) RecordStreamer();
-  if (!c->recs || !c->recs->start(c->device)) {
-    hipGetLastError();
-    return fail_msg(c, NNGP_ERR_NOMEM, "records_stream: staging buffers or worker could not be set up");
-  }
+  // rows recorded before the binding are not streamed: get_records copies them
+  S.rec_pushed.assign((size_t)S.rec_rows, 0);
   S.rec_host = host;
   return NNGP_OK;
 }
@@ -1660,8 +1665,20 @@ int nngp_get_records(nngp_ctx* c, int row0, int n_rows, double* out) {
   if ((rc = set_device(c))) return rc;
   { int ss_ = sync_stream(c); if (ss_) return ss_; }
   if (S.rec_host && out == S.rec_host + (size_t)row0 * c->n) {
-    // the bound array: its rows were streamed as they were recorded
+    // the bound array: its rows were streamed as they were recorded; rows
+    // never handed to the streamer (recorded before the binding, or never
+    // recorded) are copied from the device as on the unbound path.  The call
+    // ends the binding (nngp.h): later record_field calls stay on the device.
+    S.rec_host = nullptr;
     HIPCHK(c, c->recs->drain());
+    for (int r = row0; r < row0 + n_rows;) {
+      if (S.rec_pushed[r]) { ++r; continue; }
+      int e = r;
+      while (e < row0 + n_rows && !S.rec_pushed[e]) ++e;
+      HIPCHK(c, hipMemcpy(out + (size_t)(r - row0) * c->n, S.rec_d + (size_t)r * c->n, sizeof(double) * (size_t)(e - r) * c->n,
+                          hipMemcpyDeviceToHost));
+      r = e;
+    }
     return NNGP_OK;
   }
   HIPCHK(c, hipMemcpy(out, S.rec_d + (size_t)row0 * c->n, sizeof(double) * (size_t)n_rows * c->n, hipMemcpyDeviceToHost));

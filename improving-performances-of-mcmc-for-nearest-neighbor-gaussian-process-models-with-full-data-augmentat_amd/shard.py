@@ -130,6 +130,19 @@ def _agreed(dist, fn):
     return res
 
 
+def _same_everywhere(dist, value, what: str):
+    """The rank-local `value` (a picklable decision every rank makes on its
+    own, e.g. the chain groups of context.split_groups) must be the same on
+    every rank: ranks that went different ways would wait for peers that
+    never come.  Raises on every rank if any differs."""
+    vals = [None] * dist.get_world_size()
+    dist.all_gather_object(vals, value)
+    if any(v != vals[0] for v in vals):
+        raise RuntimeError(f"shard setup: ranks disagree on {what}: " +
+                           "; ".join(f"rank {r}: {v}" for r, v in enumerate(vals)))
+    return value
+
+
 def init_shard_comm(ctx: ShardContext, dist, rccl: bool = True) -> None:
     """Collective over the torch.distributed group: the RCCL communicator and,
     for a tile shard, the exchange of the IPC handles (every step agreed by

@@ -182,10 +182,12 @@ int nngp_get_records(nngp_ctx* ctx, int row0, int n_rows, double* out);
 /* Streams the selected chain's recorded rows into a caller-owned host array
  * (n_rows x n row-major, n_rows = the reserved rows) as they are recorded: a
  * worker thread copies each row behind the stream while the chain runs, and
- * nngp_get_records(ctx, row0, k, host + row0 * n) only waits for them.  The
+ * nngp_get_records(ctx, row0, k, host + row0 * n) only waits for them (rows
+ * not recorded since the binding are copied from the device there).  The
  * array must stay valid until that get_records, the next records_reserve,
  * nngp_records_stream(ctx, NULL, 0) or nngp_ctx_destroy, which all end the
- * binding (after the rows in flight have landed). */
+ * binding (after the rows in flight have landed).  A call that fails leaves
+ * an existing binding in place. */
 int nngp_records_stream(nngp_ctx* ctx, double* host, int n_rows);
 
 /* Vecchia log-likelihood (A6) of z = field - beta0 under factor `which` */

@@ -110,6 +110,13 @@ mcmc_nngp_update_Gaussian <- function(locs, X, observed_field, space_time_model,
   acc_anc <- acc_suf <- matrix(0, n_iterations_update, C)
   IW <- vector("list", C)
   RB <- vector("list", C)  # host vectors the field records stream into while the chains run
+  # a binding ends before its vector can go: on any exit (an error, an
+  # interrupt) the chains of a caller's context are unbound (the shim also
+  # keeps each bound vector alive; an own context ends them by nngp_destroy)
+  if (!own_ctx) on.exit(for (i in seq_len(C)) if (!is.null(RB[[i]])) try({
+    nngp_set_chain(ctx, i - 1L)
+    nngp_records_stream(ctx, NULL)
+  }, silent = TRUE), add = TRUE)
   for (i in seq_len(C)) {  # :67-90
     nngp_set_chain(ctx, i - 1L)
     if (n_saved > 0) {

@@ -22,8 +22,15 @@
 #include <string.h>
 
 #include "nngp.h"
+#include "nngp_rows.h"
 
 static SEXP ctx_tag(void) { return Rf_install("nngp_ctx"); }
+
+/* The external pointer's protected slot: a list of kKeep + 1 entries, [k] =
+ * the numeric vector bound to chain k by C_nngp_records_stream (kept alive
+ * while the library may stream rows into it, whatever happens to the R
+ * variables that referenced it), [kKeep] = the selected chain (INTSXP). */
+#define kKeep 4
 
 static void ctx_finalizer(SEXP p) {
   nngp_ctx* c = (nngp_ctx*)R_ExternalPtrAddr(p);
@@ -34,10 +41,20 @@ static void ctx_finalizer(SEXP p) {
 }
 
 static SEXP wrap_ctx(nngp_ctx* c) {
-  SEXP p = PROTECT(R_MakeExternalPtr(c, ctx_tag(), R_NilValue));
+  SEXP keep = PROTECT(Rf_allocVector(VECSXP, kKeep + 1));
+  SET_VECTOR_ELT(keep, kKeep, Rf_ScalarInteger(0));  /* a new context selects chain 0 */
+  SEXP p = PROTECT(R_MakeExternalPtr(c, ctx_tag(), keep));
   R_RegisterCFinalizerEx(p, ctx_finalizer, TRUE);
-  UNPROTECT(1);
+  UNPROTECT(2);
   return p;
+}
+
+/* the bound records vector of the selected chain (R_NilValue: none) */
+static void keep_bound(SEXP p, SEXP buf) {
+  SEXP keep = R_ExternalPtrProtected(p);
+  if (TYPEOF(keep) != VECSXP) return;
+  const int k = INTEGER(VECTOR_ELT(keep, kKeep))[0];
+  if (k >= 0 && k < kKeep) SET_VECTOR_ELT(keep, k, buf);
 }
 
 static nngp_ctx* get_ctx(SEXP p) {
@@ -141,6 +158,8 @@ SEXP C_nngp_ctx_last_error(SEXP p) { return Rf_mkString(nngp_ctx_last_error(get_
 SEXP C_nngp_set_chain(SEXP p, SEXP chain) {
   nngp_ctx* c = get_ctx(p);
   check(nngp_set_chain(c, as_int(chain)), c);
+  SEXP keep = R_ExternalPtrProtected(p);
+  if (TYPEOF(keep) == VECSXP) INTEGER(VECTOR_ELT(keep, kKeep))[0] = as_int(chain);
   return R_NilValue;
 }
 
@@ -241,6 +260,7 @@ SEXP C_nngp_set_mu(SEXP p, SEXP mu, SEXP beta0) {
 SEXP C_nngp_records_reserve(SEXP p, SEXP n_rows) {
   nngp_ctx* c = get_ctx(p);
   check(nngp_records_reserve(c, as_int(n_rows)), c);
+  keep_bound(p, R_NilValue);  /* a reserve ends the binding */
   return R_NilValue;
 }
 
@@ -251,39 +271,49 @@ SEXP C_nngp_record_field(SEXP p, SEXP row) {
 }
 
 /* binds (or, for NULL, releases) a numeric vector of rows x n as the
- * selected chain's streamed records (row-major); the caller keeps the vector
- * referenced until the binding ends (R objects do not move) */
+ * selected chain's streamed records (row-major); the context keeps the vector
+ * alive until the binding ends (R objects do not move).  A failed call
+ * leaves the binding as it was (nngp.h), so does the kept reference. */
 SEXP C_nngp_records_stream(SEXP p, SEXP buf) {
   nngp_ctx* c = get_ctx(p);
   if (buf == R_NilValue) {
     check(nngp_records_stream(c, NULL, 0), c);
+    keep_bound(p, R_NilValue);
     return R_NilValue;
   }
   if (TYPEOF(buf) != REALSXP || XLENGTH(buf) % ctx_n(c) != 0) Rf_error("nngp: records buffer must be a numeric vector of rows x n");
   check(nngp_records_stream(c, REAL(buf), (int)(XLENGTH(buf) / ctx_n(c))), c);
+  keep_bound(p, buf);
   return R_NilValue;
 }
 
-/* rows [row0, row0 + n_rows) as an n_rows x n matrix (records$field layout);
- * buf: the vector bound by C_nngp_records_stream (the rows are already
- * there: the call only waits for them), or NULL */
+/* rows [row0, row0 + n_rows) as an n_rows x n matrix (records$field layout).
+ * buf: the vector bound by C_nngp_records_stream -- the rows are already
+ * there (the call waits for them and ends the binding) and are transposed
+ * straight out of it; NULL: the rows come from the device in blocks of
+ * kRowBlock into one small temporary, each block transposed in turn. */
+#define kRowBlock 16
 SEXP C_nngp_get_records(SEXP p, SEXP row0, SEXP n_rows, SEXP buf) {
   nngp_ctx* c = get_ctx(p);
-  const int n = ctx_n(c), r = as_int(n_rows);
-  SEXP tmp;
-  if (buf == R_NilValue) {
-    tmp = PROTECT(Rf_allocVector(REALSXP, (R_xlen_t)r * n));  /* row-major from the library */
-    check(nngp_get_records(c, as_int(row0), r, REAL(tmp)), c);
-  } else {
-    if (TYPEOF(buf) != REALSXP || XLENGTH(buf) < (R_xlen_t)(as_int(row0) + r) * n) Rf_error("nngp: records buffer too short");
-    tmp = PROTECT(Rf_allocVector(REALSXP, (R_xlen_t)r * n));
-    check(nngp_get_records(c, as_int(row0), r, REAL(buf) + (R_xlen_t)as_int(row0) * n), c);
-    memcpy(REAL(tmp), REAL(buf) + (R_xlen_t)as_int(row0) * n, sizeof(double) * (size_t)r * n);
-  }
+  const int n = ctx_n(c), r = as_int(n_rows), r0 = as_int(row0);
+  if (r < 0 || r0 < 0) Rf_error("nngp: negative record rows");
   SEXP out = PROTECT(Rf_allocMatrix(REALSXP, r, n));
-  for (int i = 0; i < r; ++i)
-    for (int j = 0; j < n; ++j) REAL(out)[i + (R_xlen_t)j * r] = REAL(tmp)[(R_xlen_t)i * n + j];
-  UNPROTECT(2);
+  if (buf != R_NilValue) {
+    if (TYPEOF(buf) != REALSXP || XLENGTH(buf) < (R_xlen_t)(r0 + r) * n) Rf_error("nngp: records buffer too short");
+    check(nngp_get_records(c, r0, r, REAL(buf) + (R_xlen_t)r0 * n), c);
+    keep_bound(p, R_NilValue);
+    nngp_rows_to_colmajor(REAL(buf) + (R_xlen_t)r0 * n, REAL(out), r, r, n);
+  } else {
+    const int blk = r < kRowBlock ? r : kRowBlock;
+    SEXP tmp = PROTECT(Rf_allocVector(REALSXP, (R_xlen_t)blk * n));
+    for (int i = 0; i < r; i += blk) {
+      const int k = r - i < blk ? r - i : blk;
+      check(nngp_get_records(c, r0 + i, k, REAL(tmp)), c);
+      nngp_rows_to_colmajor(REAL(tmp), REAL(out) + i, r, k, n);
+    }
+    UNPROTECT(1);
+  }
+  UNPROTECT(1);
   return out;
 }
 

@@ -42,6 +42,8 @@ void Rf_error(const char*, ...);
 SEXP R_MakeExternalPtr(void*, SEXP, SEXP);
 void* R_ExternalPtrAddr(SEXP);
 SEXP R_ExternalPtrTag(SEXP);
+SEXP R_ExternalPtrProtected(SEXP);
+void R_SetExternalPtrProtected(SEXP, SEXP);
 void R_ClearExternalPtr(SEXP);
 typedef void (*R_CFinalizer_t)(SEXP);
 void R_RegisterCFinalizerEx(SEXP, R_CFinalizer_t, Rboolean);

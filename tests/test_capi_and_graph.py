@@ -518,6 +518,41 @@ def test_r_shim_wraps_every_abi_entry_point():
         assert c in rfun, f"{c} has no R wrapper"
 
 
+def test_r_records_transpose_matches_row_major(tmp_path):
+    """rpkg/src/nngp_rows.h (C_nngp_get_records): k row-major record rows ->
+    the first k rows of R's column-major records$field matrix, in cache
+    blocks, straight out of the bound vector (no temporary) -- checked
+    against numpy for sizes around the 64 x 64 block edges."""
+    import subprocess
+
+    root = Path(__file__).resolve().parent.parent
+    src = tmp_path / "t.c"
+    src.write_text(r"""
+#include <stdio.h>
+#include <stdlib.h>
+#include "nngp_rows.h"
+int main(int argc, char** argv) {
+  const ptrdiff_t ld = atol(argv[1]), k = atol(argv[2]), n = atol(argv[3]);
+  double* s = malloc(sizeof(double) * (k * n + 1));
+  double* d = malloc(sizeof(double) * (ld * n + 1));
+  for (ptrdiff_t e = 0; e < k * n; ++e) s[e] = (double)e;
+  for (ptrdiff_t e = 0; e < ld * n; ++e) d[e] = -1.0;
+  nngp_rows_to_colmajor(s, d, ld, k, n);
+  fwrite(d, sizeof(double), ld * n, stdout);
+  return 0;
+}
+""")
+    exe = tmp_path / "t"
+    subprocess.run(["gcc", "-O2", "-std=c99", "-Wall", "-Werror", f"-I{root / 'rpkg' / 'src'}", str(src), "-o", str(exe)],
+                   check=True)
+    for ld, k, n in [(1, 1, 1), (3, 3, 7), (64, 64, 64), (65, 65, 129), (200, 130, 70), (40, 17, 1000)]:
+        out = subprocess.run([str(exe), str(ld), str(k), str(n)], capture_output=True, check=True).stdout
+        got = np.frombuffer(out, np.float64).reshape(n, ld).T  # column-major ld x n
+        rows = np.arange(k * n, dtype=np.float64).reshape(k, n)
+        np.testing.assert_array_equal(got[:k], rows)
+        assert np.all(got[k:] == -1.0)
+
+
 def test_chain_groups_split_where_tiles_exceed_the_lds(P, monkeypatch):
     """context.make_chain_views: a chain group whose context fell back to the
     colour engine for the LDS (engine_fallback 1) or keeps r in global memory

@@ -185,18 +185,51 @@ def test_records_streamed_into_host_arrays(P):
             for k in (0, 1):
                 ctx.select(k).set_field(fields[k][r])
                 ctx.record_field(r)
+        with pytest.raises(P.NNGPError):
+            ctx.select(0).records_stream(np.zeros((2, n)))  # not the reserved rows: the binding stays
+        assert ctx._rec_host[0] is hosts[0]
         for k in (0, 1):
             out = ctx.select(k).get_records(0, 3, out=hosts[k])
             assert out is hosts[k]
+            assert k not in ctx._rec_host  # get_records on the bound array ends the binding
             np.testing.assert_array_equal(hosts[k], np.stack(fields[k]))
             np.testing.assert_array_equal(ctx.get_records(0, 3), np.stack(fields[k]))  # device path
-        with pytest.raises(P.NNGPError):
-            ctx.select(0).records_stream(np.zeros((2, n)))  # not the reserved rows
-        ctx.select(0).records_reserve(3)  # ends the binding: later rows stay on the device
-        ctx.set_field(fields[1][0])
+        ctx.select(0).set_field(fields[1][0])  # after the binding: rows stay on the device
+        ctx.record_field(0)
+        np.testing.assert_array_equal(ctx.get_records(0, 1)[0], fields[1][0])
+        np.testing.assert_array_equal(hosts[0][0], fields[0][0])
+        ctx.records_stream(hosts[0])
+        ctx.records_reserve(3)  # a reserve ends the binding too
+        assert 0 not in ctx._rec_host
+        ctx.set_field(fields[1][1])
         ctx.record_field(0)
         ctx.get_records(1, 1)
         np.testing.assert_array_equal(hosts[0][0], fields[0][0])
+
+
+def test_records_bound_after_rows_were_recorded(P):
+    """Rows recorded before nngp_records_stream (and rows never recorded)
+    are not streamed: get_records on the bound array copies them from the
+    device, so the array holds exactly what the device path returns."""
+    n = 5000
+    rng = np.random.default_rng(5)
+    locs = rng.uniform(size=(n, 2))
+    NN = P.find_ordered_nn(locs, 4)
+    col = P.naive_greedy_coloring(NN)
+    with P.ChainContext(locs, NN, col, np.arange(1, n + 1, dtype=np.int32), rng.normal(size=n), device=0) as ctx:
+        f = [rng.normal(size=n) for _ in range(4)]
+        ctx.records_reserve(4)
+        ctx.set_field(f[0])
+        ctx.record_field(0)  # before the binding
+        host = np.full((4, n), np.nan)
+        ctx.records_stream(host)
+        for r in (1, 3):  # row 2 never recorded
+            ctx.set_field(f[r])
+            ctx.record_field(r)
+        ctx.get_records(0, 4, out=host)
+        dev = ctx.get_records(0, 4)
+        np.testing.assert_array_equal(host, dev)
+        np.testing.assert_array_equal(host[[0, 1, 3]], np.stack([f[0], f[1], f[3]]))
 
 
 def test_update_records_streamed_equal_end_of_call_copy(P, toy, monkeypatch):

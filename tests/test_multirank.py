@@ -237,3 +237,44 @@ def test_tile_shard_init_two_ranks(fail_rank):
         for r in range(world):
             st, msg, _ = out[r]
             assert st == "raised" and "rank 1" in msg and "hipIpcOpenMemHandle" in msg
+
+
+def _groups_worker(rank, world, port, q, diverge):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path.insert(0, str(ROOT))
+    import _pkgload
+
+    _pkgload.load()
+    import nngp_amd.shard as S
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    groups = [[0, 1], [2]] if (diverge and rank == 1) else [[0, 1, 2]]
+    try:
+        q.put((rank, "ok", S._same_everywhere(dist, groups, "the chain groups")))
+    except RuntimeError as e:
+        q.put((rank, "raised", str(e)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("diverge", [False, True])
+def test_chain_groups_agreed_across_ranks(diverge):
+    """bench.py's sharded path: the chain groups each rank chose
+    (context.split_groups, a rank-local decision) are compared over the
+    group; ranks that disagree all raise instead of waiting for shards that
+    never pair up."""
+    world, port = 2, 29700 + os.getpid() % 200 + (50 if diverge else 0)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_groups_worker, args=(r, world, port, q, diverge)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {r: rest for r, *rest in (q.get(timeout=100) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    if diverge:
+        assert all(o[0] == "raised" and "disagree" in o[1] for o in out.values())
+    else:
+        assert all(o == ["ok", [[0, 1, 2]]] for o in out.values())
