@@ -448,6 +448,7 @@ def main():
     ap.add_argument("--n-chromatic", type=int, default=10)
     ap.add_argument("--chains", type=int, default=3)
     ap.add_argument("--no-single-chain", action="store_true")
+    ap.add_argument("--no-rebuild-calls", action="store_true", help="skip the rebuild-every-call measurement")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -520,8 +521,11 @@ def main():
 
     def timed(ctx, steps, warmup, cold=False):
         """warmup + steps sweeps of every chain of ctx in calls of n_chromatic.
-        cold: beta_0 alternates by 1e-9 between calls, so every call rebuilds
-        w -> slots and r = B w (the MCMC call shape) instead of running warm."""
+        cold: beta_0 alternates by 1e-9 between calls (the MCMC call shape
+        when no covariance proposal was accepted: beta_0 is redrawn every
+        iteration, update_Gaussian.R:219-224), so every call starts from
+        w - d and r - d B 1 (capi.hip warm_kinds) -- or, on a context opened
+        with NNGP_SWEEP_WARM=0, rebuilds w -> slots and r = B w."""
         k = ctx.n_chains
         calls = [0]
 
@@ -571,7 +575,23 @@ def main():
     el_cold, ctr = timed(ctx, args.steps, args.warmup, cold=True)
     cold_calls = {"value": args.steps * C * world / el_cold, "unit": "sweeps/s",
                   "ms_per_step": el_cold * 1e3 / args.steps,
-                  "how": "beta_0 alternates by 1e-9 between calls: every call rebuilds w -> slots and r = B w"}
+                  "how": ("beta_0 alternates by 1e-9 between calls (an MCMC iteration's beta_0 Gibbs step): "
+                          "field and factor unchanged, so every call shifts w by -d and r by -d B 1 instead of "
+                          "rebuilding them (NNGP_SWEEP_SHIFT=0: rebuild)")}
+    if not args.no_rebuild_calls and info["sweep_engine"] == 1:
+        # the call after an accepted covariance proposal (new factor: r = B w
+        # rebuilt): the same calls on a context that rebuilds every call
+        os.environ["NNGP_SWEEP_WARM"] = "0"
+        try:
+            ctxr = open_context(P, wl, covfun, cp, local_rank, C, seed=7 + rank)
+        finally:
+            os.environ.pop("NNGP_SWEEP_WARM", None)
+        el_rb, _ = timed(ctxr, args.steps, args.warmup, cold=True)
+        ctxr.close()
+        cold_calls["rebuild_calls"] = {"value": args.steps * C * world / el_rb, "unit": "sweeps/s",
+                                       "ms_per_step": el_rb * 1e3 / args.steps,
+                                       "how": "every call rebuilds w -> slots and r = B w (NNGP_SWEEP_WARM=0 "
+                                              "context): the call after an accepted covariance proposal"}
 
     # per-kernel timing with HIP events on the context's own stream: the
     # sweep kernel's launches alone (tile engine: one persistent launch per
@@ -642,8 +662,9 @@ def main():
                                         if os.environ.get("NNGP_SWEEP_WARM", "1") != "0" and info["sweep_engine"] == 1
                                         else "cold: w -> slots and r = B w rebuilt every call"),
                       "value_is": ("warm-call throughput: consecutive n_chromatic-sweep calls with nothing "
-                                   "changed in between; an MCMC iteration redraws beta_0 and runs a cold "
-                                   "call (cold_calls)"
+                                   "changed in between; an MCMC iteration redraws beta_0 (cold_calls: w and r "
+                                   "shifted) and, after an accepted covariance proposal, rebuilds r = B w "
+                                   "(cold_calls.rebuild_calls)"
                                    if os.environ.get("NNGP_SWEEP_WARM", "1") != "0" and info["sweep_engine"] == 1
                                    else "cold-call throughput"),
                       "single_chain": single,

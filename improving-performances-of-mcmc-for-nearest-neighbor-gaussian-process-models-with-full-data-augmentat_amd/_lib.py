@@ -36,7 +36,7 @@ ABI_SYMBOLS = (
     "nngp_loglik", "nngp_sweep", "nngp_sweep_chains", "nngp_ancillary_propose", "nngp_ancillary_propose_chains",
     "nngp_field_response_ratio",
     "nngp_accept_field", "nngp_beta0_stats", "nngp_sum_squared_residuals", "nngp_spmv",
-    "nngp_tri_solve", "nngp_sweep_timed", "nngp_device_normals", "nngp_get_sweep_r",
+    "nngp_tri_solve", "nngp_tri_rescues", "nngp_sweep_timed", "nngp_device_normals", "nngp_get_sweep_r",
     "nngp_ctx_create_shard", "nngp_shard_unique_id", "nngp_shard_comm_init", "nngp_sweep_chains_group",
     "nngp_records_reserve", "nngp_record_field", "nngp_get_records", "nngp_records_stream",
     "nngp_shard_ipc_handle", "nngp_shard_ipc_open", "nngp_shard_sync",
@@ -114,6 +114,7 @@ def _load():
     L.nngp_sum_squared_residuals.argtypes = [_vp, C.c_double, C.POINTER(C.c_double)]
     L.nngp_spmv.argtypes = [_vp, C.c_int, _dp, C.c_int, _dp]
     L.nngp_tri_solve.argtypes = [_vp, C.c_int, _dp, _dp]
+    L.nngp_tri_rescues.argtypes = [_vp, C.POINTER(C.c_longlong)]
     _up = np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS")
     L.nngp_sweep_chains.argtypes = [_vp, C.c_int, _dp, _dp, _dp, _up, _up]
     L.nngp_ancillary_propose_chains.argtypes = [_vp, C.c_int, _dp, _dp]

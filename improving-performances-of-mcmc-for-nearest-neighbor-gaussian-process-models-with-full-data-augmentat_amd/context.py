@@ -307,6 +307,13 @@ class ChainContext:
         self._chk(lib.nngp_tri_solve(self._h, which, f64(u), out))
         return out
 
+    def tri_rescues(self) -> int:
+        """Sync-free solves of this context that finished in the rescue's
+        ticket order (their static order stalled on non-resident waves)."""
+        out = C.c_longlong()
+        self._chk(lib.nngp_tri_rescues(self._h, C.byref(out)))
+        return out.value
+
 
 class ChainView:
     """One chain of a ChainContext with the single-chain interface (every

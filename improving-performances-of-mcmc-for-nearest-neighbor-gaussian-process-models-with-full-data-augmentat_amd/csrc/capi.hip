@@ -62,6 +62,11 @@ struct ChainState {
   bool warm = false;
   uint64_t warm_fgen = 0, warm_lgen = 0;
   double warm_beta0 = 0.0;
+  // B 1 of the current factor (device rows; generation b1_lgen): a call whose
+  // field and factor are unchanged but beta_0 moved (the no-X beta_0 Gibbs
+  // step, update_Gaussian.R:219-224) stays warm -- w -= d, r -= d B 1
+  double* b1_d = nullptr;
+  uint64_t b1_lgen = 0;
   int rs_next = 0;
   // the sweep's copy of the current factor (tile cells / colour entries and
   // precision_diag) is behind it: refreshed before the next reader (a sweep,
@@ -141,7 +146,8 @@ struct nngp_ctx {
   std::vector<int> tri_seg;      // solve plan: (lv0, lv1, kind) triples, kind 1 = one-workgroup run
   bool tri_dag = false;          // NNGP_TRI=dag: one sync-free launch for the whole DAG
   bool tri_rescue = false;       // NNGP_TRI_RESCUE=1: its ticket order from the start (tests)
-  unsigned* tri_tmo_d = nullptr; // its control words: [0] timeout, [1] rescue, [2..3] rescue tickets
+  unsigned* tri_tmo_d = nullptr; // its control words: [0] timeout, [1] rescue, [2..3] rescue tickets, [4] rescues raised
+  int tri_oversub = 1;            // NNGP_TRI_OVERSUB=k: k x the resident grid (tests: the static order cannot finish)
   unsigned* tri_tmo_h = nullptr; // pinned copy, read at the next host sync
   int* obs_ptr_d = nullptr;
   int* obs_idx_d = nullptr;
@@ -197,6 +203,7 @@ struct nngp_ctx {
   std::string engine_note;        // why this sweep engine (nngp_ctx_engine_note)
   int tstagger = 0;               // chain-split: start offset per chain (NNGP_TILE_STAGGER, 100 MHz ticks)
   int tvariant = 0;               // NNGP_TILE_VARIANT (probe builds): experiment bits
+  int tpf = 0;                    // NNGP_TILE_PF: L2 prefetch bits (tiles.hip tile_prefetch_next)
   int tile_rows_needed = 0;       // largest local rows of a tile of the layout built here (nngp_info)
   int lds_max = 0;                // LDS bytes per CU of the device
   double* rg_d = nullptr;         // sum of the tiles' local rows x C
@@ -370,6 +377,7 @@ TileDev tile_dev(nngp_ctx* c) {
   D.dbg = c->tdbg_d;
   D.probe = c->tprobe;
   D.xw = c->txw;
+  D.pf = c->tpf;
   D.K = c->tl.K;
   D.C = c->C;
   D.T = c->tl.T;
@@ -599,7 +607,7 @@ void nngp_ctx_destroy(nngp_ctx* c) {
   ptrs.push_back(c->tdev_d);
   for (int k = 0; k < kMaxChains; ++k) {
     ChainState& s = c->ch[k];
-    ptrs.insert(ptrs.end(), {s.linv_d[0], s.linv_d[1], s.field_d, s.field_prop_d, s.mu_d, s.rec_d});
+    ptrs.insert(ptrs.end(), {s.linv_d[0], s.linv_d[1], s.field_d, s.field_prop_d, s.mu_d, s.rec_d, s.b1_d});
   }
   for (void* p : ptrs) if (p) hipFree(p);
   if (c->scal_h) hipHostFree(c->scal_h);
@@ -1100,6 +1108,7 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
         c->tprobe = std::atoi(pr) == 9 ? 1 : 2;
         c->tdbg_n = (size_t)TL.T * (c->tprobe == 1 ? 8 : 512 * 16);  // tiles.hip kTimelinePhases x kTimelineSlots
         if (const char* v = std::getenv("NNGP_TILE_VARIANT")) c->tvariant = std::atoi(v);
+        if (const char* v = std::getenv("NNGP_TILE_PF")) c->tpf = std::atoi(v);
         CK(dalloc(&c->tdbg_d, c->tdbg_n));
         CK(hipMemsetAsync(c->tdbg_d, 0, sizeof(unsigned long long) * c->tdbg_n, c->st));
       }
@@ -1122,8 +1131,10 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     c->tri_dag = !per_level && !(e && std::string(e) == "levels");
     const char* er = std::getenv("NNGP_TRI_RESCUE");
     c->tri_rescue = er && std::string(er) == "1";
-    CK(dalloc(&c->tri_tmo_d, 4));
-    CK(hipMemset(c->tri_tmo_d, 0, 4 * sizeof(unsigned)));
+    const char* eo = std::getenv("NNGP_TRI_OVERSUB");
+    c->tri_oversub = eo ? std::max(1, std::min(16, std::atoi(eo))) : 1;
+    CK(dalloc(&c->tri_tmo_d, 6));
+    CK(hipMemset(c->tri_tmo_d, 0, 6 * sizeof(unsigned)));
     CK(hipHostMalloc((void**)&c->tri_tmo_h, sizeof(unsigned), hipHostMallocDefault));
     *c->tri_tmo_h = 0;
     const int L = (int)c->level_ptr.size() - 1;
@@ -1974,15 +1985,67 @@ static int shard_ranks(const nngp_ctx* c) { return c->tG > 0 ? c->tG : c->sp.G; 
 static int shard_rank(const nngp_ctx* c) { return c->tG > 0 ? c->trank : c->sp.rank; }
 
 // the chains of mask can start from the slot-order w and r the last call
-// left (call BEFORE fields_written)
-static bool warm_call(const nngp_ctx* c, int mask, const double* beta0) {
-  if (!c->warm_on || c->engine != 1 || c->shard) return false;
+// left (call BEFORE fields_written): *cold = the chains that need the
+// prologue (field -> slots, r = B w), *shift = warm chains whose beta_0 moved
+// since (their field and factor unchanged): w -= d, r -= d B 1 instead.
+// NNGP_SWEEP_WARM=0 (warm_on false): every chain cold; NNGP_SWEEP_SHIFT=0:
+// a moved beta_0 makes the chain cold (the round-5 behaviour)
+static void warm_kinds(const nngp_ctx* c, int mask, const double* beta0, int* cold, int* shift) {
+  static const bool shift_on = [] {
+    const char* e = std::getenv("NNGP_SWEEP_SHIFT");
+    return !(e && std::string(e) == "0");
+  }();
+  *cold = 0;
+  *shift = 0;
+  const bool on = c->warm_on && c->engine == 1 && !c->shard;
   for (int k = 0; k < c->C; ++k) {
     if (!((mask >> k) & 1)) continue;
     const ChainState& S = c->ch[k];
-    if (!S.warm || S.fgen != S.warm_fgen || S.lgen[0] != S.warm_lgen || beta0[k] != S.warm_beta0) return false;
+    if (!on || !S.warm || S.fgen != S.warm_fgen || S.lgen[0] != S.warm_lgen) *cold |= 1 << k;
+    else if (beta0[k] != S.warm_beta0) *(shift_on ? shift : cold) |= 1 << k;
   }
-  return true;
+}
+
+// w -= d, r -= d B 1 for the chains of shift (B 1 computed once per factor
+// generation), stream-ordered before the call's colour launches
+static int enqueue_warm_shift(nngp_ctx* c, int shift, const double* beta0) {
+  WarmShift a;
+  std::memset(&a, 0, sizeof a);
+  a.mask = shift;
+  for (int k = 0; k < c->C; ++k) {
+    if (!((shift >> k) & 1)) continue;
+    ChainState& S = c->ch[k];
+    if (!S.b1_d) HIPCHK(c, dalloc(&S.b1_d, (size_t)c->n));
+    if (S.b1_lgen != S.lgen[0]) {
+      HIPCHK(c, launch_linv_rowsum(c->st, S.linv_d[0], c->n, c->b, S.b1_d));
+      S.b1_lgen = S.lgen[0];
+    }
+    a.b1[k] = S.b1_d;
+    a.d[k] = beta0[k] - S.warm_beta0;
+  }
+  HIPCHK(c, launch_warm_shift(c->st, c->n, c->C, a, c->w_slot_d, c->r_d));
+  return NNGP_OK;
+}
+
+// the call's launches: one captured graph of the whole call when every chain
+// is cold; else the prologue graph of the cold chains, the shift of the
+// shifted ones and the graph of the colours + epilogue
+static int enqueue_call(nngp_ctx* c, int n_sweeps, int mask, int cold, int shift, const double* beta0) {
+  hipGraphExec_t ex;
+  int rc;
+  if (cold == mask) {
+    if ((rc = graph_for(c, n_sweeps, mask, &ex, kAll))) return rc;
+    HIPCHK(c, hipGraphLaunch(ex, c->st));
+    return NNGP_OK;
+  }
+  if (cold) {
+    if ((rc = graph_for(c, n_sweeps, cold, &ex, kPrologue))) return rc;
+    HIPCHK(c, hipGraphLaunch(ex, c->st));
+  }
+  if (shift && (rc = enqueue_warm_shift(c, shift, beta0))) return rc;
+  if ((rc = graph_for(c, n_sweeps, mask, &ex, kColours | kEpilogue))) return rc;
+  HIPCHK(c, hipGraphLaunch(ex, c->st));
+  return NNGP_OK;
 }
 
 // after a completed tile call (AFTER fields_written): slot-order w and r
@@ -2019,7 +2082,8 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
   const int k = c->cur, mask = 1 << k;
   double b0v[kMaxChains] = {0, 0, 0, 0};
   b0v[k] = beta0;
-  const bool warm = !z && warm_call(c, mask, b0v);
+  int cold = mask, shift = 0;
+  if (!z) warm_kinds(c, mask, b0v, &cold, &shift);
   fields_written(c, mask);
   if ((rc = sweep_prepare(c, k, beta0, log_scale, lnv, seed, counter_base))) return rc;
   if ((rc = flush_sweep_values(c, mask))) return rc;
@@ -2053,11 +2117,9 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
     if ((rc = enqueue_sweep_body(c, n_sweeps, mask, c->z_d))) return rc;
     if (c->engine == 1 && (rc = tile_chain_record(c))) return rc;
   } else {
-    // replay a captured graph of the whole call (launch-bound at small n)
-    hipGraphExec_t ex;
-    if ((rc = graph_for(c, n_sweeps, mask, &ex, warm ? kColours | kEpilogue : kAll))) return rc;
+    // replay captured graphs of the call (launch-bound at small n)
     if (c->engine == 1 && (rc = tile_chain_wait(c))) return rc;
-    HIPCHK(c, hipGraphLaunch(ex, c->st));
+    if ((rc = enqueue_call(c, n_sweeps, mask, cold, shift, b0v))) return rc;
     if (c->inject_tmo > 0 && c->engine == 1) {
       --c->inject_tmo;
       HIPCHK(c, launch_tile_inject_timeout(c->st, c->ctl_d));
@@ -2082,7 +2144,8 @@ int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const doub
   int rc;
   if ((rc = set_device(c))) return rc;
   const int all = (1 << c->C) - 1;
-  const bool warm = warm_call(c, all, beta0);
+  int cold = all, shift = 0;
+  warm_kinds(c, all, beta0, &cold, &shift);
   fields_written(c, all);
   for (int k = 0; k < c->C; ++k)
     if ((rc = sweep_prepare(c, k, beta0[k], log_scale[k], lnv[k], seed[k], counter_base[k]))) return rc;
@@ -2094,10 +2157,8 @@ int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const doub
   std::unique_lock<std::mutex> tlk;
   if (c->engine == 1) tlk = std::unique_lock<std::mutex>(tile_lock(c->device));
   const bool async = sweep_async(c);
-  hipGraphExec_t ex;
-  if ((rc = graph_for(c, n_sweeps, all, &ex, warm ? kColours | kEpilogue : kAll))) return rc;
   if (c->engine == 1 && (rc = tile_chain_wait(c))) return rc;
-  HIPCHK(c, hipGraphLaunch(ex, c->st));
+  if ((rc = enqueue_call(c, n_sweeps, all, cold, shift, beta0))) return rc;
   if (c->inject_tmo > 0 && c->engine == 1) {
     --c->inject_tmo;
     HIPCHK(c, launch_tile_inject_timeout(c->st, c->ctl_d));
@@ -2717,7 +2778,7 @@ int nngp_get_sweep_r(nngp_ctx* c, double* r) {
 static int tri_solve_dev(nngp_ctx* c, const TriArgs& ta, const double* u, double* x) {
   if (c->tri_dag) {
     HIPCHK(c, launch_tri_dag(c->st, ta, c->level_rows_d, c->n, c->nn_d, c->b, u, x, (long long)c->n * ta.stride,
-                             c->tri_tmo_d, c->tri_rescue));
+                             c->tri_tmo_d, c->tri_rescue, c->tri_oversub));
     HIPCHK(c, hipMemcpyAsync(c->tri_tmo_h, c->tri_tmo_d, sizeof(unsigned), hipMemcpyDeviceToHost, c->st));
     return NNGP_OK;
   }
@@ -2741,6 +2802,19 @@ static int tri_timeout_check(nngp_ctx* c) {
     HIPCHK(c, hipMemsetAsync(c->tri_tmo_d, 0, sizeof(unsigned), c->st));
     return fail_msg(c, NNGP_ERR_HIP, "triangular solve: a dependency wait timed out (waves not co-resident?)");
   }
+  return NNGP_OK;
+}
+
+int nngp_tri_rescues(nngp_ctx* c, long long* out) {
+  if (!c || !out) return NNGP_ERR_ARG;
+  *out = 0;
+  if (!c->tri_tmo_d) return NNGP_OK;
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  unsigned w[6];
+  HIPCHK(c, hipMemcpyAsync(w, c->tri_tmo_d, sizeof w, hipMemcpyDeviceToHost, c->st));
+  { int ss_ = sync_stream(c); if (ss_) return ss_; }
+  *out = (long long)w[4] + (w[1] == 1u ? 1 : 0);
   return NNGP_OK;
 }
 

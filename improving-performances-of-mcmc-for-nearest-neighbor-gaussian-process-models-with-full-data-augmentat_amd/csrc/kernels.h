@@ -235,6 +235,7 @@ struct TileDev {
   int probe = 0;              // dbg layout: 1 = per-tile segment sums (T x 8), 2 = timeline (T x 512 phases x 8)
   int xw = 0;                 // exchange-wave tiles: the last wave polls the hand-offs, the
                               // layout's batches are cut for NT - 64 cell threads
+  int pf = 0;                 // NNGP_TILE_PF: L2 prefetch of the next phase's stream during the own work
 };
 
 struct TileLaunch {
@@ -331,8 +332,17 @@ hipError_t launch_tri_levels_block(hipStream_t st, const TriArgs& a, const int* 
 // clears it), [1] the rescue word, [2..3] the rescue ticket counter (both
 // reset by the launch; kernels.hip tri_dag_kernel); rescue: every wave takes
 // the ticket order from the start (tests)
+// warm sweep calls after a beta_0-only change (kernels.hip warm_shift_kernel)
+struct WarmShift {
+  const double* b1[kMaxChains];  // B 1 of each chain's current factor (device rows)
+  double d[kMaxChains];          // beta_0 new - beta_0 of the last call
+  int mask;
+};
+hipError_t launch_linv_rowsum(hipStream_t st, const double* linv, int n, int b, double* out);
+hipError_t launch_warm_shift(hipStream_t st, int n, int C, const WarmShift& a, double* w_slot, double* r);
 hipError_t launch_tri_dag(hipStream_t st, const TriArgs& a, const int* rows, int nrows, const int* nn, int b,
-                          const double* u, double* x, long long x_len, unsigned* ctl, bool rescue = false);
+                          const double* u, double* x, long long x_len, unsigned* ctl, bool rescue = false,
+                          int oversub = 1);
 // y[i] = shift + scale * x[i*xstride]
 // dst[i] = src[idx[i]] (gather) / dst[idx[i]] = src[i] (scatter), i < n:
 // R order <-> device row order of a field-sized vector

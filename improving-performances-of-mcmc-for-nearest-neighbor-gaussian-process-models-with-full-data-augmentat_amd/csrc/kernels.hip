@@ -600,6 +600,137 @@ __global__ __launch_bounds__(64) void factor_pair_kernel(double var, double nugg
   }
 }
 
+// Lane groups (north star's "one wavefront per location" at the DPP-row
+// grain, NNGP_FACTOR_LANES=16, b <= 16): the 16 lanes of a DPP row own one
+// location's local block, lane q its point q (locsub order, self last) and
+// column q of the block.  Each lane computes its whole covariance column from
+// the 16 points broadcast across the row (row_newbcast), so the block is
+// symmetric bitwise (the squared differences are the same both ways); the
+// Cholesky runs right-looking: at step k lane k's column is broadcast,
+// scaled by 1/sqrt of its diagonal into L[.][k], and every lane j > k updates
+// its column with L[t][k] L[j][k] -- the Schur complement stays in the
+// lanes' own registers (L[j][k] is lane j's own entry k by symmetry).  The
+// back substitution x = L^-T e_last is sequential in 16 broadcasts: x[r] is
+// final in lane r once every x[q > r] has been folded into its running sum.
+// Registers: the column (16 doubles), the point (DS), a few scalars -- many
+// waves per SIMD where the one-lane-per-row kernel has one.  Rows differ
+// from factor_kernel's in the last bits (another operation order), within
+// the factor tolerance of the parity tests.
+template <int K>
+__device__ __forceinline__ double row_bcast(double v) {  // lane K of each row of 16, to the whole row
+  return dpp_f64<0x150 + K, 0xF, false>(v);
+}
+
+template <int FAM, int DS>
+__global__ __launch_bounds__(256) void factor_lanes_kernel(FactorJobs J, const int* __restrict__ nn, int n, int b) {
+  constexpr int BM = 16;
+  __shared__ double tab[64];
+  if (threadIdx.x < 64) tab[threadIdx.x] = kExp2Tab[threadIdx.x];
+  __syncthreads();
+  const int q = threadIdx.x & 15;
+  const long long total = (long long)n * J.n_jobs;
+  const long long gstride = (long long)gridDim.x * (blockDim.x >> 4);
+  for (long long u = (long long)blockIdx.x * (blockDim.x >> 4) + (threadIdx.x >> 4); u < total; u += gstride) {
+    const int jb = (int)(u / n), i = (int)(u - (long long)jb * n);
+    const double* sc = job_pick(J.sc, jb);
+    // point q = NNarray column c = BM-1-q (column 0: the location itself)
+    const int c = BM - 1 - q;
+    const int nc = (c < b) ? __builtin_nontemporal_load(nn + (size_t)i * b + c) : -1;
+    // bs = 1 + the last valid column (max over the row's lanes)
+    int last = (c >= 1 && nc >= 0) ? c : 0;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) last = max(last, __shfl_xor(last, o, 16));
+    const int bs = last + 1;
+    const bool valid = c < bs;
+    double xq[DS];
+#pragma unroll
+    for (int k = 0; k < DS; ++k) {
+      const double v = sc[(size_t)(valid ? nc : i) * DS + k];
+      xq[k] = valid ? v : (k == 0 ? 1e30 * (q + 1) : 0.0);  // padding: far apart from all
+    }
+    // column q of the correlation block (the diagonal 1 + nugget; padded
+    // points: an identity row and column)
+    const double nug = job_pick(J.nugget, jb);
+    double a[BM];
+#pragma unroll
+    for (int t = 0; t < BM; ++t) {
+      double s2 = 0.0;
+#pragma unroll
+      for (int k = 0; k < DS; ++k) {
+        double xt = 0.0;
+        switch (t) {  // compile-time lane of the broadcast
+#define NNGP_BC(T) case T: xt = row_bcast<T>(xq[k]); break;
+          NNGP_BC(0) NNGP_BC(1) NNGP_BC(2) NNGP_BC(3) NNGP_BC(4) NNGP_BC(5) NNGP_BC(6) NNGP_BC(7)
+          NNGP_BC(8) NNGP_BC(9) NNGP_BC(10) NNGP_BC(11) NNGP_BC(12) NNGP_BC(13) NNGP_BC(14) NNGP_BC(15)
+#undef NNGP_BC
+        }
+        pin_full_exec(xt);
+        const double d = xt - xq[k];
+        s2 = __builtin_fma(d, d, s2);
+      }
+      const double dist = sqrt_pos(s2);
+      const double e = exp_nonpos(-dist, tab);
+      const double cr = FAM == 1 ? __builtin_fma(dist, e, e) : e;
+      a[t] = (t == q) ? (valid ? 1.0 + nug : 1.0) : cr;
+    }
+    // right-looking Cholesky, lane k's column broadcast at step k
+    bool bad = false;
+    double inv = 0.0;
+#pragma unroll
+    for (int k = 0; k < BM; ++k) {
+      double dk = 0.0;
+      switch (k) {
+#define NNGP_BC(T) case T: dk = row_bcast<T>(a[T]); break;
+        NNGP_BC(0) NNGP_BC(1) NNGP_BC(2) NNGP_BC(3) NNGP_BC(4) NNGP_BC(5) NNGP_BC(6) NNGP_BC(7)
+        NNGP_BC(8) NNGP_BC(9) NNGP_BC(10) NNGP_BC(11) NNGP_BC(12) NNGP_BC(13) NNGP_BC(14) NNGP_BC(15)
+#undef NNGP_BC
+      }
+      pin_full_exec(dk);
+      if (!(dk > 0.0)) { bad = true; dk = 1.0; }
+      const double rk = rsqrt_pos(dk);
+      const double ljk = a[k] * rk;  // L[q][k] (lanes q > k)
+#pragma unroll
+      for (int t = k + 1; t < BM; ++t) {
+        double vt = 0.0;
+        switch (k) {
+#define NNGP_BC(T) case T: vt = row_bcast<T>(a[t]); break;
+          NNGP_BC(0) NNGP_BC(1) NNGP_BC(2) NNGP_BC(3) NNGP_BC(4) NNGP_BC(5) NNGP_BC(6) NNGP_BC(7)
+          NNGP_BC(8) NNGP_BC(9) NNGP_BC(10) NNGP_BC(11) NNGP_BC(12) NNGP_BC(13) NNGP_BC(14) NNGP_BC(15)
+#undef NNGP_BC
+        }
+        pin_full_exec(vt);
+        const double ltk = vt * rk;  // L[t][k]
+        a[t] = q > k ? __builtin_fma(-ltk, ljk, a[t]) : (q == k ? ltk : a[t]);
+      }
+      if (q == k) {
+        a[k] = dk * rk;
+        inv = rk;
+      }
+    }
+    // x = L^-T e_last: lane r holds column r of L (a[t], t >= r); running
+    // sums s_r += L[q][r] x[q] as each x[q] is broadcast, q = BM-1 .. 0
+    double s = 0.0, xr = 0.0;
+#pragma unroll
+    for (int k = BM - 1; k >= 0; --k) {
+      const double mine = k == BM - 1 ? inv : -s * inv;  // x[k] in lane k
+      double xk = 0.0;
+      switch (k) {
+#define NNGP_BC(T) case T: xk = row_bcast<T>(mine); break;
+        NNGP_BC(0) NNGP_BC(1) NNGP_BC(2) NNGP_BC(3) NNGP_BC(4) NNGP_BC(5) NNGP_BC(6) NNGP_BC(7)
+        NNGP_BC(8) NNGP_BC(9) NNGP_BC(10) NNGP_BC(11) NNGP_BC(12) NNGP_BC(13) NNGP_BC(14) NNGP_BC(15)
+#undef NNGP_BC
+      }
+      pin_full_exec(xk);
+      if (q == k) xr = xk;
+      s = __builtin_fma(a[k], xk, s);  // lanes q < k: L[k][q] x[k]
+    }
+    // reduce the failure flag of the row (any lane's pivot) -- every lane
+    // saw the same broadcast pivots, so lane 15's flag is the row's
+    if (bad && q == BM - 1) atomicMin(job_pick(J.fail, jb), i + 1);
+    if (c < b) job_pick(J.linv, jb)[(size_t)i * b + c] = valid ? xr * rsqrt_pos(job_pick(J.var, jb)) : 0.0;
+  }
+}
+
 // Runtime-b variant (b <= 32, and the general Matern family whose Bessel
 // evaluation defeats full unrolling): same algorithm, private arrays indexed
 // at run time (held in scratch; correct for every b, slower than the
@@ -662,12 +793,12 @@ __global__ __launch_bounds__(64) void factor_kernel_rt(double var, double nugget
 // resident one-wave workgroups of the current device, at most the row
 // groups.  Twice resident measured best at n = 1e6 (0.350 vs 0.354 ms at 1x,
 // 0.373 at 4x): a shorter last round without giving up the pipeline.
-static int resident_grid(const void* kern, int groups) {
+static int resident_grid(const void* kern, int groups, int block = 64) {
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
                                               hipSuccess || cus <= 0)
     cus = 256;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, 0) != hipSuccess || per_cu <= 0) per_cu = 4;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, 0) != hipSuccess || per_cu <= 0) per_cu = 4;
   static const int mult = [] {
     const char* e = std::getenv("NNGP_FACTOR_GRID");
     int v = e ? std::atoi(e) : 2;
@@ -677,9 +808,49 @@ static int resident_grid(const void* kern, int groups) {
   return (int)(g < groups ? g : groups);
 }
 
+static bool factor_lanes_on() {  // read at every launch (tests switch it per context)
+  const char* e = std::getenv("NNGP_FACTOR_LANES");
+  return e && std::atoi(e) == 16;
+}
+
+static hipError_t launch_factor_lanes(hipStream_t st, int family, int ds, const FactorJobs& J, const int* nn, int n,
+                                      int b) {
+  auto go = [&](auto kern) {
+    const long long units = (long long)n * J.n_jobs;
+    const int g = resident_grid(reinterpret_cast<const void*>(kern), (int)std::min<long long>((units + 15) / 16, 1 << 30),
+                                256);
+    hipLaunchKernelGGL(kern, dim3(g), dim3(256), 0, st, J, nn, n, b);
+    return hipGetLastError();
+  };
+  if (family == 0) {
+    switch (ds) {
+      case 2: return go(factor_lanes_kernel<0, 2>);
+      case 3: return go(factor_lanes_kernel<0, 3>);
+      case 4: return go(factor_lanes_kernel<0, 4>);
+    }
+  } else {
+    switch (ds) {
+      case 2: return go(factor_lanes_kernel<1, 2>);
+      case 3: return go(factor_lanes_kernel<1, 3>);
+      case 4: return go(factor_lanes_kernel<1, 4>);
+    }
+  }
+  return hipErrorInvalidValue;
+}
+
 template <int BM, int FAM, int DS>
 static hipError_t launch_factor_one(hipStream_t st, double var, double nugget, double nu, double norm,
                                     const double* sc, const int* nn, int n, int b, double* linv, int* fail) {
+  if (BM <= 16 && factor_lanes_on()) {
+    FactorJobs J;
+    J.n_jobs = 1;
+    J.var[0] = var;
+    J.nugget[0] = nugget;
+    J.sc[0] = const_cast<double*>(sc);
+    J.linv[0] = linv;
+    J.fail[0] = fail;
+    return launch_factor_lanes(st, FAM, DS, J, nn, n, b);
+  }
   // NNGP_FACTOR_PAIR=1: the lane-pair kernel (opt-in: measured slower)
   if constexpr (BM == 16) {
     const char* pe = std::getenv("NNGP_FACTOR_PAIR");
@@ -784,6 +955,8 @@ hipError_t launch_factor_jobs(hipStream_t st, int family, double nu, const Facto
                      locs_rm, n, d, ds);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  // NNGP_FACTOR_LANES=16: the 16-lane-group kernel (b <= 16, opt-in)
+  if (factor_lanes_on() && b <= 16 && family != 2) return launch_factor_lanes(st, family, ds, J, nn, n, b);
   // one launch for the register-resident kernels; the others (general
   // Matern, b > 21, the lane-pair opt-in) run job after job as launch_factor
   const char* pe = std::getenv("NNGP_FACTOR_PAIR");
@@ -1872,12 +2045,15 @@ __global__ void fill_u64_kernel(long long n, unsigned long long v, unsigned long
     p[e] = v;
 }
 
-// x := the pending sentinel; the rescue word (:= rescue: every wave goes
-// straight to the ticket order -- NNGP_TRI_RESCUE=1, the tests' way to check
-// that order) and the ticket counter of the tri_dag launch that follows := 0
-// (the timeout word ctl[0] stays set until the host has read it)
+// x := the pending sentinel; the rescue word (:= 2 when forced: every wave
+// goes straight to the ticket order -- NNGP_TRI_RESCUE=1, the tests' way to
+// check that order; a wave that raises it stores 1) and the ticket counter of
+// the tri_dag launch that follows := 0 (the timeout word ctl[0] stays set
+// until the host has read it).  ctl[4] counts the solves whose rescue was
+// raised (not forced), the previous solve's added here (nngp_tri_rescues).
 __global__ void tri_dag_init_kernel(long long n, double* __restrict__ x, unsigned* __restrict__ ctl, unsigned rescue) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
+    ctl[4] += ctl[1] == 1u ? 1u : 0u;
     ctl[1] = rescue;
     *reinterpret_cast<unsigned long long*>(ctl + 2) = 0ull;
   }
@@ -1887,7 +2063,7 @@ __global__ void tri_dag_init_kernel(long long n, double* __restrict__ x, unsigne
 }
 
 hipError_t launch_tri_dag(hipStream_t st, const TriArgs& a, const int* rows, int nrows, const int* nn, int b,
-                          const double* u, double* x, long long x_len, unsigned* ctl, bool rescue) {
+                          const double* u, double* x, long long x_len, unsigned* ctl, bool rescue, int oversub) {
   const auto kern = b <= 16 ? tri_dag_kernel<16> : tri_dag_kernel<32>;
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
@@ -1897,11 +2073,52 @@ hipError_t launch_tri_dag(hipStream_t st, const TriArgs& a, const int* rows, int
   if (e != hipSuccess) return e;
   if (per_cu <= 0) return hipErrorInvalidConfiguration;
   const long long nitems = (long long)nrows * a.nc;
-  long long g = std::min<long long>((long long)cus * per_cu, (nitems + 15) / 16);
+  // oversub > 1 (tests, NNGP_TRI_OVERSUB): a grid of oversub x the resident
+  // workgroups, so that the static order waits on waves that are not
+  // resident and only the rescue completes the solve
+  long long g = std::min<long long>((long long)cus * per_cu * (oversub > 1 ? oversub : 1), (nitems + 15) / 16);
   if (g < 1) g = 1;
   const int gf = (int)std::min<long long>((x_len + 255) / 256, 4096);
-  hipLaunchKernelGGL(tri_dag_init_kernel, dim3(gf > 0 ? gf : 1), dim3(256), 0, st, x_len, x, ctl, rescue ? 1u : 0u);
+  hipLaunchKernelGGL(tri_dag_init_kernel, dim3(gf > 0 ? gf : 1), dim3(256), 0, st, x_len, x, ctl, rescue ? 2u : 0u);
   hipLaunchKernelGGL(kern, dim3((int)g), dim3(256), 0, st, a, rows, nitems, nn, b, u, x, ctl);
+  return hipGetLastError();
+}
+
+// B 1 (row sums of the factor, device row order): a warm sweep call after a
+// beta_0-only change (update_Gaussian.R:219-224) shifts r = B w by
+// -dbeta0 B 1 instead of recomputing it (capi.hip warm_kinds)
+__global__ void linv_rowsum_kernel(const double* __restrict__ linv, int n, int b, double* __restrict__ out) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    double s = 0.0;
+    for (int j = 0; j < b; ++j) s += linv[(size_t)i * b + j];
+    out[i] = s;
+  }
+}
+
+hipError_t launch_linv_rowsum(hipStream_t st, const double* linv, int n, int b, double* out) {
+  const int g = std::min((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(linv_rowsum_kernel, dim3(g > 0 ? g : 1), dim3(256), 0, st, linv, n, b, out);
+  return hipGetLastError();
+}
+
+// the chains of a.mask: w (slot order) -= d_k, r (row order) -= d_k (B 1)_k
+// -- w = field - beta_0 and r = B w after beta_0 moved by d_k with the field
+// and the factor unchanged
+__global__ void warm_shift_kernel(int n, int C, WarmShift a, double* __restrict__ w_slot, double* __restrict__ r) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+#pragma unroll
+    for (int k = 0; k < kMaxChains; ++k) {
+      if (k < C && ((a.mask >> k) & 1)) {
+        w_slot[(size_t)i * C + k] -= a.d[k];
+        r[(size_t)i * C + k] -= a.d[k] * a.b1[k][i];
+      }
+    }
+  }
+}
+
+hipError_t launch_warm_shift(hipStream_t st, int n, int C, const WarmShift& a, double* w_slot, double* r) {
+  const int g = std::min((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(warm_shift_kernel, dim3(g > 0 ? g : 1), dim3(256), 0, st, n, C, a, w_slot, r);
   return hipGetLastError();
 }
 

@@ -319,6 +319,7 @@ struct TileState {
   bool timed_out;
   int T, t, lane, wv, K, nph, ph;
   unsigned long long tp[8], t_prev;
+  uint32_t pf_lds;                  // LDS byte address of the prefetch landing area (kTilePfLds)
 };
 
 template <int C, int GMAX>
@@ -926,6 +927,41 @@ __device__ __forceinline__ void tile_own_wl(const TileDev& D, const TileLaunch& 
     D.dbg[((size_t)S.T * kTimelinePhases + S.ph) * kTimelineSlots + 9 + S.wv] = __builtin_amdgcn_s_memrealtime();
 }
 
+// L2 prefetch without registers: one LDS-DMA dword load per lane, each
+// lane's address in a different 128-B line, landing in the tile's dummy LDS
+// area (kTilePfLds, never read).  Inline asm, so the compiler's s_waitcnt
+// bookkeeping does not see it: no wait is inserted for it, and a later wait
+// for an ordinary load (vmcnt counts in issue order) covers it conservatively.
+__device__ __forceinline__ void l2_touch(const void* p, uint32_t lds_dummy) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(p), "s"(__builtin_amdgcn_readfirstlane(lds_dummy)) : "memory");
+}
+
+// the next batch's cells of this cell wave into L2 while the own work runs
+// (NNGP_TILE_PF): its cell_pk run (R x 256 B) and, per chain, its cell_val
+// run (R x 512 B), one touch per 128 B -- lanes 16q..16q+15 take run q
+// (0: cell_pk, 1..3: chain q-1), two instructions cover R <= 8.  The bases
+// are wave-uniform (scalar registers): a few transient VGPRs per touch.
+template <int C>
+__device__ __forceinline__ void tile_prefetch_next(const TileDev& D, const TileState& S, int bnext, bool more,
+                                                   uint32_t lds_dummy) {
+  if (!more) return;
+  const int lane = S.lane;
+  const int bx = __builtin_amdgcn_readfirstlane(S.batch_s[bnext].x);
+  const int R = __builtin_amdgcn_readfirstlane(S.batch_s[bnext].y) & 0xFFFF;
+  const char* pk = reinterpret_cast<const char*>(D.cell_pk + bx);
+  const char* v0 = reinterpret_cast<const char*>(D.cell_val + bx);
+  const int q = lane >> 4;
+  const int lines = q == 0 ? 2 * R : 4 * R;
+  const char* base = (q == 0 || q > C) ? pk : v0 + (long long)(q - 1) * D.n_cells * 8;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int li = (lane & 15) + 16 * k;
+    l2_touch(base + (li < lines ? li : 0) * 128, lds_dummy);
+  }
+}
+
 // the cell waves' colour phase on wave-local batches.  DB (<= 2 chains, two
 // register sets): the wave's next batch loads at the phase start, its HBM
 // stream overlapping this colour's work; otherwise its records after the
@@ -961,6 +997,10 @@ __device__ __forceinline__ void tile_phase_wl(const TileDev& D, const TileLaunch
     if (bi + W >= bend) {  // this wave's last batch of the colour: its records are dead
       if (!DB && more) tile_load_items<C, 64, RMAX, SH>(D, S.batch_s[bnext], nxt, lane);
       if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
+      // NNGP_TILE_PF: the next batch's cells into L2 now, behind the records
+      // and ghosts (their waits do not cover it), ahead of the scatter and
+      // the draw preparation
+      if (!DB && D.pf) tile_prefetch_next<C>(D, S, bnext, more, S.pf_lds);
     }
     tile_own_scatter<C, 64, RMAX, PROBE>(S, cur, R, acc_w);
   }
@@ -1332,6 +1372,7 @@ __device__ __forceinline__ void sweep_tiles_body(const TileDev& D0, TileLaunch a
   if (PROBE == 2 && t == 0) *S.spin_s = 0;
   S.pub_s = reinterpret_cast<int*>(S.spin_s + 1);        // (tile_lds_bytes' 64-byte tail)
   if (t == 0) *S.pub_s = -1;
+  S.pf_lds = (uint32_t)reinterpret_cast<uintptr_t>(reinterpret_cast<char*>(S.spin_s) + 64);  // kTilePfLds past the tail
   TSTAMP(S, -1);
   for (int lr = t; lr < nrows; lr += NT) {
     const size_t g = (size_t)D.erow[row0 + lr] * CS;

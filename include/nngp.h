@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define NNGP_ABI_VERSION 13  /* 13: nngp_records_stream; 12: nngp_info gained tile_rows_needed, device_lds */
+#define NNGP_ABI_VERSION 14  /* 14: nngp_tri_rescues; 13: nngp_records_stream; 12: nngp_info gained tile_rows_needed, device_lds */
 #define NNGP_SHARD_ID_BYTES 128 /* RCCL unique id */
 #define NNGP_IPC_HANDLE_BYTES 192 /* HIP IPC handles of a tile shard's granule buffer, w replica, flags */
 
@@ -270,6 +270,12 @@ int nngp_sufficient_step_chains(nngp_ctx* ctx, int chain_mask, int covfun, const
 int nngp_spmv(nngp_ctx* ctx, int which, const double* X, int ncols, double* Y);
 /* x = B^{-1} u (host buffers, length n) */
 int nngp_tri_solve(nngp_ctx* ctx, int which, const double* u, double* x);
+/* Diagnostics of the sync-free solve (update_Gaussian.R:127): the solves of
+ * this context so far whose static order stalled (a wave waited 20 ms on one
+ * group, e.g. its inputs' waves were not resident) and finished in the
+ * ticket order of the rescue; forced ticket orders (NNGP_TRI_RESCUE=1) do not
+ * count.  Waits for the context's stream. */
+int nngp_tri_rescues(nngp_ctx* ctx, long long* out);
 
 /* ---------- colour-sharded sweep (multi-GPU) ----------
  * The chromatic sweep of ONE set of chains split over n_ranks contexts (one

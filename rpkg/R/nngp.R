@@ -92,6 +92,8 @@ nngp_beta0_stats <- function(ctx) .Call(C_nngp_beta0_stats, ctx)
 nngp_sum_squared_residuals <- function(ctx, beta_0) .Call(C_nngp_sum_squared_residuals, ctx, as.double(beta_0))
 nngp_spmv <- function(ctx, which, X) .Call(C_nngp_spmv, ctx, as.integer(which), X + 0)
 nngp_tri_solve <- function(ctx, which, u) .Call(C_nngp_tri_solve, ctx, as.integer(which), as.double(u))
+# solves that finished in the rescue's ticket order (diagnostic)
+nngp_tri_rescues <- function(ctx) .Call(C_nngp_tri_rescues, ctx)
 nngp_device_normals <- function(device, seed, sweep, n)
   .Call(C_nngp_device_normals, as.integer(device), as.double(seed), as.double(sweep), as.integer(n))
 # r = B (field - beta0) of the selected chain as the last sweep call left it (warm-call state)

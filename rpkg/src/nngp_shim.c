@@ -427,6 +427,13 @@ SEXP C_nngp_tri_solve(SEXP p, SEXP which, SEXP u) {
   return x;
 }
 
+SEXP C_nngp_tri_rescues(SEXP p) {
+  nngp_ctx* c = get_ctx(p);
+  long long k = 0;
+  check(nngp_tri_rescues(c, &k), c);
+  return Rf_ScalarReal((double)k);
+}
+
 SEXP C_nngp_device_normals(SEXP device, SEXP seed, SEXP sweep, SEXP n) {
   SEXP z = PROTECT(Rf_allocVector(REALSXP, as_int(n)));
   check(nngp_device_normals(as_int(device), (uint64_t)as_real(seed), (uint64_t)as_real(sweep), as_int(n), REAL(z)),
@@ -696,6 +703,7 @@ static const R_CallMethodDef call_methods[] = {
     E(C_nngp_sum_squared_residuals, 2),
     E(C_nngp_spmv, 3),
     E(C_nngp_tri_solve, 3),
+    E(C_nngp_tri_rescues, 1),
     E(C_nngp_device_normals, 4),
     E(C_nngp_get_sweep_r, 1),
     E(C_nngp_shard_unique_id, 0),

@@ -20,7 +20,7 @@ def test_header_symbols_exported(P):
     lib = C.CDLL(str(_lib.LIB_PATH))
     for s in sorted(declared):
         assert hasattr(lib, s), s
-    assert P.lib.nngp_abi_version() == 13
+    assert P.lib.nngp_abi_version() == 14
 
 
 def test_library_has_gfx950_code_object():

@@ -74,6 +74,39 @@ def test_factor_lane_pairs_match_oracle(P, O, covfun, m, monkeypatch):
     assert np.all(got[NN == O.NA] == 0.0)
 
 
+@pytest.mark.parametrize("m", [1, 5, 10, 15])
+@pytest.mark.parametrize("covfun", [c for c in COVS if c != "matern_isotropic"])
+def test_factor_lane_groups_match_oracle(P, O, m, covfun, monkeypatch):
+    """The opt-in 16-lane-group factor kernel (NNGP_FACTOR_LANES=16: one DPP
+    row of 16 lanes per Vecchia row, lane q owning point q and column q of the
+    local block, right-looking Cholesky by row broadcasts; kernels.hip
+    factor_lanes_kernel; b <= 16, so m <= 15) against the oracle's
+    GpGp::vecchia_Linv restatement at test_factor_matches_oracle's tolerance,
+    every covariance family it serves (the general Matern keeps the
+    run-time-b kernel); and the multi-chain launch (three jobs with different
+    parameters in one launch) row for row against one job at a time."""
+    monkeypatch.setenv("NNGP_FACTOR_LANES", "16")
+    locs, NN, col, lm, y = make_problem(P, 700, m, seed=m)
+    cp = COVS[covfun]
+    with _ctx(P, locs, NN, col, lm, y) as ctx:
+        ctx.factor(0, covfun, cp)
+        got = ctx.get_linv(0)
+        ref = O.vecchia_linv(covfun, cp, locs, NN)
+        np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-10)
+        assert np.all(got[NN == O.NA] == 0.0)
+        np.testing.assert_allclose(ctx.precision_diag(), O.precision_diag(ref, NN), rtol=1e-10)
+    if covfun == "matern15_isotropic":
+        cps = [[1.0 + 0.2 * k] + list(cp[1:]) for k in range(3)]
+        cps[2][1] *= 1.3
+        with P.ChainContext(locs, NN, col, lm, y, device=0, n_chains=3) as ctx:
+            st = ctx.factor_chains(0, 7, covfun, cps)
+            assert (st == 0).all()
+            jobs = [ctx.select(k).get_linv(0) for k in range(3)]
+            for k in range(3):
+                ctx.select(k).factor(0, covfun, cps[k])
+                np.testing.assert_array_equal(ctx.get_linv(0), jobs[k])
+
+
 @pytest.mark.parametrize("covfun", ["exponential_isotropic", "matern15_isotropic"])
 def test_factor_with_coinciding_points_matches_oracle(P, O, covfun):
     """Two locations at distance 0 (correlation 1) with a nugget: a positive

@@ -6,7 +6,9 @@ MI355X).
    residency or dispatch order: its ticket ("rescue") order is checked
    bitwise against the static order and the oracle, and a solve issued from
    a second host thread while another context's persistent tile sweep holds
-   every CU finishes without a timeout and matches the oracle's tri_solve.
+   every CU finishes without a timeout and matches the oracle's tri_solve;
+   with a grid twice the resident waves the rescue is proven to have run
+   (nngp_tri_rescues).
 2. A tile timeout is reported by the next host sync however many sweep calls
    were enqueued after it (the sticky timeout word, tiles.hip
    tile_call_bump_kernel): injected after the first of two async calls.
@@ -50,16 +52,24 @@ def test_tri_solve_ticket_order_equals_static_order(P, O, n, m, C, monkeypatch):
         np.testing.assert_allclose(res["1"][0][k], O.tri_solve(Ls[k], NN, us[0]), rtol=1e-9, atol=1e-10)
 
 
-def test_tri_solve_beside_a_persistent_tile_sweep(P, O, monkeypatch):
+@pytest.mark.parametrize("oversub", [1, 2])
+def test_tri_solve_beside_a_persistent_tile_sweep(P, O, monkeypatch, oversub):
     """Thread A sweeps a 3-chain tile context (256 persistent workgroups, one
     per CU: while a launch runs no other wave fits the CUs it holds); thread B
     meanwhile runs sync-free solves on a second context.  Both finish without
     a timeout, every solve equals the oracle's, and the sweep's fields equal
-    the same calls run alone, bitwise."""
+    the same calls run alone, bitwise.  oversub = 2 (NNGP_TRI_OVERSUB): the
+    solves' grids are twice what the device holds at once, so their static
+    order waits on waves that are not resident (each wave's later groups
+    depend on the first groups of waves past the resident set) and only the
+    rescue's ticket order can finish them -- asserted through the context's
+    rescue count, which proves the rescue path ran, not just that the solve
+    happened to get its CUs."""
     monkeypatch.delenv("NNGP_ENGINE", raising=False)
     monkeypatch.delenv("NNGP_TILES", raising=False)
     monkeypatch.delenv("NNGP_TRI_RESCUE", raising=False)
     monkeypatch.delenv("NNGP_TRI", raising=False)
+    monkeypatch.setenv("NNGP_TRI_OVERSUB", str(oversub))
     n, m, C = 400_000, 10, 3
     locs, NN, col, lm, y = make_problem(P, n, m, seed=91)
     fields = [np.random.default_rng(92 + k).normal(size=n) for k in range(C)]
@@ -90,6 +100,7 @@ def test_tri_solve_beside_a_persistent_tile_sweep(P, O, monkeypatch):
     def solves(ctx, out):
         try:
             out["x"] = [ctx.tri_solve(0, u) for u in us]
+            out["rescues"] = ctx.tri_rescues()
         except Exception as e:  # noqa: BLE001
             out["err"] = e
 
@@ -115,6 +126,9 @@ def test_tri_solve_beside_a_persistent_tile_sweep(P, O, monkeypatch):
         so.close()
     for u, x in zip(us, b["x"]):
         np.testing.assert_allclose(x, O.tri_solve(L2, p2[1], u), rtol=1e-9, atol=1e-10)
+    print(f"oversub {oversub}: {b['rescues']} of {len(us)} solves finished in the rescue's ticket order")
+    if oversub > 1:
+        assert b["rescues"] >= 1, "no solve ran the rescue: the static order finished on its own"
     alone = {}
     sw = open_sweeper()
     try:

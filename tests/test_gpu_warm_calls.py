@@ -11,7 +11,10 @@ NNGP_SWEEP_WARM=0.
 
 Tolerances: warm vs cold field max|a - b| <= 1e-10 max|b| per chain (the
 warm call differs only in the rounding of the carried-over w and r); r drift
-max|r - B (field - beta0)| <= 1e-11 max|B (field - beta0)|.
+max|r - B (field - beta0)| <= 1e-11 max|B (field - beta0)|.  A call whose
+field and factor are unchanged but whose beta_0 moved (the MCMC's beta_0
+Gibbs step) stays warm: w -= d, r -= d B 1 (capi.hip warm_kinds); pinned the
+same way, per call and for the drift over 100 shifted calls.
 
 Last: two contexts swept concurrently from two host threads on one device,
 whose tile grids together exceed the CUs -- the per-device tile lock
@@ -109,6 +112,71 @@ def test_warm_call_r_drift_bounded(P, monkeypatch, C):
             ctx.select(k)
             r = ctx.get_sweep_r()
             fresh = ctx.spmv(0, ctx.get_field() - b0s[k])
+            e = _rel(r, fresh)
+            assert e <= 1e-11, (k, e)
+    finally:
+        ctx.close()
+
+
+def test_beta0_shifted_warm_calls_equal_cold_calls_headline(P, monkeypatch):
+    """The MCMC call shape without an accepted covariance proposal: beta_0
+    redrawn between calls (the no-X beta_0 Gibbs step, update_Gaussian.R:
+    219-224), field and factor unchanged -- the warm context shifts w by -d and
+    r by -d B 1 (capi.hip warm_kinds / enqueue_warm_shift) instead of
+    rebuilding them.  n = 1e6, m = 15, 3 chains, four 10-sweep calls with
+    every chain's beta_0 moving by a different amount, and a fifth where
+    chain 1's factor changed (cold) while chains 0 and 2 shift: every call
+    against the cold context, <= 1e-10 max|field|."""
+    n, m, C = 1_000_000, 15, 3
+    prob = make_problem(P, n, m, seed=17)
+    cps = [[1.0, 0.05, 0.0], [1.2, 0.04, 0.0], [0.8, 0.06, 0.0]]
+    rng = np.random.default_rng(15)
+    fields = [rng.normal(size=n) for _ in range(C)]
+    b0s, lss, lnvs, seeds = [0.0, 0.1, 0.2], [0.0, 0.2, -0.1], [-0.5, -0.4, -0.6], [11, 12, 13]
+    shifts = [[0.0, 0.0, 0.0], [0.31, -0.07, 1e-9], [-0.5, 0.02, 0.0], [0.013, 0.4, -0.25], [0.1, 0.0, -0.1]]
+    res = {}
+    for warm in (True, False):
+        ctx = _open(P, monkeypatch, prob, C, warm, cps, fields, b0s)
+        b0 = list(b0s)
+        try:
+            res[warm] = []
+            for call, d in enumerate(shifts):
+                b0 = [a + x for a, x in zip(b0, d)]
+                if call == 4:  # chain 1: a new current factor -> cold, the others shift
+                    ctx.select(1).factor(0, COV, [1.1, 0.045, 0.0])
+                ctx.sweep_chains(10, b0, lss, lnvs, seeds, [10 * call] * C)
+                res[warm].append(_fields(ctx, C))
+        finally:
+            ctx.close()
+    for call in range(len(shifts)):
+        for k in range(C):
+            e = _rel(res[True][call][k], res[False][call][k])
+            assert e <= 1e-10, (call, k, e)
+
+
+@pytest.mark.parametrize("C", [1, 3])
+def test_beta0_shifted_calls_r_drift_bounded(P, monkeypatch, C):
+    """100 one-sweep calls, beta_0 moving before every one (shifted warm
+    calls: r -= d B 1 on top of the kernel's incremental r): the r the last
+    call left against a fresh r = B (field - beta_0), as the warm-call drift
+    bound."""
+    n, m = 1_000_000, 15
+    prob = make_problem(P, n, m, seed=19)
+    cps = [[1.0, 0.05, 0.0], [1.1, 0.045, 0.0], [0.9, 0.055, 0.0]][:C]
+    rng = np.random.default_rng(16)
+    fields = [rng.normal(size=n) for _ in range(C)]
+    b0s, lss, lnvs, seeds = [0.3, -0.1, 0.0][:C], [0.0, 0.1, -0.2][:C], [-0.5, -0.3, -0.7][:C], [21, 22, 23][:C]
+    ctx = _open(P, monkeypatch, prob, C, True, cps, fields, b0s)
+    b0 = list(b0s)
+    try:
+        for call in range(101):
+            if call:
+                b0 = [a + x for a, x in zip(b0, rng.normal(scale=0.05, size=C))]
+            ctx.sweep_chains(1, b0, lss, lnvs, seeds, [call] * C)
+        for k in range(C):
+            ctx.select(k)
+            r = ctx.get_sweep_r()
+            fresh = ctx.spmv(0, ctx.get_field() - b0[k])
             e = _rel(r, fresh)
             assert e <= 1e-11, (k, e)
     finally:
