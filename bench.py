@@ -205,18 +205,24 @@ def mcmc_iterations(P, wl, covfun, cp, ctx, iters, warmup, sync):
 
 def pmc_traffic(chains, n, m, kernel):
     """Per-launch HBM bytes of the sweep kernel from the committed rocprofv3
-    PMC summary of the same workload (profiles/, scripts/pmc.sh: FETCH_SIZE and
-    WRITE_SIZE passes, calibrated on known-byte kernels)."""
-    best = None
+    PMC summary of the same workload (profiles/): the request-size-resolved
+    passes (scripts/pmc_sizes.sh: TCC_EA0_RDREQ_{128B,64B,32B}, WRREQ) where
+    a round has them, else FETCH_SIZE and WRITE_SIZE calibrated on known-byte
+    kernels (scripts/pmc.sh) -- the latest round's, sized first."""
+    best, best_key = None, None
     for f in sorted((ROOT / "profiles").glob("r*_pmc_*.json")):
         try:
             d = json.loads(f.read_text())
         except Exception:
             continue
         w = d.get("workload", {})
+        if not isinstance(w, dict):
+            continue
         if (w.get("chains") == chains and w.get("n") == n and w.get("m") == m and kernel.startswith(d.get("kernel", "?"))
                 and d.get("traffic_bytes_per_launch")):
-            best = (d["traffic_bytes_per_launch"], f.name)
+            key = (f.name[:3], "RDREQ" in d.get("method", ""), f.name)
+            if best_key is None or key > best_key:
+                best, best_key = (d["traffic_bytes_per_launch"], f.name), key
     return best
 
 

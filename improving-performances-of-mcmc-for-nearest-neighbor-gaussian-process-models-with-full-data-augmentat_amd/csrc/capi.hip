@@ -118,6 +118,7 @@ struct nngp_ctx {
   int* nn_d = nullptr;       // n x b row-major, 0-based, -1 = NA
   const double** linv_cur_d = nullptr;  // C pointers: current factor of each chain
   const double** linv_cur_h = nullptr;  // pinned mirror
+  const double** b1_tab_d = nullptr;    // C pointers: each chain's B 1 buffer (ChainState::b1_d; TileDev::b1)
   int* fail_d = nullptr;         // inside res_d (kResFailOff)
   int2* sinfo_d = nullptr;       // n compact: {obs_per_loc, f0 | collen << 16}
   int* compact_loc_d = nullptr;  // n
@@ -150,6 +151,7 @@ struct nngp_ctx {
   int tri_oversub = 1;            // NNGP_TRI_OVERSUB=k: k x the resident grid (tests: the static order cannot finish)
   unsigned* tri_tmo_h = nullptr; // pinned copy, read at the next host sync
   int* obs_ptr_d = nullptr;
+  double* ysum_d = nullptr;       // per slot (compact order): the sum of its observations' y (residual sums, mu = beta_0)
   int* obs_idx_d = nullptr;
   int* lm_d = nullptr;  // locs_match, 0-based
   double* y_d = nullptr;
@@ -203,7 +205,6 @@ struct nngp_ctx {
   std::string engine_note;        // why this sweep engine (nngp_ctx_engine_note)
   int tstagger = 0;               // chain-split: start offset per chain (NNGP_TILE_STAGGER, 100 MHz ticks)
   int tvariant = 0;               // NNGP_TILE_VARIANT (probe builds): experiment bits
-  int tpf = 0;                    // NNGP_TILE_PF: L2 prefetch bits (tiles.hip tile_prefetch_next)
   int tile_rows_needed = 0;       // largest local rows of a tile of the layout built here (nngp_info)
   int lds_max = 0;                // LDS bytes per CU of the device
   double* rg_d = nullptr;         // sum of the tiles' local rows x C
@@ -377,7 +378,7 @@ TileDev tile_dev(nngp_ctx* c) {
   D.dbg = c->tdbg_d;
   D.probe = c->tprobe;
   D.xw = c->txw;
-  D.pf = c->tpf;
+  D.b1 = c->b1_tab_d;
   D.K = c->tl.K;
   D.C = c->C;
   D.T = c->tl.T;
@@ -432,7 +433,8 @@ int flush_sweep_values(nngp_ctx* c, int mask) {
     ++J.M;
   }
   if (J.M) {
-    HIPCHK(c, launch_residual_sums_jobs(c->st, c->n, sweep_dev(c), J, c->obs_ptr_d, c->obs_idx_d, c->y_d));
+    HIPCHK(c, launch_residual_sums_jobs(c->st, c->n, sweep_dev(c), J, c->obs_ptr_d, c->obs_idx_d, c->y_d, c->ysum_d,
+                                        c->sinfo_d));
     // up to date only once the pass is enqueued (a failed launch leaves them stale)
     for (int q = 0; q < J.M; ++q) c->ch[J.chain[q]].res_stale = false;
   }
@@ -583,9 +585,9 @@ void nngp_ctx_destroy(nngp_ctx* c) {
   }
   for (auto& kv : c->graphs) hipGraphExecDestroy(kv.second);
   for (auto g : c->graph_objs) hipGraphDestroy(g);
-  std::vector<void*> ptrs = {c->locs_d, c->sc_d, c->scm_d, c->nn_d, c->linv_cur_d, c->sinfo_d, c->compact_loc_d,
+  std::vector<void*> ptrs = {c->locs_d, c->sc_d, c->scm_d, c->nn_d, c->linv_cur_d, c->b1_tab_d, c->sinfo_d, c->compact_loc_d,
                              c->dr_d, c->slot_dpos_d, c->ent_pk_d, c->ent_src_d, c->ent_val_d, c->w_slot_d,
-                             c->r_d, c->level_rows_d, c->obs_ptr_d, c->obs_idx_d, c->lm_d, c->y_d, c->tmp_d,
+                             c->r_d, c->level_rows_d, c->obs_ptr_d, c->obs_idx_d, c->ysum_d, c->lm_d, c->y_d, c->tmp_d,
                              c->tmp2_d, c->partials_d, c->res_d, c->z_d, c->scal_d, c->dbg_d,
                              c->chunk_first_d, c->loc_rank_d, c->pairs_d, c->level_ptr_d, c->zbuf_d, c->ent_pos_d, c->start_mask_d,
                              c->dpos_d, c->perm_d, c->tb_d, c->tb_ptr_d, c->cell_pk_d, c->cell_src_d,
@@ -999,8 +1001,10 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     CK(dalloc(&s.field_d, n));
     CK(dalloc(&s.field_prop_d, n));
     CK(dalloc(&s.mu_d, n_obs));
+    CK(dalloc(&s.b1_d, n));
   }
   CK(dalloc(&c->linv_cur_d, C));
+  CK(dalloc(&c->b1_tab_d, C));
   CK(hipHostMalloc((void**)&c->linv_cur_h, sizeof(double*) * C, hipHostMallocDefault));
   for (int k = 0; k < C; ++k) c->linv_cur_h[k] = c->ch[k].linv_d[0];
   CK(dalloc(&c->sinfo_d, NS));
@@ -1108,7 +1112,6 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
         c->tprobe = std::atoi(pr) == 9 ? 1 : 2;
         c->tdbg_n = (size_t)TL.T * (c->tprobe == 1 ? 8 : 512 * 16);  // tiles.hip kTimelinePhases x kTimelineSlots
         if (const char* v = std::getenv("NNGP_TILE_VARIANT")) c->tvariant = std::atoi(v);
-        if (const char* v = std::getenv("NNGP_TILE_PF")) c->tpf = std::atoi(v);
         CK(dalloc(&c->tdbg_d, c->tdbg_n));
         CK(hipMemsetAsync(c->tdbg_d, 0, sizeof(unsigned long long) * c->tdbg_n, c->st));
       }
@@ -1179,6 +1182,13 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
       sd[x].y = c->engine == 1 ? c->tl.slot_f0[x] : (L.slot_f0[x] | (L.collen[x] << 16));
     }
     CK(hipMemcpy(c->sinfo_d, sd.data(), sizeof(int2) * sd.size(), hipMemcpyHostToDevice));
+    std::vector<double> ys(NS, 0.0);
+    for (size_t x = 0; x < NS; ++x) {
+      const int i = L.compact_loc[x];
+      for (int p = obs_cnt[i]; p < obs_cnt[i + 1]; ++p) ys[x] += observed_field[obs_idx[p]];
+    }
+    CK(dalloc(&c->ysum_d, NS));
+    CK(hipMemcpy(c->ysum_d, ys.data(), sizeof(double) * NS, hipMemcpyHostToDevice));
     CK(hipMemcpy(c->compact_loc_d, L.compact_loc.data(), sizeof(int) * NS, hipMemcpyHostToDevice));
   }
   CK(hipMemsetAsync(c->dr_d, 0, sizeof(double2) * NS * C, c->st));
@@ -1229,6 +1239,11 @@ static int ctx_create(const double* locs, int n, int d, const int* NNarray, int 
     CK(upload(c->sp_pairs_d, SP.pairs.data(), SP.pairs.size(), c->st));
   }
   CK(hipMemcpyAsync(c->linv_cur_d, c->linv_cur_h, sizeof(double*) * C, hipMemcpyHostToDevice, c->st));
+  {
+    std::vector<const double*> b1p(C);
+    for (int k = 0; k < C; ++k) b1p[k] = c->ch[k].b1_d;
+    CK(upload(c->b1_tab_d, b1p.data(), (size_t)C, c->st));
+  }
   CK(upload(c->level_rows_d, c->level_rows.data(), n, c->st));
   CK(upload(c->obs_ptr_d, obs_cnt.data(), (size_t)n + 1, c->st));
   CK(upload(c->obs_idx_d, obs_idx.data(), n_obs, c->st));
@@ -1874,7 +1889,7 @@ static int sweep_prepare(nngp_ctx* c, int k, double beta0, double log_scale, dou
   sc.inv_s2 = std::exp(-log_scale);
   sc.inv_t2 = std::exp(-lnv);
   sc.beta0 = beta0;
-  sc.pad = 0;
+  sc.dshift = 0.0;
   sc.seed = seed;
   sc.counter_base = counter_base;
   return NNGP_OK;
@@ -2006,31 +2021,27 @@ static void warm_kinds(const nngp_ctx* c, int mask, const double* beta0, int* co
   }
 }
 
-// w -= d, r -= d B 1 for the chains of shift (B 1 computed once per factor
-// generation), stream-ordered before the call's colour launches
-static int enqueue_warm_shift(nngp_ctx* c, int shift, const double* beta0) {
-  WarmShift a;
-  std::memset(&a, 0, sizeof a);
-  a.mask = shift;
+// the chains of shift start from w - d and r - d B 1 (the tile kernel's
+// prologue and first draws, SweepScalars::dshift; B 1 computed once per
+// factor generation, stream-ordered before the launch).  Call after
+// sweep_prepare (which zeroes dshift) and before upload_scalars.
+static int stage_warm_shift(nngp_ctx* c, int shift, const double* beta0) {
   for (int k = 0; k < c->C; ++k) {
     if (!((shift >> k) & 1)) continue;
     ChainState& S = c->ch[k];
-    if (!S.b1_d) HIPCHK(c, dalloc(&S.b1_d, (size_t)c->n));
     if (S.b1_lgen != S.lgen[0]) {
       HIPCHK(c, launch_linv_rowsum(c->st, S.linv_d[0], c->n, c->b, S.b1_d));
       S.b1_lgen = S.lgen[0];
     }
-    a.b1[k] = S.b1_d;
-    a.d[k] = beta0[k] - S.warm_beta0;
+    c->scal_h[k].dshift = beta0[k] - S.warm_beta0;
   }
-  HIPCHK(c, launch_warm_shift(c->st, c->n, c->C, a, c->w_slot_d, c->r_d));
   return NNGP_OK;
 }
 
 // the call's launches: one captured graph of the whole call when every chain
-// is cold; else the prologue graph of the cold chains, the shift of the
-// shifted ones and the graph of the colours + epilogue
-static int enqueue_call(nngp_ctx* c, int n_sweeps, int mask, int cold, int shift, const double* beta0) {
+// is cold; else the prologue graph of the cold chains and the graph of the
+// colours + epilogue (warm and shifted chains start from the last call's w, r)
+static int enqueue_call(nngp_ctx* c, int n_sweeps, int mask, int cold) {
   hipGraphExec_t ex;
   int rc;
   if (cold == mask) {
@@ -2042,7 +2053,6 @@ static int enqueue_call(nngp_ctx* c, int n_sweeps, int mask, int cold, int shift
     if ((rc = graph_for(c, n_sweeps, cold, &ex, kPrologue))) return rc;
     HIPCHK(c, hipGraphLaunch(ex, c->st));
   }
-  if (shift && (rc = enqueue_warm_shift(c, shift, beta0))) return rc;
   if ((rc = graph_for(c, n_sweeps, mask, &ex, kColours | kEpilogue))) return rc;
   HIPCHK(c, hipGraphLaunch(ex, c->st));
   return NNGP_OK;
@@ -2086,6 +2096,7 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
   if (!z) warm_kinds(c, mask, b0v, &cold, &shift);
   fields_written(c, mask);
   if ((rc = sweep_prepare(c, k, beta0, log_scale, lnv, seed, counter_base))) return rc;
+  if (shift && (rc = stage_warm_shift(c, shift, b0v))) return rc;
   if ((rc = flush_sweep_values(c, mask))) return rc;
   if ((rc = upload_scalars(c))) return rc;
   if (sharded_call(c)) {
@@ -2119,7 +2130,7 @@ int nngp_sweep(nngp_ctx* c, int n_sweeps, double beta0, double log_scale, double
   } else {
     // replay captured graphs of the call (launch-bound at small n)
     if (c->engine == 1 && (rc = tile_chain_wait(c))) return rc;
-    if ((rc = enqueue_call(c, n_sweeps, mask, cold, shift, b0v))) return rc;
+    if ((rc = enqueue_call(c, n_sweeps, mask, cold))) return rc;
     if (c->inject_tmo > 0 && c->engine == 1) {
       --c->inject_tmo;
       HIPCHK(c, launch_tile_inject_timeout(c->st, c->ctl_d));
@@ -2149,6 +2160,7 @@ int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const doub
   fields_written(c, all);
   for (int k = 0; k < c->C; ++k)
     if ((rc = sweep_prepare(c, k, beta0[k], log_scale[k], lnv[k], seed[k], counter_base[k]))) return rc;
+  if (shift && (rc = stage_warm_shift(c, shift, beta0))) return rc;
   if ((rc = flush_sweep_values(c, all))) return rc;
   if ((rc = upload_scalars(c))) return rc;
   if (sharded_call(c)) return shard_call(c, n_sweeps, all);
@@ -2158,7 +2170,7 @@ int nngp_sweep_chains(nngp_ctx* c, int n_sweeps, const double* beta0, const doub
   if (c->engine == 1) tlk = std::unique_lock<std::mutex>(tile_lock(c->device));
   const bool async = sweep_async(c);
   if (c->engine == 1 && (rc = tile_chain_wait(c))) return rc;
-  if ((rc = enqueue_call(c, n_sweeps, all, cold, shift, beta0))) return rc;
+  if ((rc = enqueue_call(c, n_sweeps, all, cold))) return rc;
   if (c->inject_tmo > 0 && c->engine == 1) {
     --c->inject_tmo;
     HIPCHK(c, launch_tile_inject_timeout(c->st, c->ctl_d));

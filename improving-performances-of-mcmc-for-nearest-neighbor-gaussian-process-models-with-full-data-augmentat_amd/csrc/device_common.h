@@ -2,6 +2,7 @@
 // DPP moves, the Philox4x32-10 counter RNG and the AS241 normal inversion.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cmath>
 #include <cstdint>
 
 namespace nngp {
@@ -13,6 +14,16 @@ __device__ __forceinline__ double dpp_f64(double x) {
   const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, RM, 0xF, BC);
   const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, RM, 0xF, BC);
   return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32));
+}
+
+// 1/sqrt(s) for normal s > 0: hardware rsq + two Newton-Raphson steps
+// (within ~1 ulp).
+__device__ __forceinline__ double rsqrt_pos(double s) {
+  double y = __builtin_amdgcn_rsq(s);
+  const double hs = 0.5 * s;
+  y = y * __builtin_fma(-hs * y, y, 1.5);
+  y = y * __builtin_fma(-hs * y, y, 1.5);
+  return y;
 }
 
 // ------------------------------------------------------------------ RNG
@@ -31,8 +42,51 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
   }
 }
 
+// log x for x in (0, 1] (AS241's tail, x = min(p, 1 - p) < 0.075): x = m 2^e
+// with m in [sqrt(1/2), sqrt(2)), log x = e ln2 + 2 atanh(s), s = (m-1)/(m+1),
+// |s| <= 0.1716, the atanh series to s^21 (truncation < 2^-55 relative);
+// s by a hardware reciprocal, two Newton steps and one residual correction.
+// Within 2 ulp of the correctly rounded log (tests: test_log_unit_accuracy,
+// CPU; device normals vs the oracle's libm-based ones to 1e-14), about a
+// third of the instructions of the library log on the sweep's critical path.
+__host__ __device__ __forceinline__ double log_unit(double x) {
+  int e;
+  double m = frexp(x, &e);
+  if (m < 0.70710678118654752440) {
+    m += m;
+    --e;
+  }
+  const double f = m - 1.0, d = m + 1.0;
+#ifdef __HIP_DEVICE_COMPILE__
+  double y = __builtin_amdgcn_rcp(d);
+#else
+  double y = 1.0 / d;
+#endif
+  y = fma(fma(-d, y, 1.0), y, y);
+  y = fma(fma(-d, y, 1.0), y, y);
+  double s = f * y;
+  s = fma(fma(-d, s, f), y, s);
+  const double z = s * s;
+  double q = 2.0 / 21.0;
+  q = fma(q, z, 2.0 / 19.0);
+  q = fma(q, z, 2.0 / 17.0);
+  q = fma(q, z, 2.0 / 15.0);
+  q = fma(q, z, 2.0 / 13.0);
+  q = fma(q, z, 2.0 / 11.0);
+  q = fma(q, z, 2.0 / 9.0);
+  q = fma(q, z, 2.0 / 7.0);
+  q = fma(q, z, 2.0 / 5.0);
+  q = fma(q, z, 2.0 / 3.0);
+  // 2 atanh(s) = 2 s + s z q; e ln2 with ln2 split (the high part has 11
+  // trailing zero bits: e ln2_hi is exact for |e| < 2^11)
+  const double ed = (double)e;
+  const double lo = fma(ed, 1.90821492927058770002e-10, s * z * q);
+  return fma(ed, 6.93147180369123816490e-01, fma(2.0, s, lo));
+}
+
 // Standard normal by inversion (R's own default, norm_rand INVERSION ->
-// qnorm): Wichura's AS241 (PPND16) at p in (0, 1).
+// qnorm): Wichura's AS241 (PPND16) at p in (0, 1); the tail's log by
+// log_unit (the oracle uses libm's: the normals agree to ~1e-16).
 __device__ __forceinline__ double qnorm_as241(double p) {
   const double q = p - 0.5;
   double r, val;
@@ -46,7 +100,7 @@ __device__ __forceinline__ double qnorm_as241(double p) {
              42.313330701600911252) * r + 1.);
   }
   r = q < 0 ? p : 1.0 - p;
-  r = sqrt(-log(r));
+  r = sqrt(-log_unit(r));
   if (r <= 5.) {
     r -= 1.6;
     val = (((((((r * 7.7454501427834140764e-4 + .0227238449892691845833) * r + .24178072517745061177) * r +

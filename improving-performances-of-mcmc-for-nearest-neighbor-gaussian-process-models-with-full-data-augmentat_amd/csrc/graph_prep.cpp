@@ -967,8 +967,8 @@ void dag_levels(const int* nn, int n, int b, std::vector<int>& level_ptr, std::v
 
 int tile_lds_bytes(int max_rows, int C, int NT, int K, int max_batches, int max_gslots) {
   const int rbytes = ((max_rows * C * 8 + 15) / 16) * 16;
-  return rbytes + kAccSlots * C * 8 + (NT / 64) * C * 8 + 4 * C * 8 + ((max_gslots * C + 1) / 2) * 16 +
-         max_batches * 16 + 4 * (K + 1) * 4 + (NT / 64) * 4 + 64 + kTilePfLds;
+  return rbytes + kAccSlots * C * 8 + (NT / 64) * C * 8 + 5 * C * 8 + ((max_gslots * C + 1) / 2) * 16 +
+         max_batches * 16 + 4 * (K + 1) * 4 + (NT / 64) * 4 + 64;
 }
 
 }  // namespace nngp

@@ -163,9 +163,6 @@ constexpr int kWaveSlotsMax = 42;  // slots of a wave-local batch (7 x 42 = 294 
 // slot totals a tile workgroup keeps in LDS (acc_s): a workgroup batch's
 // kTileSlotsMax, or the 7 cell waves' wave-local batches of a 512-thread tile
 constexpr int kAccSlots = 7 * kWaveSlotsMax > kTileSlotsMax ? 7 * kWaveSlotsMax : kTileSlotsMax;
-// the tile's LDS tail past its 64-byte words: the landing area of the L2
-// prefetch's LDS-DMA loads (64 lanes x 4 B, never read; tiles.hip)
-constexpr int kTilePfLds = 256;
 
 // Fails (returns false, err set) when the layout does not fit the packed
 // formats; the caller checks the LDS budget (max_rows).

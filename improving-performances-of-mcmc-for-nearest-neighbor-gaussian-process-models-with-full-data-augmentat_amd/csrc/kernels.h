@@ -15,7 +15,7 @@ struct SweepScalars {
   double inv_s2;     // exp(-log_scale)
   double inv_t2;     // exp(-log_noise_variance)
   double beta0;
-  double pad;
+  double dshift;     // warm tile call after a beta_0-only change: w -= dshift, r -= dshift B 1 (else 0)
   uint64_t seed;
   uint64_t counter_base;
 };
@@ -167,7 +167,8 @@ struct ResJobs {
   int M = 0;
 };
 hipError_t launch_residual_sums_jobs(hipStream_t st, int n, const SweepDev& L, const ResJobs& J,
-                                     const int* obs_ptr, const int* obs_idx, const double* y);
+                                     const int* obs_ptr, const int* obs_idx, const double* y,
+                                     const double* ysum = nullptr, const int2* sinfo = nullptr);
 // obs reductions (as launch_obs_reduce) of up to kMaxChains chains in one
 // pass; partials of job j at partials + j * kRedBlocks * 4.  Returns #blocks.
 struct ObsJobs {
@@ -228,6 +229,7 @@ struct TileDev {
   const double* r;            // device rows x C (r = B w at call start)
   double* rg;                 // tiles with r in global memory: local rows x C (null: r in LDS)
   const SweepScalars* scal;   // C
+  const double* const* b1;    // C: B 1 of each chain's current factor (device rows; read when scal.dshift != 0)
   unsigned* ctl;              // [0] call id (bumped on the device before every launch), [1] timeout word
   unsigned long long* dbg;    // NNGP_PROBE=9 / 2: per-tile phase times / per-phase timeline, else null
   int K, C, T, n;
@@ -235,7 +237,6 @@ struct TileDev {
   int probe = 0;              // dbg layout: 1 = per-tile segment sums (T x 8), 2 = timeline (T x 512 phases x 8)
   int xw = 0;                 // exchange-wave tiles: the last wave polls the hand-offs, the
                               // layout's batches are cut for NT - 64 cell threads
-  int pf = 0;                 // NNGP_TILE_PF: L2 prefetch of the next phase's stream during the own work
 };
 
 struct TileLaunch {
@@ -332,14 +333,8 @@ hipError_t launch_tri_levels_block(hipStream_t st, const TriArgs& a, const int* 
 // clears it), [1] the rescue word, [2..3] the rescue ticket counter (both
 // reset by the launch; kernels.hip tri_dag_kernel); rescue: every wave takes
 // the ticket order from the start (tests)
-// warm sweep calls after a beta_0-only change (kernels.hip warm_shift_kernel)
-struct WarmShift {
-  const double* b1[kMaxChains];  // B 1 of each chain's current factor (device rows)
-  double d[kMaxChains];          // beta_0 new - beta_0 of the last call
-  int mask;
-};
+// B 1 (row sums of a factor): the warm tile call after a beta_0-only change
 hipError_t launch_linv_rowsum(hipStream_t st, const double* linv, int n, int b, double* out);
-hipError_t launch_warm_shift(hipStream_t st, int n, int C, const WarmShift& a, double* w_slot, double* r);
 hipError_t launch_tri_dag(hipStream_t st, const TriArgs& a, const int* rows, int nrows, const int* nn, int b,
                           const double* u, double* x, long long x_len, unsigned* ctl, bool rescue = false,
                           int oversub = 1);

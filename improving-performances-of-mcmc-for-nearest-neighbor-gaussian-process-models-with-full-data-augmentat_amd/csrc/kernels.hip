@@ -179,15 +179,6 @@ __device__ __forceinline__ double sqrt_pos(double s) {
   return __builtin_fma(e, h, g);
 }
 
-// 1/sqrt(s) for normal s > 0: hardware rsq + two Newton-Raphson steps
-// (within ~1 ulp).
-__device__ __forceinline__ double rsqrt_pos(double s) {
-  double y = __builtin_amdgcn_rsq(s);
-  const double hs = 0.5 * s;
-  y = y * __builtin_fma(-hs * y, y, 1.5);
-  y = y * __builtin_fma(-hs * y, y, 1.5);
-  return y;
-}
 
 // correlation at unit-range distance dist.  FAM 0: exponential, 1: Matern 3/2,
 // 2: general Matern with norm = 2^(1-nu)/Gamma(nu)
@@ -1384,9 +1375,31 @@ __global__ void residual_sums_jobs_kernel(int n, SweepDev L, ResJobs J, const in
     if (j < J.M) L.dr[(size_t)s * L.C + J.chain[j]].y = R[j];
 }
 
+// every job with mu = beta_0 (no X, update_Gaussian.R:85-90): R = sum y -
+// n_obs beta_0 per slot from the per-slot sums of y (ysum, compact order,
+// fixed per context) -- a streaming pass instead of the gathers over the
+// observations (the data term moves with every beta_0 draw)
+__global__ void residual_sums_const_kernel(int n, SweepDev L, ResJobs J, const double* __restrict__ ysum,
+                                           const int2* __restrict__ sinfo) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const double ys = ysum[s], no = (double)sinfo[s].x;
+#pragma unroll
+  for (int j = 0; j < kMaxChains; ++j)
+    if (j < J.M) L.dr[(size_t)s * L.C + J.chain[j]].y = __builtin_fma(-no, J.beta0[j], ys);
+}
+
 hipError_t launch_residual_sums_jobs(hipStream_t st, int n, const SweepDev& L, const ResJobs& J,
-                                     const int* obs_ptr, const int* obs_idx, const double* y) {
+                                     const int* obs_ptr, const int* obs_idx, const double* y, const double* ysum,
+                                     const int2* sinfo) {
   if (J.M < 1 || J.M > kMaxChains) return hipErrorInvalidValue;
+  bool all_const = ysum && sinfo;
+  for (int j = 0; j < J.M; ++j) all_const &= J.mu[j] == nullptr;
+  if (all_const) {
+    hipLaunchKernelGGL(residual_sums_const_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, n, L, J, ysum,
+                       sinfo);
+    return hipGetLastError();
+  }
   int g = (n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(residual_sums_jobs_kernel, dim3(g), dim3(kBlock), 0, st, n, L, J, obs_ptr, obs_idx, y);
   return hipGetLastError();
@@ -2085,8 +2098,8 @@ hipError_t launch_tri_dag(hipStream_t st, const TriArgs& a, const int* rows, int
 }
 
 // B 1 (row sums of the factor, device row order): a warm sweep call after a
-// beta_0-only change (update_Gaussian.R:219-224) shifts r = B w by
-// -dbeta0 B 1 instead of recomputing it (capi.hip warm_kinds)
+// beta_0-only change (update_Gaussian.R:219-224) starts from r - d B 1
+// instead of recomputing r = B w (capi.hip warm_kinds, tiles.hip prologue)
 __global__ void linv_rowsum_kernel(const double* __restrict__ linv, int n, int b, double* __restrict__ out) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     double s = 0.0;
@@ -2098,27 +2111,6 @@ __global__ void linv_rowsum_kernel(const double* __restrict__ linv, int n, int b
 hipError_t launch_linv_rowsum(hipStream_t st, const double* linv, int n, int b, double* out) {
   const int g = std::min((n + 255) / 256, 4096);
   hipLaunchKernelGGL(linv_rowsum_kernel, dim3(g > 0 ? g : 1), dim3(256), 0, st, linv, n, b, out);
-  return hipGetLastError();
-}
-
-// the chains of a.mask: w (slot order) -= d_k, r (row order) -= d_k (B 1)_k
-// -- w = field - beta_0 and r = B w after beta_0 moved by d_k with the field
-// and the factor unchanged
-__global__ void warm_shift_kernel(int n, int C, WarmShift a, double* __restrict__ w_slot, double* __restrict__ r) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-#pragma unroll
-    for (int k = 0; k < kMaxChains; ++k) {
-      if (k < C && ((a.mask >> k) & 1)) {
-        w_slot[(size_t)i * C + k] -= a.d[k];
-        r[(size_t)i * C + k] -= a.d[k] * a.b1[k][i];
-      }
-    }
-  }
-}
-
-hipError_t launch_warm_shift(hipStream_t st, int n, int C, const WarmShift& a, double* w_slot, double* r) {
-  const int g = std::min((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(warm_shift_kernel, dim3(g > 0 ? g : 1), dim3(256), 0, st, n, C, a, w_slot, r);
   return hipGetLastError();
 }
 

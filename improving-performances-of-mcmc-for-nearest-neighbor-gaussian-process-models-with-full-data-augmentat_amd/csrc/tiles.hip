@@ -258,9 +258,13 @@ __device__ __forceinline__ void tile_prep_items(const TileDev& D, const TileLaun
       const double a0 = (var & 4) ? 1.0 : b.a0[k], a1 = (var & 4) ? 0.5 : b.a1[k], wk = (var & 4) ? 0.0 : b.w[k];
       const double P = a0 * inv_s2 + (double)((var & 4) ? 1 : b.nobs[k]) * inv_t2;
       const double cR = inv_t2 * a1 + inv_s2 * (a0 * wk);
+      // 1/sqrt(P) once (hardware rsq + Newton) for both 1/P and z/sqrt(P):
+      // a few instructions instead of a square root and two divisions on the
+      // cell waves' path (within ~2 ulp of them)
+      const double rs = rsqrt_pos(P);
       b.a0[k] = cR;
-      b.a1[k] = 1.0 / P;
-      b.zs[k] = z / sqrt(P);
+      b.a1[k] = rs * rs;
+      b.zs[k] = z * rs;
     }
   }
 }
@@ -302,6 +306,7 @@ struct TileState {
   double* wsum;
   double* sc_s;   // C x {inv_s2, inv_t2}
   unsigned long long* seed_s;  // C x {seed, counter_base}
+  double* dsh_s;  // C: the call's beta_0 shift of each chain (SweepScalars::dshift; sweep 0's w)
   int4* batch_s;  // this tile's own batches
   int* bptr_s;    // K+1: batches of colour c = batch_s[bptr_s[c] .. bptr_s[c+1])
   int* gptr_s;    // K+1: ghost cells of colour c (global indices)
@@ -318,8 +323,8 @@ struct TileState {
   int G;                            // tile shard: ranks (1: single GPU)
   bool timed_out;
   int T, t, lane, wv, K, nph, ph;
+  uint32_t lrmax;                   // the tile's last local row (padding cells read it, times a zero value)
   unsigned long long tp[8], t_prev;
-  uint32_t pf_lds;                  // LDS byte address of the prefetch landing area (kTilePfLds)
 };
 
 template <int C, int GMAX>
@@ -368,16 +373,19 @@ constexpr int kTimelineSlots = 16;  // stamps per phase (capi.hip allocates T x 
 
 // one step of a segmented inclusive scan (flag f = "a segment starts here or
 // in an earlier lane of my partial"): (f_e, v_e) (+) (f, v) = (f_e | f, f ? v : v_e + v)
+// (v = fma(e, keep, v) with keep = f ? 0 : 1 is bitwise the select of
+// e + v and v -- round(e * 1 + v) = round(e + v), e * 0 + v = v for the
+// finite e of a scan -- in one instruction instead of an add and two
+// 32-bit selects per chain)
 template <int CTRL, int RM, bool BC, int C>
 __device__ __forceinline__ void seg_scan_step(double (&v)[C], int& f) {
   double e[C];
 #pragma unroll
   for (int ch = 0; ch < C; ++ch) e[ch] = dpp_f64<CTRL, RM, BC>(v[ch]);
   const int fe = __builtin_amdgcn_update_dpp(0, f, CTRL, RM, 0xF, BC);
-  if (!f) {
+  const double keep = f ? 0.0 : 1.0;
 #pragma unroll
-    for (int ch = 0; ch < C; ++ch) v[ch] = e[ch] + v[ch];
-  }
+  for (int ch = 0; ch < C; ++ch) v[ch] = __builtin_fma(e[ch], keep, v[ch]);
   f |= fe;
 }
 
@@ -414,10 +422,11 @@ __device__ __forceinline__ void tile_own_draw(const TileDev& D, const TileLaunch
     if (j < R) {
       const uint32_t lr = tile_lr(b.pk[j]);
       const bool st = (b.pk[j] & kTStart) != 0;
+      const double keep = st ? 0.0 : 1.0;  // restart at a slot start: run * 0 + p (see seg_scan_step)
 #pragma unroll
       for (int ch = 0; ch < C; ++ch) {
         const double p = (lr != kTPad) ? b.v[j][ch] * r_s[lr * C + ch] : 0.0;
-        run[ch] = st ? p : run[ch] + p;
+        run[ch] = __builtin_fma(run[ch], keep, p);
       }
       seen_start |= st;
       if (b.pk[j] & kTEnd) {
@@ -843,33 +852,35 @@ __device__ __forceinline__ void tile_own_wl(const TileDev& D, const TileLaunch& 
   double* __restrict__ acc_s = acc_w;
   const int R = b.R, nit = b.ns * C;
   tile_cells_landed(b);
-  double run[C], cont[C];
+  // Straight-line products: every live cell's r read goes out unmasked (a
+  // padding cell reads the tile's last row, times its zero value; lanes past
+  // the batch's live ones compute garbage that only flows to higher lanes and
+  // is never stored), the running sum restarts by a 0/1 multiplier (see
+  // seg_scan_step), and every slot end stores its run into acc_s -- also the
+  // one that continues a slot of earlier lanes, completed after the scan
+  // (acc_s[cont_q] += carry: the same operands as cont + carry).  No branch
+  // per cell beyond the end stores.
+  double run[C];
   int cont_q = -1;
   bool seen_start = false;
 #pragma unroll
-  for (int ch = 0; ch < C; ++ch) { run[ch] = 0.0; cont[ch] = 0.0; }
+  for (int ch = 0; ch < C; ++ch) run[ch] = 0.0;
 #pragma unroll
   for (int j = 0; j < RMAX; ++j) {
     if (j < R) {
-      const uint32_t lr = tile_lr(b.pk[j]);
-      const bool st = (b.pk[j] & kTStart) != 0;
+      const uint32_t pk = b.pk[j];
+      const uint32_t lr = min(tile_lr(pk), S.lrmax);
+      const bool st = (pk & kTStart) != 0;
+      const double keep = st ? 0.0 : 1.0;
 #pragma unroll
-      for (int ch = 0; ch < C; ++ch) {
-        const double p = (lr != kTPad) ? b.v[j][ch] * r_s[lr * C + ch] : 0.0;
-        run[ch] = st ? p : run[ch] + p;
+      for (int ch = 0; ch < C; ++ch) run[ch] = __builtin_fma(run[ch], keep, b.v[j][ch] * r_s[lr * C + ch]);
+      const int q = (int)((pk >> kTileQShift) & kTileQMask);
+      if (pk & kTEnd) {
+#pragma unroll
+        for (int ch = 0; ch < C; ++ch) acc_s[q * C + ch] = run[ch];
       }
-      seen_start |= st;
-      if (b.pk[j] & kTEnd) {
-        const int q = (int)((b.pk[j] >> kTileQShift) & kTileQMask);
-        if (seen_start) {
-#pragma unroll
-          for (int ch = 0; ch < C; ++ch) acc_s[q * C + ch] = run[ch];
-        } else {
-          cont_q = q;
-#pragma unroll
-          for (int ch = 0; ch < C; ++ch) cont[ch] = run[ch];
-        }
-      }
+      seen_start |= st;  // (before the end test: a slot may start and end at this cell)
+      cont_q = ((pk & kTEnd) && !seen_start && cont_q < 0) ? q : cont_q;
     }
   }
   // segmented inclusive scan of the lane tails inside the wave (as
@@ -889,7 +900,7 @@ __device__ __forceinline__ void tile_own_wl(const TileDev& D, const TileLaunch& 
   for (int ch = 0; ch < C; ++ch) {
     const double up = dpp_f64<0x138, 0xF, true>(v[ch]);  // wave_shr:1
     const double cp = lane ? up : 0.0;
-    if (cont_q >= 0) acc_s[cont_q * C + ch] = cont[ch] + cp;
+    if (cont_q >= 0) acc_s[cont_q * C + ch] = acc_s[cont_q * C + ch] + cp;
   }
   wave_lds_order();
 #pragma unroll
@@ -927,41 +938,6 @@ __device__ __forceinline__ void tile_own_wl(const TileDev& D, const TileLaunch& 
     D.dbg[((size_t)S.T * kTimelinePhases + S.ph) * kTimelineSlots + 9 + S.wv] = __builtin_amdgcn_s_memrealtime();
 }
 
-// L2 prefetch without registers: one LDS-DMA dword load per lane, each
-// lane's address in a different 128-B line, landing in the tile's dummy LDS
-// area (kTilePfLds, never read).  Inline asm, so the compiler's s_waitcnt
-// bookkeeping does not see it: no wait is inserted for it, and a later wait
-// for an ordinary load (vmcnt counts in issue order) covers it conservatively.
-__device__ __forceinline__ void l2_touch(const void* p, uint32_t lds_dummy) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(p), "s"(__builtin_amdgcn_readfirstlane(lds_dummy)) : "memory");
-}
-
-// the next batch's cells of this cell wave into L2 while the own work runs
-// (NNGP_TILE_PF): its cell_pk run (R x 256 B) and, per chain, its cell_val
-// run (R x 512 B), one touch per 128 B -- lanes 16q..16q+15 take run q
-// (0: cell_pk, 1..3: chain q-1), two instructions cover R <= 8.  The bases
-// are wave-uniform (scalar registers): a few transient VGPRs per touch.
-template <int C>
-__device__ __forceinline__ void tile_prefetch_next(const TileDev& D, const TileState& S, int bnext, bool more,
-                                                   uint32_t lds_dummy) {
-  if (!more) return;
-  const int lane = S.lane;
-  const int bx = __builtin_amdgcn_readfirstlane(S.batch_s[bnext].x);
-  const int R = __builtin_amdgcn_readfirstlane(S.batch_s[bnext].y) & 0xFFFF;
-  const char* pk = reinterpret_cast<const char*>(D.cell_pk + bx);
-  const char* v0 = reinterpret_cast<const char*>(D.cell_val + bx);
-  const int q = lane >> 4;
-  const int lines = q == 0 ? 2 * R : 4 * R;
-  const char* base = (q == 0 || q > C) ? pk : v0 + (long long)(q - 1) * D.n_cells * 8;
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int li = (lane & 15) + 16 * k;
-    l2_touch(base + (li < lines ? li : 0) * 128, lds_dummy);
-  }
-}
-
 // the cell waves' colour phase on wave-local batches.  DB (<= 2 chains, two
 // register sets): the wave's next batch loads at the phase start, its HBM
 // stream overlapping this colour's work; otherwise its records after the
@@ -997,10 +973,6 @@ __device__ __forceinline__ void tile_phase_wl(const TileDev& D, const TileLaunch
     if (bi + W >= bend) {  // this wave's last batch of the colour: its records are dead
       if (!DB && more) tile_load_items<C, 64, RMAX, SH>(D, S.batch_s[bnext], nxt, lane);
       if (g1 > g0) tile_load_ghosts<C, NT, GMAX>(D, g0, g1, gr, t);
-      // NNGP_TILE_PF: the next batch's cells into L2 now, behind the records
-      // and ghosts (their waits do not cover it), ahead of the scatter and
-      // the draw preparation
-      if (!DB && D.pf) tile_prefetch_next<C>(D, S, bnext, more, S.pf_lds);
     }
     tile_own_scatter<C, 64, RMAX, PROBE>(S, cur, R, acc_w);
   }
@@ -1343,6 +1315,7 @@ __device__ __forceinline__ void sweep_tiles_body(const TileDev& D0, TileLaunch a
     D.dwx += 2 * ch0;  // 16-B granules
     D.r += ch0;
     D.scal += ch0;
+    D.b1 += ch0;
     a.chain_mask >>= ch0;
     if (a.z_in) a.z_in += ch0;
   }
@@ -1355,13 +1328,15 @@ __device__ __forceinline__ void sweep_tiles_body(const TileDev& D0, TileLaunch a
   S.t_prev = 0;
   const int T = S.T, t = S.t, K = D.K;
   const int row0 = D.erow_ptr[T], nrows = D.erow_ptr[T + 1] - row0;
+  S.lrmax = nrows > 0 ? (uint32_t)(nrows - 1) : 0u;
   const int b_lo = D.batch_ptr[T * K], nbt = D.batch_ptr[T * K + K] - b_lo;
   S.r_s = RG ? D.rg + (size_t)row0 * C : smem;
   S.acc_s = RG ? smem : smem + ((nrows * C + 1) / 2) * 2;  // kAccSlots x C: slot totals, then dw
   S.wsum = S.acc_s + kAccSlots * C;              // NW x C: segmented wave totals
   S.sc_s = S.wsum + NW * C;                      // C x {inv_s2, inv_t2}
   S.seed_s = reinterpret_cast<unsigned long long*>(S.sc_s + 2 * C);
-  S.gdw_s = reinterpret_cast<double*>(S.seed_s + 2 * C);  // max foreign slots x C (even count)
+  S.dsh_s = reinterpret_cast<double*>(S.seed_s + 2 * C);  // C
+  S.gdw_s = S.dsh_s + C;                         // max foreign slots x C (even count)
   S.batch_s = reinterpret_cast<int4*>(S.gdw_s + ((D.max_gslots * C + 1) / 2) * 2);
   S.bptr_s = reinterpret_cast<int*>(S.batch_s + nbt);
   S.gptr_s = S.bptr_s + K + 1;
@@ -1372,12 +1347,21 @@ __device__ __forceinline__ void sweep_tiles_body(const TileDev& D0, TileLaunch a
   if (PROBE == 2 && t == 0) *S.spin_s = 0;
   S.pub_s = reinterpret_cast<int*>(S.spin_s + 1);        // (tile_lds_bytes' 64-byte tail)
   if (t == 0) *S.pub_s = -1;
-  S.pf_lds = (uint32_t)reinterpret_cast<uintptr_t>(reinterpret_cast<char*>(S.spin_s) + 64);  // kTilePfLds past the tail
   TSTAMP(S, -1);
-  for (int lr = t; lr < nrows; lr += NT) {
-    const size_t g = (size_t)D.erow[row0 + lr] * CS;
+  // r of the local rows as the last call left it; a warm call after a
+  // beta_0-only change (capi.hip warm_kinds) starts from r - d B 1, and its
+  // own slots' w from w - d (below)
+  double dsh[C];
 #pragma unroll
-    for (int ch = 0; ch < C; ++ch) S.r_s[lr * C + ch] = D.r[g + ch];
+  for (int ch = 0; ch < C; ++ch) dsh[ch] = D.scal[ch].dshift;
+  for (int lr = t; lr < nrows; lr += NT) {
+    const int row = D.erow[row0 + lr];
+    const size_t g = (size_t)row * CS;
+#pragma unroll
+    for (int ch = 0; ch < C; ++ch) {
+      const double v = D.r[g + ch];
+      S.r_s[lr * C + ch] = dsh[ch] != 0.0 ? __builtin_fma(-dsh[ch], D.b1[ch][row], v) : v;
+    }
   }
   // per-tile metadata in LDS: no dependent scalar loads in the phase loop
   for (int i = t; i < nbt; i += NT) S.batch_s[i] = D.batch[b_lo + i];
@@ -1388,6 +1372,7 @@ __device__ __forceinline__ void sweep_tiles_body(const TileDev& D0, TileLaunch a
     if (IB) S.bsp_s[i] = i < K ? D.batch_split[T * K + i] - b_lo : 0;
   }
   if (t < C) {
+    S.dsh_s[t] = D.scal[t].dshift;
     S.sc_s[2 * t] = D.scal[t].inv_s2;
     S.sc_s[2 * t + 1] = D.scal[t].inv_t2;
     S.seed_s[2 * t] = D.scal[t].seed;
@@ -1398,6 +1383,17 @@ __device__ __forceinline__ void sweep_tiles_body(const TileDev& D0, TileLaunch a
   S.tmo = D.ctl + 1;
   S.gran = __builtin_amdgcn_make_buffer_rsrc(SH ? sh.gx[rk] : D.dwx, 0, 0x7FFFFFFF, 0x00020000);
   __syncthreads();
+  bool shifted = false;
+#pragma unroll
+  for (int ch = 0; ch < C; ++ch) shifted |= dsh[ch] != 0.0;
+  if (shifted && nbt > 0) {
+    // w = field - beta_0 of the own slots (one contiguous range: slot order
+    // is tile-major, the batches cover it in order) moved by -d before any
+    // batch loads it; the stores are this workgroup's, ordered by the barrier
+    const int x0 = S.batch_s[0].w, x1 = S.batch_s[nbt - 1].w + S.batch_s[nbt - 1].z;
+    for (int u = t; u < (x1 - x0) * C; u += NT) D.w_slot[tile_xu<C, CS>(x0, u)] -= S.dsh_s[u % C];
+    __syncthreads();
+  }
   if constexpr (XW) {
     if (S.wv == NW - 1) {  // the exchange wave
       TileGhostRegs<C, GMAX> GX;

@@ -1,6 +1,7 @@
 #!/bin/bash
 # the driver's bench command, the default bench, rocprofv3 kernel stats of the bench and the PMC
-# FETCH/WRITE passes of the sweep kernel (scripts/pmc.sh) -> gpurun_out/
+# FETCH/WRITE passes of the sweep kernel (scripts/pmc.sh) and the request-size passes
+# (scripts/pmc_sizes.sh) -> gpurun_out/
 cd $GRAFT_REPO_ROOT
 ROOTDIR=$(pwd); export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -10,4 +11,4 @@ timeout -k 10 400 python -u bench.py > gpurun_out/bench_default.json 2> gpurun_o
 cut -c1-300 gpurun_out/bench_default.json
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOTDIR/gpurun_out/prof_final -o run -- python3 $ROOTDIR/bench.py --steps 60 --warmup 10 --no-cpu-baseline --mcmc-iters 0 > $ROOTDIR/gpurun_out/bench_prof_final.json 2> $ROOTDIR/gpurun_out/bench_prof_final.err) || exit 1
 f=$(find gpurun_out/prof_final -name "*kernel_stats.csv" | head -1); head -6 "$f" | cut -c1-200
-bash scripts/pmc.sh
+bash scripts/pmc.sh && bash scripts/pmc_sizes.sh

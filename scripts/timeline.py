@@ -97,4 +97,13 @@ ownc = own.reshape(T, S, K).mean(axis=(0, 1))
 ownmax = own.reshape(T, S, K).max(axis=0).mean(axis=0)
 print("per colour: phase mean / own mean / own max over tiles")
 print(" ".join(f"{c}:{byc[c]:.1f}/{ownc[c]:.1f}/{ownmax[c]:.1f}" for c in range(K)))
+# per colour, every segment of the cell waves' chain (mean over tiles and sweeps)
+segs = [("own", own), ("scatter", scat - pub), ("prep", landed - scat), ("wait", hand - landed), ("ghost", tail)]
+print("per colour segments (us): " + " / ".join(n for n, _ in segs))
+for c in range(K):
+    print(f"  c{c:2d} " + " ".join(f"{a.reshape(T, S, K)[:, :, c].mean():5.2f}" for _, a in segs) +
+          f"  = {byc[c]:5.2f}")
+if os.environ.get("NNGP_TIMELINE_KEEP"):
+    import shutil
+    shutil.copy(out, os.environ["NNGP_TIMELINE_KEEP"])
 ctx.close()

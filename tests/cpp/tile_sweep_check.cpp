@@ -176,6 +176,22 @@ int main(int argc, char** argv) {
         const TileBatch B = L.batch[bi];
         REQUIRE(B.slot0 >= L.rank_slot0[t / Tl] && B.slot0 + B.nslots <= L.rank_slot0[t / Tl + 1]);
       }
+    // a tile's batches, in order, cover one contiguous slot range with no gap
+    // (the kernel's beta_0-shift pass over [first batch's slot0, last batch's
+    // end), tiles.hip prologue), and the tiles' ranges partition the slots
+    {
+      int next = 0;
+      for (int t = 0; t < L.T; ++t) {
+        const int b0 = L.batch_ptr[(size_t)t * K], b1 = L.batch_ptr[(size_t)t * K + K];
+        if (b0 == b1) continue;
+        REQUIRE(L.batch[b0].slot0 == next);
+        for (int bi = b0; bi < b1; ++bi) {
+          REQUIRE(L.batch[bi].slot0 == next);
+          next += L.batch[bi].nslots;
+        }
+      }
+      REQUIRE(next == n);
+    }
     if (G > 1) {
       std::vector<uint32_t> want(n, 0u);
       for (int t = 0; t < L.T; ++t)

@@ -518,6 +518,23 @@ def test_r_shim_wraps_every_abi_entry_point():
         assert c in rfun, f"{c} has no R wrapper"
 
 
+def test_log_unit_accuracy(tmp_path):
+    """device_common.h log_unit (the log in the AS241 tail of the sweep's
+    normals, hardware reciprocal + atanh series) within 2 ulp of libm's log
+    over 4e6 of the sweep's uniforms and their scalings down to 2^-112
+    (host build of the same header with hipcc; no GPU needed)."""
+    import subprocess
+
+    root = Path(__file__).resolve().parent.parent
+    exe = tmp_path / "log_unit_check"
+    inc = root / "improving-performances-of-mcmc-for-nearest-neighbor-gaussian-process-models-with-full-data-augmentat_amd" / "csrc"
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", f"-I{inc}", str(root / "tests" / "cpp" / "log_unit_check.cpp"),
+                    "-o", str(exe)], check=True, capture_output=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "max_ulp" in r.stdout
+
+
 def test_r_records_transpose_matches_row_major(tmp_path):
     """rpkg/src/nngp_rows.h (C_nngp_get_records): k row-major record rows ->
     the first k rows of R's column-major records$field matrix, in cache
