@@ -412,34 +412,30 @@ __device__ __forceinline__ void tile_own_draw(const TileDev& D, const TileLaunch
   // cells may continue a slot of earlier threads: its end (if here) waits for
   // the carry of those threads.
   tile_cells_landed(b);
-  double run[C], cont[C];
+  // straight-line products as tile_own_wl's (padding reads the tile's last
+  // row times a zero value; every slot end stores its run, the continued
+  // slot of earlier threads completed after the scan)
+  double run[C];
   int cont_q = -1;
   bool seen_start = false;
 #pragma unroll
-  for (int ch = 0; ch < C; ++ch) { run[ch] = 0.0; cont[ch] = 0.0; }
+  for (int ch = 0; ch < C; ++ch) run[ch] = 0.0;
 #pragma unroll
   for (int j = 0; j < RMAX; ++j) {
     if (j < R) {
-      const uint32_t lr = tile_lr(b.pk[j]);
-      const bool st = (b.pk[j] & kTStart) != 0;
+      const uint32_t pk = b.pk[j];
+      const uint32_t lr = min(tile_lr(pk), S.lrmax);
+      const bool st = (pk & kTStart) != 0;
       const double keep = st ? 0.0 : 1.0;  // restart at a slot start: run * 0 + p (see seg_scan_step)
 #pragma unroll
-      for (int ch = 0; ch < C; ++ch) {
-        const double p = (lr != kTPad) ? b.v[j][ch] * r_s[lr * C + ch] : 0.0;
-        run[ch] = __builtin_fma(run[ch], keep, p);
-      }
-      seen_start |= st;
-      if (b.pk[j] & kTEnd) {
-        const int q = (int)((b.pk[j] >> kTileQShift) & kTileQMask);
-        if (seen_start) {
+      for (int ch = 0; ch < C; ++ch) run[ch] = __builtin_fma(run[ch], keep, b.v[j][ch] * r_s[lr * C + ch]);
+      const int q = (int)((pk >> kTileQShift) & kTileQMask);
+      if (pk & kTEnd) {
 #pragma unroll
-          for (int ch = 0; ch < C; ++ch) acc_s[q * C + ch] = run[ch];
-        } else {
-          cont_q = q;
-#pragma unroll
-          for (int ch = 0; ch < C; ++ch) cont[ch] = run[ch];
-        }
+        for (int ch = 0; ch < C; ++ch) acc_s[q * C + ch] = run[ch];
       }
+      seen_start |= st;  // (before the end test: a slot may start and end at this cell)
+      cont_q = ((pk & kTEnd) && !seen_start && cont_q < 0) ? q : cont_q;
     }
   }
   TSTAMP(S, 1);
@@ -476,7 +472,7 @@ __device__ __forceinline__ void tile_own_draw(const TileDev& D, const TileLaunch
     const double Sv = f ? v[ch] : v[ch] + in[ch];
     const double up = dpp_f64<0x138, 0xF, true>(Sv);  // wave_shr:1
     const double cp = lane ? up : in[ch];
-    if (cont_q >= 0) acc_s[cont_q * C + ch] = cont[ch] + cp;
+    if (cont_q >= 0) acc_s[cont_q * C + ch] = acc_s[cont_q * C + ch] + cp;
   }
   __syncthreads();
   TSTAMP(S, 2);
