@@ -584,21 +584,6 @@ def main():
                   "how": ("beta_0 alternates by 1e-9 between calls (an MCMC iteration's beta_0 Gibbs step): "
                           "field and factor unchanged, so every call shifts w by -d and r by -d B 1 instead of "
                           "rebuilding them (NNGP_SWEEP_SHIFT=0: rebuild)")}
-    if not args.no_rebuild_calls and info["sweep_engine"] == 1:
-        # the call after an accepted covariance proposal (new factor: r = B w
-        # rebuilt): the same calls on a context that rebuilds every call
-        os.environ["NNGP_SWEEP_WARM"] = "0"
-        try:
-            ctxr = open_context(P, wl, covfun, cp, local_rank, C, seed=7 + rank)
-        finally:
-            os.environ.pop("NNGP_SWEEP_WARM", None)
-        el_rb, _ = timed(ctxr, args.steps, args.warmup, cold=True)
-        ctxr.close()
-        cold_calls["rebuild_calls"] = {"value": args.steps * C * world / el_rb, "unit": "sweeps/s",
-                                       "ms_per_step": el_rb * 1e3 / args.steps,
-                                       "how": "every call rebuilds w -> slots and r = B w (NNGP_SWEEP_WARM=0 "
-                                              "context): the call after an accepted covariance proposal"}
-
     # per-kernel timing with HIP events on the context's own stream: the
     # sweep kernel's launches alone (tile engine: one persistent launch per
     # call of n_chromatic sweeps; colour engine: one launch per colour)
@@ -644,6 +629,24 @@ def main():
             mcmc = mcmc_iterations(P, wl, covfun, cp, ctx, args.mcmc_iters, 2, sync)
         except Exception as e:  # report, do not hide the throughput line
             log(f"mcmc iterations failed: {e}", rank)
+    if not args.no_rebuild_calls and info["sweep_engine"] == 1:
+        # the call after an accepted covariance proposal (new factor: r = B w
+        # rebuilt): the same calls on a context that rebuilds every call --
+        # after the kernel timing and the MCMC iterations (a second 3-chain
+        # context on the device left the live kernel timing ~95 us slower
+        # afterwards, not the throughput: profiles/r06_rebuild_timing_effect_*)
+        os.environ["NNGP_SWEEP_WARM"] = "0"
+        try:
+            ctxr = open_context(P, wl, covfun, cp, local_rank, C, seed=7 + rank)
+        finally:
+            os.environ.pop("NNGP_SWEEP_WARM", None)
+        el_rb, _ = timed(ctxr, args.steps, args.warmup, cold=True)
+        ctxr.close()
+        cold_calls["rebuild_calls"] = {"value": args.steps * C * world / el_rb, "unit": "sweeps/s",
+                                       "ms_per_step": el_rb * 1e3 / args.steps,
+                                       "how": "every call rebuilds w -> slots and r = B w (NNGP_SWEEP_WARM=0 "
+                                              "context): the call after an accepted covariance proposal"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log(f"cpu baseline (oracle, {C} threads)...", rank)
