@@ -31,6 +31,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -455,6 +456,8 @@ def main():
     ap.add_argument("--chains", type=int, default=3)
     ap.add_argument("--no-single-chain", action="store_true")
     ap.add_argument("--no-rebuild-calls", action="store_true", help="skip the rebuild-every-call measurement")
+    ap.add_argument("--sustained-s", type=float, default=5.0,
+                    help="seconds of back-to-back warm calls timed as one region (config.sustained; 0: skip)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -622,6 +625,15 @@ def main():
                     "algorithmic_bytes_per_launch": bytes_launch,
                     "sweeps_per_launch": ksw / launches,
                     "launches_per_sweep": launches / ksw}
+    sustained = None
+    if args.sustained_s > 0:
+        # the same warm calls back to back for a few seconds as one timed
+        # region: the rate with clocks and caches at steady state, and GPU
+        # work long enough for a sampling monitor beside the bench to see
+        ssteps = max(nc, int(math.ceil(args.sustained_s / (elapsed / args.steps) / nc)) * nc)
+        el_s, ctr = timed(ctx, ssteps, 0)
+        sustained = {"value": ssteps * C * world / el_s, "unit": "sweeps/s", "steps": ssteps,
+                     "seconds": el_s, "ms_per_step": el_s * 1e3 / ssteps}
     mcmc = None
     if args.mcmc_iters > 0:
         sync = (lambda: torch.cuda.synchronize(local_rank)) if torch.cuda.is_available() else (lambda: None)
@@ -678,6 +690,7 @@ def main():
                                    else "cold-call throughput"),
                       "single_chain": single,
                       "cold_calls": cold_calls,
+                      "sustained": sustained,
                       "parallelism": f"chains {C} per GPU x {world} GPUs (independent)"},
            "roofline": roofline, "cpu_baseline": cpu, "secondary": mcmc}
     if rank == 0:

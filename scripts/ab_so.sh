@@ -9,7 +9,7 @@ cp lib/libnngp.so lib/libnngp_cur.so
 for r in $(seq 1 $reps); do
   for v in "$@"; do
     cp lib/libnngp_$v.so lib/libnngp.so
-    timeout -k 10 300 python -u bench.py --no-cpu-baseline --mcmc-iters 0 --no-rebuild-calls $AB_ARGS > gpurun_out/ab_so_${v}_$r.json 2> gpurun_out/ab_so_${v}_$r.err || { tail -5 gpurun_out/ab_so_${v}_$r.err; cp lib/libnngp_cur.so lib/libnngp.so; exit 1; }
+    timeout -k 10 300 python -u bench.py --no-cpu-baseline --mcmc-iters 0 --sustained-s 0 --no-rebuild-calls $AB_ARGS > gpurun_out/ab_so_${v}_$r.json 2> gpurun_out/ab_so_${v}_$r.err || { tail -5 gpurun_out/ab_so_${v}_$r.err; cp lib/libnngp_cur.so lib/libnngp.so; exit 1; }
     python3 -c "
 import json; d=json.loads(open('gpurun_out/ab_so_${v}_$r.json').read().strip().splitlines()[-1]); c=d['config']
 print('rep $r $v', round(d['value']), 'single', round(c['single_chain']['value']) if c.get('single_chain') else None,

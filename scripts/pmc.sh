@@ -8,7 +8,7 @@ run() {  # $1 = tag, $2 = program kind, rest = counters
   if [ "$kind" = bench ]; then
     # warmup 10 + steps 10 = two calls of n_chromatic = 10 sweeps: every
     # dispatch of the tile kernel covers 10 sweeps
-    (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d $ROOTDIR/gpurun_out/pmc/$tag -o run -- python3 $ROOTDIR/bench.py --steps 10 --warmup 10 --no-cpu-baseline --no-kernel-timing --no-single-chain --mcmc-iters 0 --chains ${CHAINS:-3} > $ROOTDIR/gpurun_out/pmc/$tag.log 2>&1)
+    (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d $ROOTDIR/gpurun_out/pmc/$tag -o run -- python3 $ROOTDIR/bench.py --steps 10 --warmup 10 --no-cpu-baseline --no-kernel-timing --no-single-chain --mcmc-iters 0 --sustained-s 0 --chains ${CHAINS:-3} > $ROOTDIR/gpurun_out/pmc/$tag.log 2>&1)
   else
     (cd /tmp && timeout -k 10 120 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d $ROOTDIR/gpurun_out/pmc/$tag -o run -- $ROOTDIR/scripts/micro/calib > $ROOTDIR/gpurun_out/pmc/$tag.log 2>&1)
   fi

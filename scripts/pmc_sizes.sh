@@ -10,7 +10,7 @@ D=gpurun_out/pmcs; mkdir -p $D
 run() {  # $1 tag, $2 bench|calib, rest counters
   tag=$1; kind=$2; shift 2
   if [ "$kind" = bench ]; then
-    (cd /tmp && timeout -s KILL 150 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d $ROOTDIR/$D/$tag -o run -- python3 $ROOTDIR/bench.py --steps 10 --warmup 10 --no-cpu-baseline --no-kernel-timing --no-single-chain --no-rebuild-calls --mcmc-iters 0 --chains ${CHAINS:-3} > $ROOTDIR/$D/$tag.log 2>&1)
+    (cd /tmp && timeout -s KILL 150 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d $ROOTDIR/$D/$tag -o run -- python3 $ROOTDIR/bench.py --steps 10 --warmup 10 --no-cpu-baseline --no-kernel-timing --no-single-chain --no-rebuild-calls --mcmc-iters 0 --sustained-s 0 --chains ${CHAINS:-3} > $ROOTDIR/$D/$tag.log 2>&1)
   else
     (cd /tmp && timeout -s KILL 90 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d $ROOTDIR/$D/$tag -o run -- $ROOTDIR/scripts/micro/calib > $ROOTDIR/$D/$tag.log 2>&1)
   fi

@@ -16,7 +16,7 @@ run() {  # $1 tag, rest counters
   tag=$1; shift
   [ -z "$*" ] && { echo "$tag: no counters"; return 0; }
   echo "$tag: $*"
-  (cd /tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $* --output-format csv -d $ROOTDIR/gpurun_out/pmc6/$tag -o run -- python3 $ROOTDIR/bench.py --steps 10 --warmup 10 --no-cpu-baseline --no-kernel-timing --no-single-chain --no-rebuild-calls --mcmc-iters 0 > $ROOTDIR/gpurun_out/pmc6/$tag.log 2>&1)
+  (cd /tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $* --output-format csv -d $ROOTDIR/gpurun_out/pmc6/$tag -o run -- python3 $ROOTDIR/bench.py --steps 10 --warmup 10 --no-cpu-baseline --no-kernel-timing --no-single-chain --no-rebuild-calls --mcmc-iters 0 --sustained-s 0 > $ROOTDIR/gpurun_out/pmc6/$tag.log 2>&1)
   echo "$tag rc=$?"
 }
 run req $(pick TCC_BUBBLE TCC_EA0_RDREQ_32B TCC_EA0_RDREQ) && \

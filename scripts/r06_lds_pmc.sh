@@ -6,7 +6,7 @@ ROOTDIR=$(pwd)
 run() {  # $1 tag, rest counters
   tag=$1; shift
   echo "$tag: $*"
-  (cd /tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $* --output-format csv -d $ROOTDIR/gpurun_out/pmcl/$tag -o run -- python3 $ROOTDIR/bench.py --steps 10 --warmup 10 --no-cpu-baseline --no-kernel-timing --no-single-chain --no-rebuild-calls --mcmc-iters 0 > $ROOTDIR/gpurun_out/pmcl/$tag.log 2>&1)
+  (cd /tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $* --output-format csv -d $ROOTDIR/gpurun_out/pmcl/$tag -o run -- python3 $ROOTDIR/bench.py --steps 10 --warmup 10 --no-cpu-baseline --no-kernel-timing --no-single-chain --no-rebuild-calls --mcmc-iters 0 --sustained-s 0 > $ROOTDIR/gpurun_out/pmcl/$tag.log 2>&1)
   echo "$tag rc=$?"
 }
 run l1 SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_INSTS_LDS_LOAD SQ_INSTS_LDS_LOAD_BANDWIDTH SQ_WAIT_INST_LDS SQ_LDS_DATA_FIFO_FULL && \
