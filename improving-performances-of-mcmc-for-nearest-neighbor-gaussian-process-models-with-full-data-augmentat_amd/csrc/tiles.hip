@@ -225,7 +225,15 @@ __device__ __forceinline__ void tile_load_cells(const TileDev& D, const int4 B, 
 #pragma unroll
       for (int ch = 0; ch < C; ++ch) b.v[j][ch] = __builtin_nontemporal_load(D.cell_val + ch * D.n_cells + e);
     } else {
-      b.pk[j] = 0u;  // padding (device encoding, tile_lr)
+      // padding (device encoding, tile_lr); where the products run whole
+      // groups of cells (tile_products: wave-local batches) with a
+      // zero value, so that a cell past R is a no-op there (the tile's last
+      // row times 0)
+      b.pk[j] = 0u;
+      if constexpr (NT == 64) {
+#pragma unroll
+        for (int ch = 0; ch < C; ++ch) b.v[j][ch] = 0.0;
+      }
     }
   }
 }
@@ -396,6 +404,56 @@ __device__ __forceinline__ void seg_scan_step(double (&v)[C], int& f) {
 // holds no cells, passes exactly as many per batch (tile_phase_xw); a barrier
 // added or removed here must change this count.
 constexpr int kOwnDrawBarriers = 3;
+// the products of one own batch: running sums over a thread's cells,
+// restarted at slot starts (run * keep + p, keep in {0, 1}: see
+// seg_scan_step), every slot end stored into acc_s; cont_q = the slot this
+// thread continues from earlier threads (completed after the scan).  The r
+// reads of a group of GRP cells go out together, before any of its
+// arithmetic: one LDS round trip per group instead of one or two per cell
+// (the per-cell `j < R` blocks kept each cell's reads behind the previous
+// cell's).  Cells past R are padding with a zero value (tile_load_cells), so
+// the last group runs whole; padding reads the tile's last row.  Wave-local
+// batches only (tile_own_wl); tile_own_draw keeps its cell-by-cell loop (the
+// group's registers spill its 2-chain instantiation)
+template <int C, int RMAX, int GRP, class TB>
+__device__ __forceinline__ void tile_products(const TB& b, int R, const double* __restrict__ r_s,
+                                              double* __restrict__ acc_s, uint32_t lrmax, double (&run)[C],
+                                              int& cont_q, bool& seen_start) {
+#pragma unroll
+  for (int ch = 0; ch < C; ++ch) run[ch] = 0.0;
+#pragma unroll
+  for (int j0 = 0; j0 < RMAX; j0 += GRP) {
+    if (j0 >= R) break;
+    double rv[GRP][C];
+#pragma unroll
+    for (int jj = 0; jj < GRP; ++jj) {
+      if (j0 + jj < RMAX) {
+        const uint32_t lr = min(tile_lr(b.pk[j0 + jj]), lrmax);
+#pragma unroll
+        for (int ch = 0; ch < C; ++ch) rv[jj][ch] = r_s[lr * C + ch];
+      }
+    }
+#pragma unroll
+    for (int jj = 0; jj < GRP; ++jj) {
+      const int j = j0 + jj;
+      if (j < RMAX) {
+        const uint32_t pk = b.pk[j];
+        const bool st = (pk & kTStart) != 0;
+        const double keep = st ? 0.0 : 1.0;
+#pragma unroll
+        for (int ch = 0; ch < C; ++ch) run[ch] = __builtin_fma(run[ch], keep, b.v[j][ch] * rv[jj][ch]);
+        const int q = (int)((pk >> kTileQShift) & kTileQMask);
+        if (pk & kTEnd) {
+#pragma unroll
+          for (int ch = 0; ch < C; ++ch) acc_s[q * C + ch] = run[ch];
+        }
+        seen_start |= st;  // (before the end test: a slot may start and end at this cell)
+        cont_q = ((pk & kTEnd) && !seen_start && cont_q < 0) ? q : cont_q;
+      }
+    }
+  }
+}
+
 template <int C, int NT, int RMAX, int PROBE, int SH, int CS = C>
 __device__ __forceinline__ void tile_own_draw(const TileDev& D, const TileLaunch& a, const TileShard& sh, TileState& S,
                                               TileBatchRegs<C, NT, RMAX>& b, unsigned epoch) {
@@ -859,26 +917,7 @@ __device__ __forceinline__ void tile_own_wl(const TileDev& D, const TileLaunch& 
   double run[C];
   int cont_q = -1;
   bool seen_start = false;
-#pragma unroll
-  for (int ch = 0; ch < C; ++ch) run[ch] = 0.0;
-#pragma unroll
-  for (int j = 0; j < RMAX; ++j) {
-    if (j < R) {
-      const uint32_t pk = b.pk[j];
-      const uint32_t lr = min(tile_lr(pk), S.lrmax);
-      const bool st = (pk & kTStart) != 0;
-      const double keep = st ? 0.0 : 1.0;
-#pragma unroll
-      for (int ch = 0; ch < C; ++ch) run[ch] = __builtin_fma(run[ch], keep, b.v[j][ch] * r_s[lr * C + ch]);
-      const int q = (int)((pk >> kTileQShift) & kTileQMask);
-      if (pk & kTEnd) {
-#pragma unroll
-        for (int ch = 0; ch < C; ++ch) acc_s[q * C + ch] = run[ch];
-      }
-      seen_start |= st;  // (before the end test: a slot may start and end at this cell)
-      cont_q = ((pk & kTEnd) && !seen_start && cont_q < 0) ? q : cont_q;
-    }
-  }
+  tile_products<C, RMAX, 4>(b, R, r_s, acc_s, S.lrmax, run, cont_q, seen_start);
   // segmented inclusive scan of the lane tails inside the wave (as
   // tile_own_draw's); lane 0 holds the first cell of the wave's first slot,
   // so nothing is carried in from another wave
